@@ -1,0 +1,102 @@
+/*
+ * sbft_gpuverify.h — C ABI of libsbft_gpuverify.so, the MI355X signature-verification
+ * engine behind SmartBFT's api.Verifier plugin.
+ *
+ * Drop-in boundary. The reference's plugin interface is Go:
+ *   pkg/api/dependencies.go:54-71   type Verifier interface { VerifyProposal, VerifyRequest,
+ *                                   VerifyConsenterSig, VerifySignature, VerificationSequence,
+ *                                   RequestsFromProposal, AuxiliaryData }
+ * and the library calls it at internal/bft/view.go:555 (VerifyProposal), view.go:631 and
+ * view.go:834 (VerifyConsenterSig), viewchanger.go:718 and controller.go:239. Every in-tree
+ * implementation is an accept-all stub (test/test_app.go:206-253,
+ * examples/naive_chain/node.go:64-100); the arithmetic a real plugin runs is Go 1.24.1
+ * crypto/ecdsa.Verify (P-256) + crypto/sha256. This header is what a cgo shim binds to
+ * replace that arithmetic with one GPU launch per proposal / per quorum (binding in
+ * INTEGRATION.md; the plugin-level mirror is include/sbft_verifier.h).
+ *
+ * Conventions
+ *  - Every 256-bit field is 32 bytes big-endian (Go big.Int.FillBytes(make([]byte,32))).
+ *  - Batches are structure-of-arrays: field i of tuple k is at ptr + 32*k.
+ *  - digest is the hash already normalised as Go's hashToNat consumes it: the first 32
+ *    bytes of a hash of >= 32 bytes, a shorter hash left-padded with zeros
+ *    (sbft_gv_normalize_hash). r/s/x/y wider than 32 bytes or negative are rejected by
+ *    the caller before the call (sbft_gv_normalize_scalar returns 0 for them).
+ *  - Verdicts: ok_out[k] = 1 accept, 0 reject — bit-exact with crypto/ecdsa.Verify,
+ *    including r/s out of [1, n-1], Q off-curve or non-canonical, R = infinity.
+ *  - Return value: 0 on success, negative SBFT_GV_E* on an infrastructure failure
+ *    (distinct from a 0 verdict). Host-pointer calls are synchronous; the caller owns all
+ *    buffers. A context is thread-safe (calls are serialised per device).
+ *  - *_dev entry points take device pointers already resident in HBM on `device` and a
+ *    hipStream_t (as void*); they enqueue and return without synchronising.
+ */
+#ifndef SBFT_GPUVERIFY_H
+#define SBFT_GPUVERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBFT_GV_OK 0
+#define SBFT_GV_EINVAL (-1)     /* bad argument */
+#define SBFT_GV_ENODEV (-2)     /* no usable GPU / device mask selects none */
+#define SBFT_GV_ENOMEM (-3)     /* device or pinned allocation failed */
+#define SBFT_GV_ELAUNCH (-4)    /* kernel launch failed */
+#define SBFT_GV_EDEVICE (-5)    /* HIP runtime error during copy/sync */
+
+typedef struct sbft_gv_ctx sbft_gv_ctx;
+
+typedef struct sbft_gv_opts {
+    uint32_t device_mask;   /* bit d selects HIP device d; 0 = all visible devices */
+    uint32_t min_split;     /* batches smaller than this stay on one device (0 = default 65536) */
+    uint64_t reserved[4];
+} sbft_gv_opts;
+
+/* Create a context (per-device stream + device/pinned staging grown on demand).
+ * opts may be NULL. Replaces: the plugin construction a Go app does before handing its
+ * Verifier to consensus.Consensus.Verifier (pkg/consensus/consensus.go:36). */
+int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out);
+void sbft_gv_destroy(sbft_gv_ctx* ctx);
+int sbft_gv_device_count(const sbft_gv_ctx* ctx);
+const char* sbft_gv_strerror(int code);
+
+/* Batched P-256 ECDSA verify, host buffers, synchronous. Split over the context's devices
+ * for n >= min_split. Replaces n calls of crypto/ecdsa.Verify made by a Verifier inside
+ * VerifyProposal (view.go:555) / VerifyConsenterSig (view.go:631, :834). */
+int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* r, const uint8_t* s,
+                        const uint8_t* qx, const uint8_t* qy, size_t n, uint8_t* ok_out);
+
+/* Batched SHA-256 over variable-length messages: message k = blob[off[k] .. off[k]+len[k]).
+ * Replaces crypto/sha256.Sum256 per request payload. */
+int sbft_gv_sha256(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, const uint64_t* off,
+                   const uint32_t* len, size_t n, uint8_t* dig_out);
+
+/* Fused: digest_k = SHA-256(message k) stays on the GPU and feeds the verify of tuple k.
+ * dig_out may be NULL. */
+int sbft_gv_sha256_verify_p256(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len,
+                               const uint64_t* off, const uint32_t* len, const uint8_t* r,
+                               const uint8_t* s, const uint8_t* qx, const uint8_t* qy, size_t n,
+                               uint8_t* ok_out, uint8_t* dig_out);
+
+/* Device-resident variants (inputs already in HBM on `device`; stream = hipStream_t). */
+int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, const void* d_r,
+                            const void* d_s, const void* d_qx, const void* d_qy, size_t n,
+                            void* d_ok, void* stream);
+int sbft_gv_sha256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob, const void* d_off,
+                       const void* d_len, size_t n, void* d_dig, void* stream);
+int sbft_gv_sha256_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob,
+                                   const void* d_off, const void* d_len, const void* d_r,
+                                   const void* d_s, const void* d_qx, const void* d_qy, size_t n,
+                                   void* d_ok, void* d_dig, void* stream);
+
+/* Go-semantics host helpers (no GPU). */
+void sbft_gv_normalize_hash(const uint8_t* hash, size_t len, uint8_t out32[32]);
+/* Big-endian magnitude of arbitrary length -> 32 bytes; returns 0 if it needs > 256 bits. */
+int sbft_gv_normalize_scalar(const uint8_t* be, size_t len, uint8_t out32[32]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

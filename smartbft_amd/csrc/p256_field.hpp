@@ -1,0 +1,358 @@
+// p256_field.hpp — P-256 field (mod p) and scalar (mod n) arithmetic for gfx950.
+//
+// Representation: 8 x 32-bit limbs, little-endian, one field element per lane
+// (VALU integer work; MFMA is deliberately not used — see DESIGN.md). Measured on
+// MI355X: v_mad_u64_u32 issues at ~34 T lane-ops/s, ~87% of the plain integer
+// VALU rate (tools/valu_peak.hip), so the design goal is the fewest VALU
+// instructions per product, not the fewest multiplies.
+//
+// Mod p: Montgomery form (R = 2^256) with the sparse reduction that P-256 allows:
+// -p^-1 = 1 (mod 2^32), so the reduction multiplier of each word IS the word, and
+// m*p = m*2^256 - m*2^224 + m*2^192 + m*2^96 - m becomes four 32-bit adds per
+// column instead of eight products. Values are kept lazily reduced in [0, 2^256);
+// fp_canon() maps to [0, p) where an exact comparison is needed.
+//
+// Mod n: generic product-scanning Montgomery (n has no special form).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sbft {
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+struct fe {
+    u32 v[8];
+};
+
+#define SBFT_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- primitives
+// acc += a*b with the 64-bit carry-out added into c2 (v_mad_u64_u32 carry-out
+// lands in an SGPR lane mask, v_addc folds it back into a VGPR).
+SBFT_DEV void madc(u64& acc, u32& c2, u32 a, u32 b) {
+    u64 cc;
+    asm(
+        "v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
+        "v_addc_co_u32 %2, vcc, 0, %2, %1"
+        : "+v"(acc), "=&s"(cc), "+v"(c2)
+        : "v"(a), "v"(b)
+        : "vcc");
+}
+// acc + x (x zero-extended), one instruction
+SBFT_DEV u64 mad1(u32 x, u64 acc) {
+    u64 r, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(r), "=s"(cc) : "v"(x), "v"(acc));
+    return r;
+}
+// acc + x (x sign-extended), one instruction
+SBFT_DEV u64 madi1(u32 x, u64 acc) {
+    u64 r, cc;
+    asm("v_mad_i64_i32 %0, %1, %2, 1, %3" : "=v"(r), "=s"(cc) : "v"(x), "v"(acc));
+    return r;
+}
+// zero-extend to a 64-bit register pair, one instruction
+SBFT_DEV u64 z64(u32 x) {
+    u64 r, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, 1, 0" : "=v"(r), "=s"(cc) : "v"(x));
+    return r;
+}
+SBFT_DEV u32 lo32(u64 x) { return (u32)x; }
+SBFT_DEV u32 hi32(u64 x) { return (u32)(x >> 32); }
+
+// 256 x 256 -> 512 product, product scanning (Comba) with a 96-bit column accumulator.
+SBFT_DEV void mul512(u32 t[16], const fe& a, const fe& b) {
+    u64 acc = 0;
+    u32 c2 = 0;
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+        bool first = true;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = k - i;
+            if (j < 0 || j > 7) continue;
+            if (first) {
+                acc += (u64)a.v[i] * b.v[j];  // acc < 2^40 here: cannot overflow
+                first = false;
+            } else {
+                madc(acc, c2, a.v[i], b.v[j]);
+            }
+        }
+        t[k] = lo32(acc);
+        acc = (acc >> 32) | ((u64)c2 << 32);
+        c2 = 0;
+    }
+    t[15] = lo32(acc);
+}
+
+// Squaring: off-diagonal triangle once, doubled, plus the diagonal.
+SBFT_DEV void sqr512(u32 t[16], const fe& a) {
+    u32 x[16];
+    u64 acc = 0;
+    u32 c2 = 0;
+    x[0] = 0;
+#pragma unroll
+    for (int k = 1; k < 14; ++k) {
+        bool first = true;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = k - i;
+            if (j <= i || j > 7) continue;
+            if (first) {
+                acc += (u64)a.v[i] * a.v[j];
+                first = false;
+            } else {
+                madc(acc, c2, a.v[i], a.v[j]);
+            }
+        }
+        x[k] = lo32(acc);
+        acc = (acc >> 32) | ((u64)c2 << 32);
+        c2 = 0;
+    }
+    x[14] = lo32(acc);
+    x[15] = hi32(acc);
+    // t = 2*x + diag, one carry chain over 16 words
+    u64 c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u64 d = (u64)a.v[k] * a.v[k];
+        u64 s0 = (u64)x[2 * k] * 2 + lo32(d) + c;          // < 2^34
+        t[2 * k] = lo32(s0);
+        u64 s1 = (u64)x[2 * k + 1] * 2 + hi32(d) + hi32(s0);
+        t[2 * k + 1] = lo32(s1);
+        c = hi32(s1);
+    }
+}
+
+// ------------------------------------------------------------------ mod p
+__device__ __constant__ static const u32 P256_P[8] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0,
+                                                      0,           0,           1,           0xffffffffu};
+
+// Montgomery reduction t * 2^-256 mod p, t < 2^512 -> [0, 2^256).
+// Column k of t + sum_i m_i * p * 2^(32 i) receives +m_{k-3} +m_{k-6} -m_{k-7} +m_{k-8}
+// (the -m_k term zeroes the low word and is implicit); m_k = column k for k < 8.
+SBFT_DEV void fp_redc(fe& r, const u32 t[16]) {
+    const u32 m0 = t[0], m1 = t[1], m2 = t[2];
+    u64 c;
+    c = mad1(m0, z64(t[3]));
+    const u32 m3 = lo32(c);
+    c = madi1(hi32(c), mad1(m1, z64(t[4])));
+    const u32 m4 = lo32(c);
+    c = madi1(hi32(c), mad1(m2, z64(t[5])));
+    const u32 m5 = lo32(c);
+    c = madi1(hi32(c), mad1(m0, mad1(m3, z64(t[6]))));
+    const u32 m6 = lo32(c);
+    c = madi1(hi32(c), mad1(m1, mad1(m4, z64(t[7])))) - m0;
+    const u32 m7 = lo32(c);
+    u32 o[8];
+    c = madi1(hi32(c), mad1(m0, mad1(m2, mad1(m5, z64(t[8]))))) - m1;
+    o[0] = lo32(c);
+    c = madi1(hi32(c), mad1(m1, mad1(m3, mad1(m6, z64(t[9]))))) - m2;
+    o[1] = lo32(c);
+    c = madi1(hi32(c), mad1(m2, mad1(m4, mad1(m7, z64(t[10]))))) - m3;
+    o[2] = lo32(c);
+    c = madi1(hi32(c), mad1(m3, mad1(m5, z64(t[11])))) - m4;
+    o[3] = lo32(c);
+    c = madi1(hi32(c), mad1(m4, mad1(m6, z64(t[12])))) - m5;
+    o[4] = lo32(c);
+    c = madi1(hi32(c), mad1(m5, mad1(m7, z64(t[13])))) - m6;
+    o[5] = lo32(c);
+    c = madi1(hi32(c), mad1(m6, z64(t[14]))) - m7;
+    o[6] = lo32(c);
+    c = madi1(hi32(c), mad1(m7, z64(t[15])));
+    o[7] = lo32(c);
+    // value = o + top*2^256 < 2^256 + p; subtract top*p (masked constant p).
+    const u32 top = hi32(c);
+    const u32 mask = 0u - top;
+    const u32 pm[8] = {mask, mask, mask, 0, 0, 0, top, mask};
+    u64 b = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u64 d = (u64)o[k] - pm[k] - b;
+        r.v[k] = lo32(d);
+        b = d >> 63;
+    }
+}
+
+SBFT_DEV void fp_mul(fe& r, const fe& a, const fe& b) {
+    u32 t[16];
+    mul512(t, a, b);
+    fp_redc(r, t);
+}
+SBFT_DEV void fp_sqr(fe& r, const fe& a) {
+    u32 t[16];
+    sqr512(t, a);
+    fp_redc(r, t);
+}
+
+// r = a + (mask ? k : 0) over 8 limbs; returns the carry-out.
+SBFT_DEV u32 add_masked_p(fe& r, const fe& a, u32 mask) {
+    const u32 top = mask & 1u;
+    const u32 pm[8] = {mask, mask, mask, 0, 0, 0, top, mask};
+    u64 c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        c = (u64)a.v[k] + pm[k] + c;
+        r.v[k] = lo32(c);
+        c >>= 32;
+    }
+    return (u32)c;
+}
+SBFT_DEV u32 sub_masked_p(fe& r, const fe& a, u32 mask) {
+    const u32 top = mask & 1u;
+    const u32 pm[8] = {mask, mask, mask, 0, 0, 0, top, mask};
+    u64 b = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u64 d = (u64)a.v[k] - pm[k] - b;
+        r.v[k] = lo32(d);
+        b = d >> 63;
+    }
+    return (u32)b;
+}
+
+// a + b mod p, inputs and output in [0, 2^256).
+SBFT_DEV void fp_add(fe& r, const fe& a, const fe& b) {
+    u64 c = 0;
+    fe s;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        c = (u64)a.v[k] + b.v[k] + c;
+        s.v[k] = lo32(c);
+        c >>= 32;
+    }
+    const u32 carry = (u32)c;
+    const u32 borrow = sub_masked_p(r, s, 0u - carry);
+    // carry and no borrow: the value was >= 2^256 + p; subtract p once more (rare).
+    const u32 again = carry & (borrow ^ 1u);
+    if (__builtin_expect(__any(again), 0)) {
+        // r + (2^256 - p) == r - p (mod 2^256) for the lanes that need it
+        fe t;
+        sub_masked_p(t, r, 0u - again);
+        r = t;
+    }
+}
+// a - b mod p, inputs and output in [0, 2^256).
+SBFT_DEV void fp_sub(fe& r, const fe& a, const fe& b) {
+    u64 bw = 0;
+    fe d;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u64 x = (u64)a.v[k] - b.v[k] - bw;
+        d.v[k] = lo32(x);
+        bw = x >> 63;
+    }
+    const u32 borrow = (u32)bw;
+    const u32 carry = add_masked_p(r, d, 0u - borrow);
+    // borrow and no carry: a - b + p is still negative (b >= p); add p again (rare).
+    const u32 again = borrow & (carry ^ 1u);
+    if (__builtin_expect(__any(again), 0)) {
+        fe t;
+        add_masked_p(t, r, 0u - again);
+        r = t;
+    }
+}
+// [0, 2^256) -> [0, p)
+SBFT_DEV void fp_canon(fe& r, const fe& a) {
+    fe t;
+    const u32 borrow = sub_masked_p(t, a, 0xffffffffu);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.v[k] = borrow ? a.v[k] : t.v[k];
+}
+SBFT_DEV bool fe_is_zero_raw(const fe& a) {
+    u32 o = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o |= a.v[k];
+    return o == 0;
+}
+// a == 0 (mod p) for a lazily reduced value: a == 0 or a == p.
+SBFT_DEV bool fp_is_zero(const fe& a) {
+    u32 z = 0, q = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        z |= a.v[k];
+        q |= a.v[k] ^ ((k < 3 || k == 7) ? 0xffffffffu : (k == 6 ? 1u : 0u));
+    }
+    return z == 0 || q == 0;
+}
+SBFT_DEV bool fe_eq(const fe& a, const fe& b) {
+    u32 d = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d |= a.v[k] ^ b.v[k];
+    return d == 0;
+}
+// a < m for 8-limb values
+SBFT_DEV bool fe_lt(const fe& a, const u32* m) {
+    u64 b = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u64 d = (u64)a.v[k] - m[k] - b;
+        b = d >> 63;
+    }
+    return b != 0;
+}
+
+// ------------------------------------------------------------------ mod n
+__device__ __constant__ static const u32 P256_N[8] = {0xfc632551u, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
+                                                      0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu};
+#define P256_N_PRIME 0xee00bc4fu /* -n^-1 mod 2^32 */
+
+// Montgomery product mod n (R = 2^256), product scanning with interleaved m*n.
+// Inputs < 2^256, output in [0, 2^256) (congruent, conditionally reduced once).
+SBFT_DEV void fn_mul(fe& r, const fe& a, const fe& b) {
+    u32 m[8];
+    u32 o[8];
+    u64 acc = 0;
+    u32 c2 = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = k - i;
+            if (j < 0 || j > 7) continue;
+            madc(acc, c2, a.v[i], b.v[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = k - i;
+            if (i >= k || j < 0 || j > 7) continue;
+            madc(acc, c2, m[i], P256_N[j]);
+        }
+        if (k < 8) {
+            m[k] = lo32(acc) * P256_N_PRIME;
+            madc(acc, c2, m[k], P256_N[0]);  // low word becomes 0
+        } else {
+            o[k - 8] = lo32(acc);
+        }
+        if (k < 15) {
+            acc = (acc >> 32) | ((u64)c2 << 32);
+            c2 = 0;
+        }
+    }
+    // value = o + hi*2^256 (hi in {0,1}); subtract n once if hi.
+    const u32 top = hi32(acc);
+    const u32 mask = 0u - top;
+    u64 bw = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u64 d = (u64)o[k] - (P256_N[k] & mask) - bw;
+        r.v[k] = lo32(d);
+        bw = d >> 63;
+    }
+}
+// [0, 2^256) -> [0, n)
+SBFT_DEV void fn_canon(fe& r, const fe& a) {
+    fe t;
+    u64 bw = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u64 d = (u64)a.v[k] - P256_N[k] - bw;
+        t.v[k] = lo32(d);
+        bw = d >> 63;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.v[k] = bw ? a.v[k] : t.v[k];
+}
+
+}  // namespace sbft

@@ -1,0 +1,16 @@
+// sbft_kernels.h — internal launcher declarations shared by the HIP kernels and the
+// host runtime (gpuverify.cpp). Not part of the public C ABI (include/sbft_gpuverify.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+extern "C" {
+// P-256 verify of n SoA tuples (32-byte big-endian fields) -> n verdict bytes.
+int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
+                            const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok, uint32_t n,
+                            hipStream_t stream);
+// SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable >= 68 bytes
+// past its last message (funnel over-read). Digests are 32-byte big-endian.
+int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
+                       uint8_t* d_dig, uint32_t n, hipStream_t stream);
+}

@@ -1,0 +1,185 @@
+"""ctypes binding of libsbft_gpuverify.so (include/sbft_gpuverify.h).
+
+This is the product path used by tests and bench.py: every call goes through the C ABI
+into the HIP kernels. There is no CPU fallback: if the shared library is missing or no
+GPU is visible, construction raises (GpuVerifyError), loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsbft_gpuverify.so")
+
+EXPORTS = [
+    "sbft_gv_init", "sbft_gv_destroy", "sbft_gv_device_count", "sbft_gv_strerror",
+    "sbft_gv_verify_p256", "sbft_gv_sha256", "sbft_gv_sha256_verify_p256",
+    "sbft_gv_verify_p256_dev", "sbft_gv_sha256_dev", "sbft_gv_sha256_verify_p256_dev",
+    "sbft_gv_normalize_hash", "sbft_gv_normalize_scalar",
+]
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+
+
+class GpuVerifyError(RuntimeError):
+    pass
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("device_mask", ctypes.c_uint32), ("min_split", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint64 * 4)]
+
+
+_LIB = None
+
+
+def load_library():
+    """Load the HIP shared library (raises if it was not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise GpuVerifyError(f"{LIB_PATH} missing: run `make -C smartbft_amd/csrc` "
+                             "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    L.sbft_gv_init.argtypes = [ctypes.POINTER(Opts), ctypes.POINTER(_vp)]
+    L.sbft_gv_destroy.argtypes = [_vp]
+    L.sbft_gv_destroy.restype = None
+    L.sbft_gv_device_count.argtypes = [_vp]
+    L.sbft_gv_strerror.argtypes = [ctypes.c_int]
+    L.sbft_gv_strerror.restype = ctypes.c_char_p
+    L.sbft_gv_verify_p256.argtypes = [_vp] + [_u8p] * 5 + [ctypes.c_size_t, _u8p]
+    L.sbft_gv_sha256.argtypes = [_vp, _u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, _u8p]
+    L.sbft_gv_sha256_verify_p256.argtypes = [_vp, _u8p, ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_uint64),
+                                             ctypes.POINTER(ctypes.c_uint32)] + [_u8p] * 4 + \
+                                            [ctypes.c_size_t, _u8p, _u8p]
+    L.sbft_gv_verify_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 5 + [ctypes.c_size_t, _vp, _vp]
+    L.sbft_gv_sha256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 3 + [ctypes.c_size_t, _vp, _vp]
+    L.sbft_gv_sha256_verify_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 7 + \
+                                                [ctypes.c_size_t, _vp, _vp, _vp]
+    L.sbft_gv_normalize_hash.argtypes = [_u8p, ctypes.c_size_t, _u8p]
+    L.sbft_gv_normalize_hash.restype = None
+    L.sbft_gv_normalize_scalar.argtypes = [_u8p, ctypes.c_size_t, _u8p]
+    _LIB = L
+    return L
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(_u8p)
+
+
+def _soa(a, n: int) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.uint8))
+    if a.shape != (n, 32):
+        raise ValueError(f"expected ({n}, 32) uint8, got {a.shape}")
+    return a
+
+
+def normalize_hash(h: bytes) -> bytes:
+    L = load_library()
+    out = (ctypes.c_uint8 * 32)()
+    buf = (ctypes.c_uint8 * max(1, len(h))).from_buffer_copy(h or b"\0")
+    L.sbft_gv_normalize_hash(buf, len(h), out)
+    return bytes(out)
+
+
+def normalize_scalar(be: bytes) -> bytes | None:
+    L = load_library()
+    out = (ctypes.c_uint8 * 32)()
+    buf = (ctypes.c_uint8 * max(1, len(be))).from_buffer_copy(be or b"\0")
+    return bytes(out) if L.sbft_gv_normalize_scalar(buf, len(be), out) else None
+
+
+class GpuVerifier:
+    """One sbft_gv_ctx. Host-array calls are synchronous; *_dev calls take torch tensors
+    (device-resident) and enqueue on the given (or current) stream."""
+
+    def __init__(self, device_mask: int = 0, min_split: int = 0):
+        self.L = load_library()
+        ctx = _vp()
+        opts = Opts(device_mask, min_split)
+        rc = self.L.sbft_gv_init(ctypes.byref(opts), ctypes.byref(ctx))
+        if rc:
+            raise GpuVerifyError(f"sbft_gv_init: {self.L.sbft_gv_strerror(rc).decode()} ({rc})")
+        self.ctx = ctx
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.L.sbft_gv_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc:
+            raise GpuVerifyError(f"{what}: {self.L.sbft_gv_strerror(rc).decode()} ({rc})")
+
+    @property
+    def device_count(self) -> int:
+        return self.L.sbft_gv_device_count(self.ctx)
+
+    def verify(self, digest, r, s, qx, qy) -> np.ndarray:
+        n = len(digest)
+        arrs = [_soa(a, n) for a in (digest, r, s, qx, qy)]
+        ok = np.zeros(n, dtype=np.uint8)
+        self._check(self.L.sbft_gv_verify_p256(self.ctx, *[_p(a) for a in arrs], n, _p(ok)),
+                    "sbft_gv_verify_p256")
+        return ok
+
+    def sha256(self, blob: np.ndarray, off: np.ndarray, ln: np.ndarray) -> np.ndarray:
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(ln, dtype=np.uint32)
+        n = off.shape[0]
+        dig = np.zeros((n, 32), dtype=np.uint8)
+        self._check(self.L.sbft_gv_sha256(self.ctx, _p(blob) if blob.size else None, blob.size,
+                                          off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                          ln.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n,
+                                          _p(dig)), "sbft_gv_sha256")
+        return dig
+
+    def sha256_verify(self, blob, off, ln, r, s, qx, qy, want_digests=False):
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(ln, dtype=np.uint32)
+        n = off.shape[0]
+        arrs = [_soa(a, n) for a in (r, s, qx, qy)]
+        ok = np.zeros(n, dtype=np.uint8)
+        dig = np.zeros((n, 32), dtype=np.uint8) if want_digests else None
+        self._check(self.L.sbft_gv_sha256_verify_p256(
+            self.ctx, _p(blob) if blob.size else None, blob.size,
+            off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+            ln.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), *[_p(a) for a in arrs], n, _p(ok),
+            _p(dig) if dig is not None else None), "sbft_gv_sha256_verify_p256")
+        return (ok, dig) if want_digests else ok
+
+    # ---- device-resident (torch tensors on a HIP device) ----
+    @staticmethod
+    def _stream(stream):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def verify_dev(self, d_digest, d_r, d_s, d_qx, d_qy, d_ok, stream=None):
+        n = d_ok.numel()
+        dev = d_ok.device.index
+        self._check(self.L.sbft_gv_verify_p256_dev(
+            self.ctx, dev, d_digest.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), d_qx.data_ptr(),
+            d_qy.data_ptr(), n, d_ok.data_ptr(), self._stream(stream)), "sbft_gv_verify_p256_dev")
+
+    def sha256_dev(self, d_blob, d_off, d_len, d_dig, stream=None):
+        n = d_off.numel()
+        self._check(self.L.sbft_gv_sha256_dev(self.ctx, d_dig.device.index, d_blob.data_ptr(),
+                                              d_off.data_ptr(), d_len.data_ptr(), n,
+                                              d_dig.data_ptr(), self._stream(stream)),
+                    "sbft_gv_sha256_dev")

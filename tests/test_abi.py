@@ -1,0 +1,58 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/*.h declares, and
+its host-only helpers follow Go semantics. No compute call is made without a GPU."""
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        syms |= set(re.findall(r"\b(sbft_\w+)\s*\(", text))
+    return syms
+
+
+def test_library_exports_every_declared_symbol():
+    from smartbft_amd import gpuverify
+    lib = gpuverify.load_library()
+    syms = _declared_symbols()
+    assert len(syms) >= len(gpuverify.EXPORTS)
+    missing = [s for s in sorted(syms) if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header():
+    from smartbft_amd import gpuverify
+    hdr = set()
+    text = open(os.path.join(ROOT, "include", "sbft_gpuverify.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    hdr |= set(re.findall(r"\b(sbft_gv_\w+)\s*\(", text))
+    assert hdr == set(gpuverify.EXPORTS)
+
+
+def test_normalize_helpers_go_semantics():
+    from smartbft_amd import gpuverify
+    import oracle
+    for h in [b"", b"\x05", bytes(range(20)), bytes(range(32)), bytes(range(48)), bytes(range(64))]:
+        assert gpuverify.normalize_hash(h) == oracle.normalize_hash(h)
+    assert gpuverify.normalize_scalar(b"\x01\x02") == b"\0" * 30 + b"\x01\x02"
+    assert gpuverify.normalize_scalar(b"\0" * 5 + b"\xff" * 32) == b"\xff" * 32
+    assert gpuverify.normalize_scalar(b"\x01" + b"\0" * 32) is None  # 257 bits: reject
+
+
+def test_strerror_and_no_gpu_failure_is_loud():
+    from smartbft_amd import gpuverify
+    lib = gpuverify.load_library()
+    assert lib.sbft_gv_strerror(-2) == b"no usable GPU"
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: the no-GPU error path is not reachable")
+    with pytest.raises(gpuverify.GpuVerifyError):
+        gpuverify.GpuVerifier()
