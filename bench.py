@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""bench.py — P-256 ECDSA verifies/s on MI355X (BASELINE.json metric, config 2).
+
+A "step" is one launch of the verify hot path over one batch of device-resident
+synthetic tuples: 1,000,000 per GPU (32-byte SHA-256 digests, distinct key per tuple,
+~10% corrupted; smartbft_amd/workload.py). Multi-GPU (weak scaling): one process per GPU,
+rank r owns tuples [r*N, (r+1)*N) — no data-path collective (there is nothing to reduce;
+SURVEY.md 8(e)); a barrier brackets the timed region and the time is the max over ranks.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n TUPLES]
+  N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+Prints ONE JSON line on rank 0 (fields: see DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Roofline accounting: algorithmic work per verify = 4,096 F_p-multiplication
+# equivalents x 64 32x32->64 products; peak = measured v_mad_u64_u32 rate on
+# MI355X (tools/valu_peak.hip: 33.9 T lane-ops/s; profiles/r01_valu_peak.txt).
+PRODUCTS_PER_VERIFY = 262_144
+MAD_PEAK_T = 33.9
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1_000_000, help="tuples per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=131072)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_verify_latest.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(wl, sample: int, threads: int):
+    """Oracle ('port') and OpenSSL timed on host cores over a bounded sample of the same
+    workload; also returns the oracle verdicts of the sample (a free parity check)."""
+    import oracle  # test infrastructure: the cpu_baseline leg is one of its allowed users
+    sample = min(sample, wl.n)
+    f = wl.host_fields(0, sample)
+    oracle.lib()
+    t0 = time.perf_counter()
+    ok_cpu = oracle.verify_batch(*f, nthreads=threads)
+    dt = time.perf_counter() - t0
+    port = {"value": round(sample / dt, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
+            "sample": f"first {sample} tuples of the bench workload, oracle/p256_oracle.c "
+                      f"(C restatement of Go crypto/ecdsa.Verify), {threads} pthreads, {dt:.2f} s"}
+    go_proxy = None
+    exe = os.path.join(ROOT, "oracle", "openssl_bench")
+    if os.path.exists(exe):
+        with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as tf:
+            tf.write(np.concatenate(f, axis=1).tobytes())
+            path = tf.name
+        try:
+            out = subprocess.run([exe, path, str(threads), "10"], capture_output=True, text=True,
+                                 timeout=120)
+            if out.returncode == 0:
+                j = json.loads(out.stdout.strip().splitlines()[-1])
+                go_proxy = {"value": j["verifies_per_s"], "unit": "verifies/s", "cores": threads,
+                            "kind": "fallback: OpenSSL 3.0.2 ECDSA_do_verify, not Go (Go absent)",
+                            "sample": f"{sample} workload tuples cycled for {j['seconds']:.1f} s"}
+        finally:
+            os.unlink(path)
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    port["cpu"] = cpu_model
+    if go_proxy:
+        go_proxy["cpu"] = cpu_model
+    return port, go_proxy, ok_cpu
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    from smartbft_amd import GpuVerifier
+    from smartbft_amd.workload import make_workload
+
+    gv = GpuVerifier(device_mask=1 << local)
+    n = args.n
+    wl = make_workload(gv, n, start=rank * n, device=local)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        gv.verify_dev(wl.digest, wl.r, wl.s, wl.qx, wl.qy, ok, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    # parity property at full size: verdict == not corrupted, for every tuple
+    expect = (~wl.corrupted).to(torch.uint8)
+    mismatches = int((ok != expect).sum())
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        mm = torch.tensor([mismatches], dtype=torch.int64, device=dev)
+        dist.all_reduce(mm)
+        mismatches = int(mm.item())
+    kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+
+    if rank == 0:
+        total = n * world * args.steps
+        value = total / elapsed
+        achieved_t = n * PRODUCTS_PER_VERIFY / avg_kern_s / 1e12
+        traffic = None
+        if os.path.exists(args.traffic_file):
+            try:
+                tj = json.load(open(args.traffic_file))
+                if tj.get("n") == n:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        rec = {
+            "metric": "P-256 ECDSA verifies/sec",
+            "value": round(value, 1),
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (256-bit integers as 8x32-bit limbs)",
+            "data": "synthetic (on-GPU seeded keys/signatures, ~10% corrupted; smartbft_amd/workload.py)",
+            "config": {"workload": "BASELINE config 2: synthetic P-256 verifies, 32-byte SHA-256 digests, "
+                                   "distinct key per tuple, 10% corrupted, device-resident",
+                       "tuples_per_gpu": n, "parallelism": f"batch split x{world} (no collective)"},
+            "roofline": {"bound": "valu", "achieved": round(achieved_t, 3), "peak": MAD_PEAK_T,
+                         "unit": "T 32x32->64 products/s (v_mad_u64_u32)",
+                         "frac": round(achieved_t / MAD_PEAK_T, 4), "traffic": traffic,
+                         "kernel": "p256_verify_kernel", "avg_kernel_ms": round(avg_kern_s * 1e3, 4),
+                         "products_per_verify": PRODUCTS_PER_VERIFY},
+            "parity": {"full_size_mismatches": mismatches,
+                       "expected_accepts": int(expect.sum()) * world},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            port, go_proxy, ok_cpu = cpu_baseline(wl, args.cpu_sample, args.cpu_threads)
+            rec["cpu_baseline"] = port
+            if go_proxy:
+                rec["cpu_baseline_go_proxy"] = go_proxy
+            rec["parity"]["oracle_sample_mismatches"] = int(
+                (ok[:len(ok_cpu)].cpu().numpy() != ok_cpu).sum())
+            rec["speedup_vs_cpu_baseline"] = round(value / port["value"], 1)
+            if go_proxy:
+                rec["speedup_vs_go_proxy"] = round(value / go_proxy["value"], 1)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -168,6 +168,21 @@ int sbft_gv_sha256_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_b
     return sbft_gv_verify_p256_dev(ctx, device, d_dig, d_r, d_s, d_qx, d_qy, n, d_ok, stream);
 }
 
+int sbft_gv_sign_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_d, const void* d_k,
+                          const void* d_digest, size_t n, void* d_qx, void* d_qy, void* d_r,
+                          void* d_s, void* d_status, void* stream) {
+    if (!ctx || (n && (!d_d || !d_k || !d_digest || !d_qx || !d_qy || !d_r || !d_s || !d_status)))
+        return SBFT_GV_EINVAL;
+    if (n > 0xffffffffu) return SBFT_GV_EINVAL;
+    if (!slot_for(ctx, device)) return SBFT_GV_ENODEV;
+    if (hipSetDevice(device) != hipSuccess) return SBFT_GV_EDEVICE;
+    return sbft_launch_p256_sign((const uint8_t*)d_d, (const uint8_t*)d_k, (const uint8_t*)d_digest,
+                                 (uint8_t*)d_qx, (uint8_t*)d_qy, (uint8_t*)d_r, (uint8_t*)d_s,
+                                 (uint8_t*)d_status, (uint32_t)n, (hipStream_t)stream)
+               ? SBFT_GV_ELAUNCH
+               : SBFT_GV_OK;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------- host buffers
@@ -270,6 +285,30 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
     return SBFT_GV_OK;
 }
 
+// Sign tuples [c.begin, +c.count): inputs d | k | digest, outputs qx | qy | r | s | status.
+int enqueue_sign(const Chunk& c, const uint8_t* d, const uint8_t* k, const uint8_t* digest, uint8_t* qx,
+                 uint8_t* qy, uint8_t* r, uint8_t* s, uint8_t* status) {
+    Slot* sl = c.slot;
+    const size_t f = align_up(32 * c.count, 256);
+    HIPCHK(hipSetDevice(sl->device));
+    int rc = sl->reserve(7 * f + align_up(c.count, 256));
+    if (rc) return rc;
+    uint8_t* b = sl->dbuf;
+    const uint8_t* src[3] = {d, k, digest};
+    for (int i = 0; i < 3; ++i)
+        HIPCHK(hipMemcpyAsync(b + i * f, src[i] + 32 * c.begin, 32 * c.count, hipMemcpyHostToDevice,
+                              sl->stream));
+    if (sbft_launch_p256_sign(b, b + f, b + 2 * f, b + 3 * f, b + 4 * f, b + 5 * f, b + 6 * f, b + 7 * f,
+                              (uint32_t)c.count, sl->stream))
+        return SBFT_GV_ELAUNCH;
+    uint8_t* dst[4] = {qx, qy, r, s};
+    for (int i = 0; i < 4; ++i)
+        HIPCHK(hipMemcpyAsync(dst[i] + 32 * c.begin, b + (3 + i) * f, 32 * c.count, hipMemcpyDeviceToHost,
+                              sl->stream));
+    HIPCHK(hipMemcpyAsync(status + c.begin, b + 7 * f, c.count, hipMemcpyDeviceToHost, sl->stream));
+    return SBFT_GV_OK;
+}
+
 template <class F>
 int run_chunks(sbft_gv_ctx* ctx, size_t n, F&& enqueue) {
     std::vector<Chunk> chunks = plan(ctx, n);
@@ -296,6 +335,16 @@ int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* 
     if (!digest || !r || !s || !qx || !qy || !ok_out || n > 0xffffffffu) return SBFT_GV_EINVAL;
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
         return enqueue_verify(c, digest, r, s, qx, qy, ok_out);
+    });
+}
+
+int sbft_gv_sign_p256(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_t* digest,
+                      size_t n, uint8_t* qx, uint8_t* qy, uint8_t* r, uint8_t* s, uint8_t* status) {
+    if (!ctx) return SBFT_GV_EINVAL;
+    if (n == 0) return SBFT_GV_OK;
+    if (!d || !k || !digest || !qx || !qy || !r || !s || !status || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
+        return enqueue_sign(c, d, k, digest, qx, qy, r, s, status);
     });
 }
 

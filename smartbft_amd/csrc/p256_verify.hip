@@ -13,235 +13,10 @@
 // wave-uniform guard, so adversarial inputs take the slow path only when present.
 //
 // Inputs: SoA, 32-byte big-endian fields. Output: one verdict byte per tuple.
-#include "p256_field.hpp"
-#include "p256_tables.inc"
+#include "p256_point.hpp"
 #include "sbft_kernels.h"
 
 namespace sbft {
-
-struct jp {
-    fe x, y, z;
-};
-
-__device__ __constant__ static const u32 C_R2P[8] = P256_R2P_LIMBS;
-__device__ __constant__ static const u32 C_ONEP[8] = P256_ONEP_LIMBS;
-__device__ __constant__ static const u32 C_BM[8] = P256_BM_LIMBS;
-__device__ __constant__ static const u32 C_R2N[8] = P256_R2N_LIMBS;
-__device__ __constant__ static const u32 C_ONEN[8] = P256_ONEN_LIMBS;
-__device__ __constant__ static const u32 C_GTAB[2 * 8 * P256_GTAB4_ENTRIES] = P256_GTAB4_DATA;
-
-SBFT_DEV fe fe_const(const u32* c) {
-    fe r;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r.v[k] = c[k];
-    return r;
-}
-SBFT_DEV fe fe_zero() {
-    fe r;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r.v[k] = 0;
-    return r;
-}
-SBFT_DEV void fe_sel(fe& r, bool c, const fe& a) {  // r = c ? a : r
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r.v[k] = c ? a.v[k] : r.v[k];
-}
-SBFT_DEV void jp_sel(jp& r, bool c, const jp& a) {
-    fe_sel(r.x, c, a.x);
-    fe_sel(r.y, c, a.y);
-    fe_sel(r.z, c, a.z);
-}
-
-// 32 big-endian bytes -> 8 little-endian limbs
-SBFT_DEV fe load_be32(const uint8_t* p) {
-    const uint4* q = reinterpret_cast<const uint4*>(p);
-    const uint4 a = q[0], b = q[1];
-    fe r;
-    r.v[7] = __builtin_bswap32(a.x);
-    r.v[6] = __builtin_bswap32(a.y);
-    r.v[5] = __builtin_bswap32(a.z);
-    r.v[4] = __builtin_bswap32(a.w);
-    r.v[3] = __builtin_bswap32(b.x);
-    r.v[2] = __builtin_bswap32(b.y);
-    r.v[1] = __builtin_bswap32(b.z);
-    r.v[0] = __builtin_bswap32(b.w);
-    return r;
-}
-
-// ------------------------------------------------------------ scalar field
-// Fermat inverse a^(n-2) mod n, Montgomery domain in and out.
-// n-2 = FFFFFFFF 00000000 FFFFFFFF FFFFFFFF | BCE6FAAD A7179E84 F3B9CAC2 FC63254F
-SBFT_DEV void fn_sqr_n(fe& r, int count) {
-#pragma unroll 1
-    for (int i = 0; i < count; ++i) fn_mul(r, r, r);
-}
-SBFT_DEV void fn_inv(fe& r, const fe& a) {
-    fe x2, x4, x8, x16, x32, t;
-    t = a;
-    fn_mul(t, t, t);
-    fn_mul(x2, t, a);  // 2^2-1
-    t = x2;
-    fn_sqr_n(t, 2);
-    fn_mul(x4, t, x2);
-    t = x4;
-    fn_sqr_n(t, 4);
-    fn_mul(x8, t, x4);
-    t = x8;
-    fn_sqr_n(t, 8);
-    fn_mul(x16, t, x8);
-    t = x16;
-    fn_sqr_n(t, 16);
-    fn_mul(x32, t, x16);
-    t = x32;             // FFFFFFFF
-    fn_sqr_n(t, 64);     // FFFFFFFF 00000000 00000000
-    fn_mul(t, t, x32);   // FFFFFFFF 00000000 FFFFFFFF
-    fn_sqr_n(t, 32);
-    fn_mul(t, t, x32);   // FFFFFFFF 00000000 FFFFFFFF FFFFFFFF
-    // low 128 bits, binary from the top
-    const u32 low[4] = {0xFC63254Fu, 0xF3B9CAC2u, 0xA7179E84u, 0xBCE6FAADu};
-#pragma unroll 1
-    for (int w = 3; w >= 0; --w) {
-        const u32 bits = low[w];
-#pragma unroll 1
-        for (int b = 31; b >= 0; --b) {
-            fn_mul(t, t, t);
-            if ((bits >> b) & 1u) fn_mul(t, t, a);
-        }
-    }
-    r = t;
-}
-
-// ------------------------------------------------------------ point arithmetic
-// Doubling, a = -3 (dbl-2001-b): 3M + 5S. Infinity (Z == 0) maps to infinity.
-SBFT_DEV void pt_dbl(jp& r, const jp& p) {
-    fe delta, gamma, beta, alpha, t0, t1, x3;
-    fp_sqr(delta, p.z);
-    fp_sqr(gamma, p.y);
-    fp_mul(beta, p.x, gamma);
-    fp_sub(t0, p.x, delta);
-    fp_add(t1, p.x, delta);
-    fp_mul(alpha, t0, t1);
-    fp_add(t0, alpha, alpha);
-    fp_add(alpha, t0, alpha);  // 3(X-d)(X+d)
-    fp_sqr(t0, alpha);
-    fp_add(beta, beta, beta);
-    fp_add(beta, beta, beta);  // 4 beta
-    fp_add(t1, beta, beta);    // 8 beta
-    fp_sub(x3, t0, t1);
-    fp_add(t0, p.y, p.z);
-    fp_sqr(t0, t0);
-    fp_sub(t0, t0, gamma);
-    fp_sub(r.z, t0, delta);
-    fp_sub(t0, beta, x3);
-    fp_mul(t0, alpha, t0);
-    fp_sqr(gamma, gamma);
-    fp_add(gamma, gamma, gamma);
-    fp_add(gamma, gamma, gamma);
-    fp_add(gamma, gamma, gamma);  // 8 gamma^2
-    fp_sub(r.y, t0, gamma);
-    r.x = x3;
-}
-
-// acc += b (b Jacobian, never infinity). Handles acc = infinity, acc == b
-// (doubling) and acc == -b (infinity). use == false leaves acc unchanged.
-SBFT_DEV void pt_add_jac(jp& acc, bool& inf, const jp& b, bool use) {
-    fe z1z1, z2z2, u1, u2, s1, s2, h, rr, t;
-    fp_sqr(z1z1, acc.z);
-    fp_sqr(z2z2, b.z);
-    fp_mul(u1, acc.x, z2z2);
-    fp_mul(u2, b.x, z1z1);
-    fp_mul(t, b.z, z2z2);
-    fp_mul(s1, acc.y, t);
-    fp_mul(t, acc.z, z1z1);
-    fp_mul(s2, b.y, t);
-    fp_sub(h, u2, u1);
-    fp_sub(rr, s2, s1);
-    const bool hz = fp_is_zero(h);
-    const bool rz = fp_is_zero(rr);
-    jp sum;
-    fe hh, hhh, v;
-    fp_sqr(hh, h);
-    fp_mul(hhh, hh, h);
-    fp_mul(v, u1, hh);
-    fp_sqr(sum.x, rr);
-    fp_sub(sum.x, sum.x, hhh);
-    fp_sub(sum.x, sum.x, v);
-    fp_sub(sum.x, sum.x, v);
-    fp_sub(t, v, sum.x);
-    fp_mul(sum.y, rr, t);
-    fp_mul(t, s1, hhh);
-    fp_sub(sum.y, sum.y, t);
-    fp_mul(t, acc.z, b.z);
-    fp_mul(sum.z, t, h);
-    bool sum_inf = false;
-    const bool live = use && !inf;
-    const bool need_dbl = live && hz && rz;
-    if (__builtin_expect(__any(need_dbl), 0)) {
-        jp d;
-        pt_dbl(d, acc);
-        jp_sel(sum, need_dbl, d);
-    }
-    sum_inf = hz && !rz;
-    // assemble: !use -> acc; inf -> b; else sum
-    jp out = acc;
-    bool out_inf = inf;
-    jp_sel(out, live, sum);
-    if (live) out_inf = sum_inf;
-    jp_sel(out, use && inf, b);
-    if (use && inf) out_inf = false;
-    acc = out;
-    inf = out_inf;
-}
-
-// acc += (x2, y2) affine (Montgomery), never infinity: mixed addition 8M + 3S.
-SBFT_DEV void pt_add_aff(jp& acc, bool& inf, const fe& x2, const fe& y2, bool use) {
-    fe z1z1, u2, s2, h, rr, t;
-    fp_sqr(z1z1, acc.z);
-    fp_mul(u2, x2, z1z1);
-    fp_mul(t, acc.z, z1z1);
-    fp_mul(s2, y2, t);
-    fp_sub(h, u2, acc.x);
-    fp_sub(rr, s2, acc.y);
-    const bool hz = fp_is_zero(h);
-    const bool rz = fp_is_zero(rr);
-    jp sum;
-    fe hh, hhh, v;
-    fp_sqr(hh, h);
-    fp_mul(hhh, hh, h);
-    fp_mul(v, acc.x, hh);
-    fp_sqr(sum.x, rr);
-    fp_sub(sum.x, sum.x, hhh);
-    fp_sub(sum.x, sum.x, v);
-    fp_sub(sum.x, sum.x, v);
-    fp_sub(t, v, sum.x);
-    fp_mul(sum.y, rr, t);
-    fp_mul(t, acc.y, hhh);
-    fp_sub(sum.y, sum.y, t);
-    fp_mul(sum.z, acc.z, h);
-    const bool live = use && !inf;
-    const bool need_dbl = live && hz && rz;
-    if (__builtin_expect(__any(need_dbl), 0)) {
-        jp d;
-        pt_dbl(d, acc);
-        jp_sel(sum, need_dbl, d);
-    }
-    const bool sum_inf = hz && !rz;
-    jp out = acc;
-    bool out_inf = inf;
-    jp_sel(out, live, sum);
-    if (live) out_inf = sum_inf;
-    if (use && inf) {
-        out.x = x2;
-        out.y = y2;
-        out.z = fe_const(C_ONEP);
-        out_inf = false;
-    }
-    acc = out;
-    inf = out_inf;
-}
-
-// Radix-16 Booth digit from the 5-bit window (b3 b2 b1 b0 b-1): value in [-8, 8].
-SBFT_DEV int booth(u32 w5) { return (int)((w5 >> 1) + (w5 & 1u)) - (int)((w5 >> 4) << 4); }
 
 // ------------------------------------------------------------ the kernel
 __global__ __launch_bounds__(256) void p256_verify_kernel(const uint8_t* __restrict__ digest,

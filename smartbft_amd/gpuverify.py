@@ -18,7 +18,7 @@ EXPORTS = [
     "sbft_gv_init", "sbft_gv_destroy", "sbft_gv_device_count", "sbft_gv_strerror",
     "sbft_gv_verify_p256", "sbft_gv_sha256", "sbft_gv_sha256_verify_p256",
     "sbft_gv_verify_p256_dev", "sbft_gv_sha256_dev", "sbft_gv_sha256_verify_p256_dev",
-    "sbft_gv_normalize_hash", "sbft_gv_normalize_scalar",
+    "sbft_gv_normalize_hash", "sbft_gv_normalize_scalar", "sbft_gv_sign_p256", "sbft_gv_sign_p256_dev",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -63,6 +63,8 @@ def load_library():
     L.sbft_gv_sha256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 3 + [ctypes.c_size_t, _vp, _vp]
     L.sbft_gv_sha256_verify_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 7 + \
                                                 [ctypes.c_size_t, _vp, _vp, _vp]
+    L.sbft_gv_sign_p256.argtypes = [_vp] + [_u8p] * 3 + [ctypes.c_size_t] + [_u8p] * 5
+    L.sbft_gv_sign_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 3 + [ctypes.c_size_t] + [_vp] * 6
     L.sbft_gv_normalize_hash.argtypes = [_u8p, ctypes.c_size_t, _u8p]
     L.sbft_gv_normalize_hash.restype = None
     L.sbft_gv_normalize_scalar.argtypes = [_u8p, ctypes.c_size_t, _u8p]
@@ -135,6 +137,23 @@ class GpuVerifier:
         self._check(self.L.sbft_gv_verify_p256(self.ctx, *[_p(a) for a in arrs], n, _p(ok)),
                     "sbft_gv_verify_p256")
         return ok
+
+    def sign(self, d, k, digest):
+        """Q = d*G and ECDSA (r, s) with nonces k. Returns (qx, qy, r, s, status)."""
+        n = len(d)
+        ins = [_soa(a, n) for a in (d, k, digest)]
+        outs = [np.zeros((n, 32), dtype=np.uint8) for _ in range(4)]
+        st = np.zeros(n, dtype=np.uint8)
+        self._check(self.L.sbft_gv_sign_p256(self.ctx, *[_p(a) for a in ins], n,
+                                             *[_p(a) for a in outs], _p(st)), "sbft_gv_sign_p256")
+        return (*outs, st)
+
+    def sign_dev(self, d_d, d_k, d_e, d_qx, d_qy, d_r, d_s, d_status, stream=None):
+        n = d_status.numel()
+        self._check(self.L.sbft_gv_sign_p256_dev(
+            self.ctx, d_status.device.index, d_d.data_ptr(), d_k.data_ptr(), d_e.data_ptr(), n,
+            d_qx.data_ptr(), d_qy.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), d_status.data_ptr(),
+            self._stream(stream)), "sbft_gv_sign_p256_dev")
 
     def sha256(self, blob: np.ndarray, off: np.ndarray, ln: np.ndarray) -> np.ndarray:
         blob = np.ascontiguousarray(blob, dtype=np.uint8)

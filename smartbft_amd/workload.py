@@ -1,0 +1,122 @@
+"""Synthetic signed workloads of BASELINE.json config 2 ("1M ECDSA P-256 verifies, 32-byte
+SHA-256 digests, 10% corrupted sigs"), generated on the GPU by the engine itself (its
+SHA-256 and signer kernels) so that bench setup takes seconds, not CPU-minutes.
+
+Tuple i (global index; rank r of a multi-GPU run owns [r*N, (r+1)*N)):
+  d_i = SHA-256(seed | "key" | le64(i)) mod n      (distinct key per tuple)
+  m_i = SHA-256(seed | "msg" | le64(i)) || SHA-256(seed | "ms2" | le64(i))   (64-byte message)
+  e_i = SHA-256(m_i)                                (the 32-byte digest that is verified)
+  k_i = SHA-256(seed | "k" | le64(i)) mod n         (nonce)
+  corrupted iff SHA-256(seed | "c" | le64(i))[0] < 26   (~10.2%)
+  corruption kind = (i mod 7): flip an r bit, flip an s bit, flip an e bit, r = 0,
+  s = n, Q off-curve (y xor 1), Q replaced by the neighbour's key.
+seed = b"SBFT-GPUV-1".
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+SEED = b"SBFT-GPUV-1"
+N_BYTES = bytes.fromhex("FFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551")
+
+
+def _tag_messages(tag: bytes, start: int, n: int) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Fixed-width messages seed|tag|le64(i) for i in [start, start+n) as (blob, off, len)."""
+    head = np.frombuffer(SEED + tag, dtype=np.uint8)
+    w = len(head) + 8
+    blob = np.empty((n, w), dtype=np.uint8)
+    blob[:, :len(head)] = head
+    idx = np.arange(start, start + n, dtype=np.uint64)
+    blob[:, len(head):] = idx.view(np.uint8).reshape(n, 8)
+    off = (np.arange(n, dtype=np.uint64) * w)
+    ln = np.full(n, w, dtype=np.uint32)
+    return blob.reshape(-1), off, ln
+
+
+def _gpu_sha(gv, blob: np.ndarray, off: np.ndarray, ln: np.ndarray, dev) -> torch.Tensor:
+    pad = np.zeros(blob.size + 128, dtype=np.uint8)
+    pad[:blob.size] = blob
+    d_blob = torch.from_numpy(pad).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(ln.astype(np.int32)).to(dev)
+    d_dig = torch.empty((len(off), 32), dtype=torch.uint8, device=dev)
+    gv.sha256_dev(d_blob, d_off, d_len, d_dig)
+    return d_dig
+
+
+def _reduce_mod_n(x: torch.Tensor) -> torch.Tensor:
+    """Values >= n (probability ~2^-32 each) are replaced by value - n, on the host."""
+    nb = torch.tensor(list(N_BYTES), dtype=torch.uint8, device=x.device)
+    # lexicographic compare of big-endian rows against n
+    diff = x.to(torch.int16) - nb.to(torch.int16)
+    first = torch.argmax((diff != 0).to(torch.int8), dim=1)
+    sign = diff.gather(1, first[:, None]).squeeze(1)
+    ge = sign >= 0
+    if bool(ge.any()):
+        for i in torch.nonzero(ge).flatten().tolist():
+            v = (int.from_bytes(bytes(x[i].tolist()), "big") - int.from_bytes(N_BYTES, "big"))
+            x[i] = torch.tensor(list(v.to_bytes(32, "big")), dtype=torch.uint8, device=x.device)
+    return x
+
+
+class Workload:
+    """Device-resident SoA tuples + the expected verdicts implied by construction."""
+
+    def __init__(self, digest, r, s, qx, qy, corrupted: torch.Tensor, start: int):
+        self.digest, self.r, self.s, self.qx, self.qy = digest, r, s, qx, qy
+        self.corrupted = corrupted
+        self.start = start
+
+    @property
+    def n(self) -> int:
+        return self.digest.shape[0]
+
+    def host_fields(self, lo: int = 0, hi: int | None = None):
+        sl = slice(lo, hi)
+        return [t[sl].cpu().numpy() for t in (self.digest, self.r, self.s, self.qx, self.qy)]
+
+
+def make_workload(gv, n: int, start: int = 0, device: int = 0, corrupt: bool = True) -> Workload:
+    dev = torch.device(f"cuda:{device}")
+    d = _reduce_mod_n(_gpu_sha(gv, *_tag_messages(b"key", start, n), dev))
+    k = _reduce_mod_n(_gpu_sha(gv, *_tag_messages(b"k", start, n), dev))
+    m1 = _gpu_sha(gv, *_tag_messages(b"msg", start, n), dev)
+    m2 = _gpu_sha(gv, *_tag_messages(b"ms2", start, n), dev)
+    msg = torch.cat([m1, m2], dim=1).contiguous()  # 64-byte messages
+    blob = msg.reshape(-1).cpu().numpy()
+    e = _gpu_sha(gv, blob, np.arange(n, dtype=np.uint64) * 64, np.full(n, 64, dtype=np.uint32), dev)
+    qx = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    qy, r, s = torch.empty_like(qx), torch.empty_like(qx), torch.empty_like(qx)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    gv.sign_dev(d, k, e, qx, qy, r, s, st)
+    torch.cuda.synchronize(dev)
+    if not bool((st == 1).all()):
+        raise RuntimeError(f"signer rejected {int((st != 1).sum())} synthetic keys/nonces")
+    c = _gpu_sha(gv, *_tag_messages(b"c", start, n), dev)
+    corrupted = c[:, 0] < 26 if corrupt else torch.zeros(n, dtype=torch.bool, device=dev)
+    if corrupt:
+        idx = torch.nonzero(corrupted).flatten()
+        kind = (idx + start) % 7
+        byte = (c[idx, 1] % 32).long()
+        bit = (1 << (c[idx, 2] % 8).to(torch.int32)).to(torch.uint8)
+        for kk, t in ((0, r), (1, s), (2, e)):
+            sel = idx[kind == kk]
+            if sel.numel():
+                b = byte[kind == kk]
+                t[sel, b] ^= bit[kind == kk]
+        sel = idx[kind == 3]
+        r[sel] = 0
+        sel = idx[kind == 4]
+        s[sel] = torch.tensor(list(N_BYTES), dtype=torch.uint8, device=dev)
+        sel = idx[kind == 5]
+        qy[sel, 31] ^= 1
+        sel = idx[kind == 6]
+        nb = (sel + 1) % n
+        qx_nb, qy_nb = qx[nb].clone(), qy[nb].clone()
+        qx[sel] = qx_nb
+        qy[sel] = qy_nb
+        # a neighbour that is itself replaced keeps its own original key: equal keys would
+        # make the swap a no-op only if two tuples shared d, which distinct hashes exclude.
+    torch.cuda.synchronize(dev)
+    return Workload(e, r, s, qx, qy, corrupted, start)

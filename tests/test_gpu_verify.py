@@ -157,3 +157,44 @@ def test_fused_hash_then_verify(gpu):
     exp = oracle.verify_batch(dig, *cols)
     assert np.array_equal(ok, exp)
     assert exp.sum() == n - len(range(0, n, 5))
+
+
+def test_signer_matches_oracle(gpu):
+    """GPU key derivation + signing with fixed nonces == the oracle's, byte for byte."""
+    rng = np.random.default_rng(21)
+    n = 700
+    d = [int.from_bytes(rng.bytes(32), "big") % oracle.N or 1 for _ in range(n)]
+    k = [int.from_bytes(rng.bytes(32), "big") % oracle.N or 1 for _ in range(n)]
+    d[0], k[0] = 1, 1
+    d[1], k[1] = oracle.N - 1, oracle.N - 1
+    e = [rng.bytes(32) for _ in range(n)]
+    e[2] = b"\xff" * 32
+    arr = lambda xs: np.frombuffer(b"".join(x if isinstance(x, bytes) else x.to_bytes(32, "big")
+                                            for x in xs), dtype=np.uint8).reshape(-1, 32)
+    qx, qy, r, s, st = gpu.sign(arr(d), arr(k), arr(e))
+    assert st.all()
+    for i in range(n):
+        ox, oy = oracle.pubkey(d[i])
+        orr, oss = oracle.sign(d[i], k[i], e[i])
+        assert (qx[i].tobytes(), qy[i].tobytes()) == (ox, oy), i
+        assert (r[i].tobytes(), s[i].tobytes()) == (orr, oss), i
+    # out-of-range private keys / nonces are flagged, not signed
+    bad = arr([0, oracle.N, oracle.N + 5])
+    *_, st2 = gpu.sign(bad, arr([1, 1, 1]), arr([b"\0" * 32] * 3))
+    assert not st2.any()
+
+
+def test_bench_workload_properties(gpu):
+    """The synthetic bench workload: every uncorrupted tuple verifies, every corrupted one
+    does not (by construction), and a sample agrees with the oracle."""
+    import torch
+    from smartbft_amd.workload import make_workload
+    wl = make_workload(gpu, 20000, start=12345)
+    ok = torch.empty(wl.n, dtype=torch.uint8, device="cuda:0")
+    gpu.verify_dev(wl.digest, wl.r, wl.s, wl.qx, wl.qy, ok)
+    torch.cuda.synchronize()
+    assert torch.equal(ok, (~wl.corrupted).to(torch.uint8))
+    frac = float(wl.corrupted.float().mean())
+    assert 0.07 < frac < 0.13
+    f = wl.host_fields(0, 3000)
+    assert np.array_equal(oracle.verify_batch(*f), ok[:3000].cpu().numpy())
