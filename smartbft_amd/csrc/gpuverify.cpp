@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -20,16 +21,43 @@
 
 namespace {
 
+struct Workspace {
+    void* ptr = nullptr;
+    size_t cap = 0;
+};
+
 struct Slot {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
     uint8_t* dbuf = nullptr;
     size_t dcap = 0;
+    // verify workspaces of the device-resident entry points, one per caller stream (work on
+    // one stream is ordered, so a stream never races with itself on its workspace)
+    std::mutex ws_mu;
+    std::map<hipStream_t, Workspace> ws;
+
+    uint32_t* stream_workspace(hipStream_t st, size_t bytes) {
+        std::lock_guard<std::mutex> g(ws_mu);
+        Workspace& w = ws[st];
+        if (w.cap < bytes) {
+            if (w.ptr) {
+                // the stream may still be using the old buffer
+                if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+                if (hipFree(w.ptr) != hipSuccess) return nullptr;
+            }
+            w.ptr = nullptr;
+            w.cap = 0;
+            const size_t want = std::max(bytes, (size_t)1 << 16);
+            if (hipMalloc(&w.ptr, want) != hipSuccess) return nullptr;
+            w.cap = want;
+        }
+        return (uint32_t*)w.ptr;
+    }
 
     int reserve(size_t bytes) {
         if (bytes <= dcap) return SBFT_GV_OK;
-        if (dbuf) hipFree(dbuf);
+        if (dbuf) (void)hipFree(dbuf);
         dbuf = nullptr;
         dcap = 0;
         size_t want = std::max(bytes, (size_t)1 << 20);
@@ -95,10 +123,14 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
 void sbft_gv_destroy(sbft_gv_ctx* ctx) {
     if (!ctx) return;
     for (Slot* s : ctx->slots) {
-        hipSetDevice(s->device);
-        if (s->stream) hipStreamSynchronize(s->stream);
-        if (s->dbuf) hipFree(s->dbuf);
-        if (s->stream) hipStreamDestroy(s->stream);
+        (void)hipSetDevice(s->device);
+        if (s->stream) (void)hipStreamSynchronize(s->stream);
+        if (s->dbuf) (void)hipFree(s->dbuf);
+        for (auto& kv : s->ws) {
+            (void)hipStreamSynchronize(kv.first);
+            if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+        }
+        if (s->stream) (void)hipStreamDestroy(s->stream);
         delete s;
     }
     delete ctx;
@@ -137,11 +169,15 @@ int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, 
                             void* d_ok, void* stream) {
     if (!ctx || (n && (!d_digest || !d_r || !d_s || !d_qx || !d_qy || !d_ok))) return SBFT_GV_EINVAL;
     if (n > 0xffffffffu) return SBFT_GV_EINVAL;
-    if (!slot_for(ctx, device)) return SBFT_GV_ENODEV;
+    Slot* sl = slot_for(ctx, device);
+    if (!sl) return SBFT_GV_ENODEV;
+    if (n == 0) return SBFT_GV_OK;
     if (hipSetDevice(device) != hipSuccess) return SBFT_GV_EDEVICE;
+    uint32_t* work = sl->stream_workspace((hipStream_t)stream, sbft_verify_work_bytes(n));
+    if (!work) return SBFT_GV_ENOMEM;
     return sbft_launch_p256_verify((const uint8_t*)d_digest, (const uint8_t*)d_r, (const uint8_t*)d_s,
                                    (const uint8_t*)d_qx, (const uint8_t*)d_qy, (uint8_t*)d_ok,
-                                   (uint32_t)n, (hipStream_t)stream)
+                                   (uint32_t)n, work, (hipStream_t)stream)
                ? SBFT_GV_ELAUNCH
                : SBFT_GV_OK;
 }
@@ -220,15 +256,17 @@ int enqueue_verify(const Chunk& c, const uint8_t* digest, const uint8_t* r, cons
     Slot* sl = c.slot;
     const size_t f = align_up(32 * c.count, 256);
     HIPCHK(hipSetDevice(sl->device));
-    int rc = sl->reserve(5 * f + align_up(c.count, 256));
+    const size_t fo = align_up(c.count, 256);
+    int rc = sl->reserve(5 * f + fo + sbft_verify_work_bytes(c.count));
     if (rc) return rc;
     uint8_t* base = sl->dbuf;
+    uint32_t* work = (uint32_t*)(base + 5 * f + fo);
     const uint8_t* src[5] = {digest, r, s, qx, qy};
     for (int k = 0; k < 5; ++k)
         HIPCHK(hipMemcpyAsync(base + k * f, src[k] + 32 * c.begin, 32 * c.count, hipMemcpyHostToDevice,
                               sl->stream));
     if (sbft_launch_p256_verify(base, base + f, base + 2 * f, base + 3 * f, base + 4 * f, base + 5 * f,
-                                (uint32_t)c.count, sl->stream))
+                                (uint32_t)c.count, work, sl->stream))
         return SBFT_GV_ELAUNCH;
     HIPCHK(hipMemcpyAsync(ok_out + c.begin, base + 5 * f, c.count, hipMemcpyDeviceToHost, sl->stream));
     return SBFT_GV_OK;
@@ -254,7 +292,8 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
     const size_t fo = align_up(8 * c.count, 256), fl = align_up(4 * c.count, 256);
     const size_t fd = align_up(32 * c.count, 256);
     const bool verify = ok_out != nullptr;
-    const size_t need = fb + fo + fl + fd + (verify ? 4 * fd + align_up(c.count, 256) : 0);
+    const size_t need = fb + fo + fl + fd +
+                        (verify ? 4 * fd + align_up(c.count, 256) + sbft_verify_work_bytes(c.count) : 0);
     HIPCHK(hipSetDevice(sl->device));
     int rc = sl->reserve(need);
     if (rc) return rc;
@@ -273,8 +312,9 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
             HIPCHK(hipMemcpyAsync(v + k * fd, src[k] + 32 * c.begin, 32 * c.count, hipMemcpyHostToDevice,
                                   sl->stream));
         uint8_t* d_ok = v + 4 * fd;
+        uint32_t* work = (uint32_t*)(d_ok + align_up(c.count, 256));
         if (sbft_launch_p256_verify(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_ok, (uint32_t)c.count,
-                                    sl->stream))
+                                    work, sl->stream))
             return SBFT_GV_ELAUNCH;
         HIPCHK(hipMemcpyAsync(ok_out + c.begin, d_ok, c.count, hipMemcpyDeviceToHost, sl->stream));
     }
@@ -318,7 +358,7 @@ int run_chunks(sbft_gv_ctx* ctx, size_t n, F&& enqueue) {
     int rc = SBFT_GV_OK;
     for (size_t i = 0; i < chunks.size() && rc == SBFT_GV_OK; ++i) rc = enqueue(chunks[i], i);
     for (auto& c : chunks) {
-        hipSetDevice(c.slot->device);
+        (void)hipSetDevice(c.slot->device);
         if (hipStreamSynchronize(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
     }
     return rc;

@@ -86,7 +86,9 @@ SBFT_DEV void mul512(u32 t[16], const fe& a, const fe& b) {
     t[15] = lo32(acc);
 }
 
-// Squaring: off-diagonal triangle once, doubled, plus the diagonal.
+// Squaring: off-diagonal triangle once (28 products), doubled by a one-bit funnel shift
+// (v_alignbit), then the 8 diagonal squares added pairwise with one v_mad_u64_u32 each and
+// the carry chained through SGPR lane masks.
 SBFT_DEV void sqr512(u32 t[16], const fe& a) {
     u32 x[16];
     u64 acc = 0;
@@ -112,16 +114,31 @@ SBFT_DEV void sqr512(u32 t[16], const fe& a) {
     }
     x[14] = lo32(acc);
     x[15] = hi32(acc);
-    // t = 2*x + diag, one carry chain over 16 words
-    u64 c = 0;
+    // x2 = 2x (x < 2^511, so no bit is lost)
+    u32 d[16];
+    d[0] = 0;
+#pragma unroll
+    for (int i = 1; i < 16; ++i) d[i] = __builtin_amdgcn_alignbit(x[i], x[i - 1], 31);
+    u64 cin = 0;  // lane mask
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const u64 d = (u64)a.v[k] * a.v[k];
-        u64 s0 = (u64)x[2 * k] * 2 + lo32(d) + c;          // < 2^34
-        t[2 * k] = lo32(s0);
-        u64 s1 = (u64)x[2 * k + 1] * 2 + hi32(d) + hi32(s0);
-        t[2 * k + 1] = lo32(s1);
-        c = hi32(s1);
+        const u64 pair = ((u64)d[2 * k + 1] << 32) | d[2 * k];
+        u64 sum, c1, c3;
+        asm("v_mad_u64_u32 %0, %1, %2, %2, %3" : "=v"(sum), "=s"(c1) : "v"(a.v[k]), "v"(pair));
+        u32 lo = lo32(sum), hi = hi32(sum);
+        if (k == 0) {
+            t[0] = lo;
+            t[1] = hi;
+            cin = c1;
+            continue;
+        }
+        asm("v_addc_co_u32 %0, %2, %0, 0, %3\n\t"
+            "v_addc_co_u32 %1, %2, %1, 0, %2"
+            : "+v"(lo), "+v"(hi), "=&s"(c3)
+            : "s"(cin));
+        t[2 * k] = lo;
+        t[2 * k + 1] = hi;
+        cin = c1 | c3;
     }
 }
 

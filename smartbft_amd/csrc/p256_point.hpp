@@ -17,6 +17,12 @@ __device__ __constant__ static const u32 C_BM[8] = P256_BM_LIMBS;
 __device__ __constant__ static const u32 C_R2N[8] = P256_R2N_LIMBS;
 __device__ __constant__ static const u32 C_ONEN[8] = P256_ONEN_LIMBS;
 __device__ __constant__ static const u32 C_GTAB[2 * 8 * P256_GTAB4_ENTRIES] = P256_GTAB4_DATA;
+// Verify-side fixed-base table: [k]G, k = 1..128 (signed radix-256 windows), 8 KiB, staged
+// into LDS once per workgroup.
+#define GODD8_WORDS (2 * 8 * P256_GODD8_ENTRIES)
+__device__ __constant__ static const u32 C_GODD8[GODD8_WORDS] = P256_GODD8_DATA;
+__device__ __constant__ static const u32 C_G2X[8] = P256_G2X_LIMBS;
+__device__ __constant__ static const u32 C_G2Y[8] = P256_G2Y_LIMBS;
 
 SBFT_DEV fe fe_const(const u32* c) {
     fe r;
@@ -228,8 +234,70 @@ SBFT_DEV void pt_add_aff(jp& acc, bool& inf, const fe& x2, const fe& y2, bool us
     inf = out_inf;
 }
 
+
+// ---- lean additions for the verify loop (signed-odd digits: every add is live) ----
+// acc += b with no case analysis. If H == 0 (acc == +-b: a doubling or a cancellation to
+// infinity) the result is garbage and `exc` is raised; the caller re-verifies such tuples
+// with the general routines (p256_verify.hip fixup kernel). Rare: adversarial inputs or
+// scalars whose partial sums collide.
+SBFT_DEV void pt_add_jac_lean(jp& acc, bool& exc, const jp& b) {
+    fe z1z1, u2, s2, t, u1, s1, h, rr;
+    fp_sqr(z1z1, acc.z);
+    fp_mul(u2, b.x, z1z1);
+    fp_mul(t, acc.z, z1z1);
+    fp_mul(s2, b.y, t);
+    fp_sqr(t, b.z);  // z2z2
+    fp_mul(u1, acc.x, t);
+    fp_mul(t, b.z, t);
+    fp_mul(s1, acc.y, t);
+    fp_sub(h, u2, u1);
+    fp_sub(rr, s2, s1);
+    exc = exc || fp_is_zero(h);
+    fe hh, hhh;
+    fp_sqr(hh, h);
+    fp_mul(hhh, hh, h);
+    fp_mul(u1, u1, hh);  // v = U1 H^2
+    fp_mul(t, acc.z, b.z);
+    fp_mul(acc.z, t, h);
+    fp_sqr(t, rr);
+    fp_sub(t, t, hhh);
+    fp_sub(t, t, u1);
+    fp_sub(acc.x, t, u1);
+    fp_sub(t, u1, acc.x);
+    fp_mul(t, rr, t);
+    fp_mul(s1, s1, hhh);
+    fp_sub(acc.y, t, s1);
+}
+
+// acc += (x2, y2) affine, same structure (8M + 3S on the common path).
+SBFT_DEV void pt_add_aff_lean(jp& acc, bool& exc, const fe& x2, const fe& y2) {
+    fe z1z1, u2, s2, h, rr;
+    fp_sqr(z1z1, acc.z);
+    fp_mul(u2, x2, z1z1);
+    fp_mul(s2, acc.z, z1z1);
+    fp_mul(s2, y2, s2);
+    fp_sub(h, u2, acc.x);
+    fp_sub(rr, s2, acc.y);
+    exc = exc || fp_is_zero(h);
+    fe hh, hhh;
+    fp_sqr(hh, h);
+    fp_mul(hhh, hh, h);
+    fp_mul(u2, acc.x, hh);  // v = X1 H^2
+    fp_mul(acc.z, acc.z, h);
+    fp_sqr(s2, rr);
+    fp_sub(s2, s2, hhh);
+    fp_sub(s2, s2, u2);
+    fp_sub(acc.x, s2, u2);
+    fp_sub(s2, u2, acc.x);
+    fp_mul(s2, rr, s2);
+    fp_mul(hhh, acc.y, hhh);
+    fp_sub(acc.y, s2, hhh);
+}
+
 // Radix-16 Booth digit from the 5-bit window (b3 b2 b1 b0 b-1): value in [-8, 8].
 SBFT_DEV int booth(u32 w5) { return (int)((w5 >> 1) + (w5 & 1u)) - (int)((w5 >> 4) << 4); }
+// Radix-256 Booth digit from the 9-bit window (b7..b0 b-1): value in [-128, 128].
+SBFT_DEV int booth8(u32 w9) { return (int)((w9 >> 1) + (w9 & 1u)) - (int)((w9 >> 8) << 8); }
 
 
 // Field inverse a^(p-2) mod p, Montgomery domain in and out (255 S + 12 M).

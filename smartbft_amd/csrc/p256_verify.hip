@@ -5,9 +5,10 @@
 //   1. range checks r, s in [1, n-1]; Qx, Qy < p; Q on y^2 = x^3 - 3x + b
 //   2. e = digest mod n; w = s^-1 mod n (Fermat, Montgomery mod n)
 //   3. u1 = e*w, u2 = r*w
-//   4. R = u1*G + u2*Q: one shared doubling chain (Straus/Shamir), radix-16 Booth
-//      (signed) digits for both scalars; [1..8]Q built per lane (Jacobian, scratch),
-//      [1..8]G read from an LDS copy of a precomputed affine table (mixed additions)
+//   4. R = u1*G + u2*Q: one shared doubling chain (Straus/Shamir) with regular signed-odd
+//      digits (never zero, so every addition is live and select-free): radix 16 for u2 over
+//      [1,3,..,15]Q built per lane (Jacobian, scratch), radix 256 for u1 over
+//      [1,3,..,255]G, an 8 KiB affine table staged in LDS (33 mixed additions)
 //   5. R = infinity -> reject; accept iff X == r*Z^2 or (r+n < p and X == (r+n)*Z^2)
 // Exceptional additions (P + P, P + (-P), infinity) are branched per lane under a
 // wave-uniform guard, so adversarial inputs take the slow path only when present.
@@ -18,27 +19,12 @@
 
 namespace sbft {
 
-// ------------------------------------------------------------ the kernel
-__global__ __launch_bounds__(256) void p256_verify_kernel(const uint8_t* __restrict__ digest,
-                                                          const uint8_t* __restrict__ rr,
-                                                          const uint8_t* __restrict__ ss,
-                                                          const uint8_t* __restrict__ qxx,
-                                                          const uint8_t* __restrict__ qyy,
-                                                          uint8_t* __restrict__ ok, uint32_t n) {
-    __shared__ u32 gtab[2 * 8 * P256_GTAB4_ENTRIES];
-    for (int i = threadIdx.x; i < 2 * 8 * P256_GTAB4_ENTRIES; i += blockDim.x) gtab[i] = C_GTAB[i];
-    __syncthreads();
-
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool active = gid < n;
-    const uint32_t idx = active ? gid : (n - 1);
-
-    const fe e_raw = load_be32(digest + 32ull * idx);
-    const fe r = load_be32(rr + 32ull * idx);
-    const fe s = load_be32(ss + 32ull * idx);
-    const fe qx = load_be32(qxx + 32ull * idx);
-    const fe qy = load_be32(qyy + 32ull * idx);
-
+// ------------------------------------------------------------ general path
+// The fully case-split verify (Booth radix-16 digits including zero, explicit infinity and
+// doubling branches in every addition). It runs only for tuples the lean kernel flagged:
+// adversarial inputs whose Shamir ladder hits P + P, P + (-P) or infinity.
+__device__ __noinline__ bool verify_general(const fe& e_raw, const fe& r, const fe& s, const fe& qx,
+                                            const fe& qy, const u32* gtab) {
     // 1. range checks
     bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
                  fe_lt(qx, P256_P) && fe_lt(qy, P256_P);
@@ -179,18 +165,259 @@ __global__ __launch_bounds__(256) void p256_verify_kernel(const uint8_t* __restr
             accept = accept || fe_eq(lhs, xc);
         }
     }
-    if (active) ok[gid] = (valid && accept) ? 1 : 0;
+    return valid && accept;
+}
+
+__global__ __launch_bounds__(256) void p256_verify_fixup_kernel(const uint8_t* __restrict__ digest,
+                                                                const uint8_t* __restrict__ rr,
+                                                                const uint8_t* __restrict__ ss,
+                                                                const uint8_t* __restrict__ qxx,
+                                                                const uint8_t* __restrict__ qyy,
+                                                                uint8_t* __restrict__ ok,
+                                                                const uint32_t* __restrict__ work) {
+    __shared__ u32 gtab[2 * 8 * P256_GTAB4_ENTRIES];
+    for (int i = threadIdx.x; i < 2 * 8 * P256_GTAB4_ENTRIES; i += blockDim.x) gtab[i] = C_GTAB[i];
+    __syncthreads();
+    const uint32_t count = work[0];
+    const uint32_t* list = work + 1;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
+        const uint32_t idx = list[j];
+        const bool v = verify_general(load_be32(digest + 32ull * idx), load_be32(rr + 32ull * idx),
+                                      load_be32(ss + 32ull * idx), load_be32(qxx + 32ull * idx),
+                                      load_be32(qyy + 32ull * idx), gtab);
+        ok[idx] = v ? 1 : 0;
+    }
+}
+
+// ------------------------------------------------------------ the kernel
+#ifndef SBFT_VERIFY_WAVES
+#define SBFT_VERIFY_WAVES 3
+#endif
+__global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(const uint8_t* __restrict__ digest,
+                                                          const uint8_t* __restrict__ rr,
+                                                          const uint8_t* __restrict__ ss,
+                                                          const uint8_t* __restrict__ qxx,
+                                                          const uint8_t* __restrict__ qyy,
+                                                          uint8_t* __restrict__ ok, uint32_t n,
+                                                          uint32_t* __restrict__ work) {
+    __shared__ u32 gtab[GODD8_WORDS];
+    for (int i = threadIdx.x; i < GODD8_WORDS; i += blockDim.x) gtab[i] = C_GODD8[i];
+    __syncthreads();
+
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = gid < n;
+    const uint32_t idx = active ? gid : (n - 1);
+
+    const fe e_raw = load_be32(digest + 32ull * idx);
+    const fe r = load_be32(rr + 32ull * idx);
+    const fe s = load_be32(ss + 32ull * idx);
+    const fe qx = load_be32(qxx + 32ull * idx);
+    const fe qy = load_be32(qyy + 32ull * idx);
+
+    // 1. range checks
+    bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
+                 fe_lt(qx, P256_P) && fe_lt(qy, P256_P);
+
+    // Q to Montgomery form and on-curve check y^2 == x^3 - 3x + b
+    const fe r2p = fe_const(C_R2P);
+    jp q;
+    fp_mul(q.x, qx, r2p);
+    fp_mul(q.y, qy, r2p);
+    q.z = fe_const(C_ONEP);
+    {
+        fe lhs, rhs, t;
+        fp_sqr(lhs, q.y);
+        fp_sqr(rhs, q.x);
+        fp_mul(rhs, rhs, q.x);
+        fp_add(t, q.x, q.x);
+        fp_add(t, t, q.x);
+        fp_sub(rhs, rhs, t);
+        fp_add(rhs, rhs, fe_const(C_BM));
+        fp_canon(lhs, lhs);
+        fp_canon(rhs, rhs);
+        valid = valid && fe_eq(lhs, rhs);
+    }
+
+    // 2-3. scalars: w = s^-1, u1 = e w, u2 = r w (canonical, < n)
+    fe e;
+    fn_canon(e, e_raw);
+    fe sm, w, u1, u2;
+    fn_mul(sm, s, fe_const(C_R2N));  // s*R mod n
+    fn_inv(w, sm);                    // s^-1 * R
+    fn_mul(u1, e, w);                 // e*s^-1 (plain)
+    fn_mul(u2, r, w);                 // r*s^-1 (plain)
+    fn_canon(u1, u1);
+    fn_canon(u2, u2);
+    // Invalid lanes run a harmless stand-in (u1 = u2 = 1, Q = 2G) so they never take the
+    // exceptional path; their verdict is masked by `valid` at the end.
+    if (!valid) {
+        q.x = fe_const(C_G2X);
+        q.y = fe_const(C_G2Y);
+        u1 = fe_zero();
+        u1.v[0] = 1;
+        u2 = u1;
+    }
+    // Signed-odd (regular) recoding needs odd scalars: u even -> use n - u with the base
+    // negated ((n-u)(-P) = uP). u == 0 becomes n, whose ladder cancels to infinity.
+    const bool neg1 = (u1.v[0] & 1u) == 0;
+    const bool neg2 = (u2.v[0] & 1u) == 0;
+    {
+        fe t1, t2;
+        u64 b1 = 0, b2 = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const u64 d1 = (u64)P256_N[k] - u1.v[k] - b1;
+            const u64 d2 = (u64)P256_N[k] - u2.v[k] - b2;
+            t1.v[k] = lo32(d1);
+            t2.v[k] = lo32(d2);
+            b1 = d1 >> 63;
+            b2 = d2 >> 63;
+        }
+        fe_sel(u1, neg1, t1);
+        fe_sel(u2, neg2, t2);
+    }
+    if (neg2) {
+        fe ny;
+        fp_sub(ny, fe_zero(), q.y);
+        q.y = ny;
+    }
+
+    // 4. odd multiples [1,3,...,15]Q in Jacobian form (scratch)
+    jp tq[8];
+    tq[0] = q;
+    {
+        jp q2;
+        pt_dbl(q2, q);
+        bool texc = false;  // (2k+1)Q == +-2Q is impossible for a point of prime order n
+#pragma unroll 1
+        for (int k = 1; k < 8; ++k) {
+            jp t = tq[k - 1];
+            pt_add_jac_lean(t, texc, q2);
+            tq[k] = t;
+        }
+    }
+
+    // u = sum_{i<64} d_i 16^i + 16^64 with d_i = 2*((u >> (4i+1)) & 15) - 15 (odd, nonzero);
+    // likewise radix 256 for u1 over the [1,3,...,255]G table. The top digits are 1, so the
+    // accumulator starts at Q + G, never at infinity.
+    jp acc = q;
+    bool exc = false;
+    {
+        fe gx, gy;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            gx.v[k] = gtab[k];
+            gy.v[k] = gtab[8 + k];
+        }
+        if (neg1) {
+            fe ny;
+            fp_sub(ny, fe_zero(), gy);
+            gy = ny;
+        }
+        pt_add_aff_lean(acc, exc, gx, gy);
+    }
+    fe k1 = u1, k2 = u2;
+    u32 above1 = 0, above2 = 0;
+#pragma unroll 1
+    for (int limb = 7; limb >= 0; --limb) {
+        const u32 cur1 = k1.v[7], cur2 = k2.v[7];
+#pragma unroll
+        for (int k = 7; k > 0; --k) {
+            k1.v[k] = k1.v[k - 1];
+            k2.v[k] = k2.v[k - 1];
+        }
+        const u64 f1 = ((u64)above1 << 32) | cur1;
+        const u64 f2 = ((u64)above2 << 32) | cur2;
+        above1 = cur1;
+        above2 = cur2;
+#pragma unroll 1
+        for (int nib = 7; nib >= 0; --nib) {
+#pragma unroll 1
+            for (int d = 0; d < 4; ++d) pt_dbl(acc, acc);
+            // Q digit (odd, in [-15, 15])
+            {
+                const int d2 = 2 * (int)((u32)(f2 >> (4 * nib + 1)) & 15u) - 15;
+                jp t = tq[(d2 < 0 ? -d2 : d2) >> 1];
+                if (d2 < 0) {
+                    fe ny;
+                    fp_sub(ny, fe_zero(), t.y);
+                    t.y = ny;
+                }
+                pt_add_jac_lean(acc, exc, t);
+            }
+            // G digit (odd, in [-255, 255]) on every other radix-16 window
+            if ((nib & 1) == 0) {
+                const int d1 = 2 * (int)((u32)(f1 >> (4 * nib + 1)) & 255u) - 255;
+                const int base = ((d1 < 0 ? -d1 : d1) >> 1) * 16;
+                fe gx, gy;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    gx.v[k] = gtab[base + k];
+                    gy.v[k] = gtab[base + 8 + k];
+                }
+                if ((d1 < 0) != neg1) {
+                    fe ny;
+                    fp_sub(ny, fe_zero(), gy);
+                    gy = ny;
+                }
+                pt_add_aff_lean(acc, exc, gx, gy);
+            }
+        }
+    }
+
+    // 5. x(R) mod n == r, projectively (R is finite on every unflagged lane)
+    bool accept;
+    {
+        const fe rv = load_be32(rr + 32ull * idx);  // reload: keeps r out of the loop's registers
+        fe z2, lhs, xc, rm;
+        fp_sqr(z2, acc.z);
+        fp_canon(xc, acc.x);
+        fp_mul(rm, rv, r2p);
+        fp_mul(lhs, rm, z2);
+        fp_canon(lhs, lhs);
+        accept = fe_eq(lhs, xc);
+        // R.x in [n, p): compare with r + n as well when r + n < p
+        fe rn;
+        u64 c = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            c = (u64)rv.v[k] + P256_N[k] + c;
+            rn.v[k] = lo32(c);
+            c >>= 32;
+        }
+        if (c == 0 && fe_lt(rn, P256_P)) {
+            fp_mul(rm, rn, r2p);
+            fp_mul(lhs, rm, z2);
+            fp_canon(lhs, lhs);
+            accept = accept || fe_eq(lhs, xc);
+        }
+    }
+    if (active) {
+        if (exc && valid) {
+            const uint32_t slot = atomicAdd(work, 1u);
+            work[1 + slot] = gid;
+        } else {
+            ok[gid] = (valid && accept) ? 1 : 0;
+        }
+    }
 }
 
 }  // namespace sbft
 
+// Workspace: work[0] = count of flagged tuples, work[1..n] = their indices. The counter is
+// zeroed on the stream before the lean kernel; the fixup grid reads it on the device, so
+// the whole sequence stays asynchronous.
 extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                        const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
-                                       uint32_t n, hipStream_t stream) {
+                                       uint32_t n, uint32_t* d_work, hipStream_t stream) {
     if (n == 0) return 0;
+    if (hipMemsetAsync(d_work, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     const unsigned threads = 256;
     const unsigned blocks = (n + threads - 1) / threads;
     hipLaunchKernelGGL(sbft::p256_verify_kernel, dim3(blocks), dim3(threads), 0, stream, d_digest, d_r,
-                       d_s, d_qx, d_qy, d_ok, n);
+                       d_s, d_qx, d_qy, d_ok, n, d_work);
+    const unsigned fix_blocks = blocks < 64 ? blocks : 64;
+    hipLaunchKernelGGL(sbft::p256_verify_fixup_kernel, dim3(fix_blocks), dim3(threads), 0, stream,
+                       d_digest, d_r, d_s, d_qx, d_qy, d_ok, (const uint32_t*)d_work);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

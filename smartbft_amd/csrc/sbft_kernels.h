@@ -6,9 +6,11 @@
 
 extern "C" {
 // P-256 verify of n SoA tuples (32-byte big-endian fields) -> n verdict bytes.
+// d_work: device workspace of sbft_verify_work_bytes(n) bytes, private to the stream.
 int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                             const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok, uint32_t n,
-                            hipStream_t stream);
+                            uint32_t* d_work, hipStream_t stream);
+static inline size_t sbft_verify_work_bytes(size_t n) { return 4 * (n + 1); }
 // SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable >= 68 bytes
 // past its last message (funnel over-read). Digests are 32-byte big-endian.
 int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,

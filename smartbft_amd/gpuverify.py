@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsbft_gpuverify.so")
+LIB_PATH = os.environ.get("SBFT_GV_LIB") or os.path.join(_HERE, "libsbft_gpuverify.so")
 
 EXPORTS = [
     "sbft_gv_init", "sbft_gv_destroy", "sbft_gv_device_count", "sbft_gv_strerror",
