@@ -102,6 +102,11 @@ int sbft_gv_sign_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_d, const v
                           const void* d_digest, size_t n, void* d_qx, void* d_qy, void* d_r,
                           void* d_s, void* d_status, void* stream);
 
+/* Element-wise self-test of the device primitives (diagnostics; op codes in
+ * smartbft_amd/csrc/p256_selftest.hip). a, b, out: n x 32 bytes big-endian. */
+int sbft_gv_selftest_field(sbft_gv_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, size_t n,
+                           uint8_t* out);
+
 /* Go-semantics host helpers (no GPU). */
 void sbft_gv_normalize_hash(const uint8_t* hash, size_t len, uint8_t out32[32]);
 /* Big-endian magnitude of arbitrary length -> 32 bytes; returns 0 if it needs > 256 bits. */

@@ -349,6 +349,20 @@ int enqueue_sign(const Chunk& c, const uint8_t* d, const uint8_t* k, const uint8
     return SBFT_GV_OK;
 }
 
+int enqueue_selftest(const Chunk& c, int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
+    Slot* sl = c.slot;
+    const size_t f = align_up(32 * c.count, 256);
+    HIPCHK(hipSetDevice(sl->device));
+    int rc = sl->reserve(3 * f);
+    if (rc) return rc;
+    uint8_t* d = sl->dbuf;
+    HIPCHK(hipMemcpyAsync(d, a + 32 * c.begin, 32 * c.count, hipMemcpyHostToDevice, sl->stream));
+    HIPCHK(hipMemcpyAsync(d + f, b + 32 * c.begin, 32 * c.count, hipMemcpyHostToDevice, sl->stream));
+    if (sbft_launch_selftest(op, d, d + f, d + 2 * f, (uint32_t)c.count, sl->stream)) return SBFT_GV_ELAUNCH;
+    HIPCHK(hipMemcpyAsync(out + 32 * c.begin, d + 2 * f, 32 * c.count, hipMemcpyDeviceToHost, sl->stream));
+    return SBFT_GV_OK;
+}
+
 template <class F>
 int run_chunks(sbft_gv_ctx* ctx, size_t n, F&& enqueue) {
     std::vector<Chunk> chunks = plan(ctx, n);
@@ -386,6 +400,14 @@ int sbft_gv_sign_p256(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, cons
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
         return enqueue_sign(c, d, k, digest, qx, qy, r, s, status);
     });
+}
+
+int sbft_gv_selftest_field(sbft_gv_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, size_t n,
+                           uint8_t* out) {
+    if (!ctx) return SBFT_GV_EINVAL;
+    if (n == 0) return SBFT_GV_OK;
+    if (!a || !b || !out || op < 0 || op > 9 || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    return run_chunks(ctx, n, [&](const Chunk& c, size_t) { return enqueue_selftest(c, op, a, b, out); });
 }
 
 int sbft_gv_sha256(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, const uint64_t* off,

@@ -40,6 +40,15 @@ SBFT_DEV void madc(u64& acc, u32& c2, u32 a, u32 b) {
         : "v"(a), "v"(b)
         : "vcc");
 }
+// acc += a*b, c2 = carry-out (first capture of a column: no zero-initialised c2 needed)
+SBFT_DEV void madc_first(u64& acc, u32& c2, u32 a, u32 b) {
+    u64 cc;
+    asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
+        "v_addc_co_u32 %2, vcc, 0, 0, %1"
+        : "+v"(acc), "=&s"(cc), "=v"(c2)
+        : "v"(a), "v"(b)
+        : "vcc");
+}
 // acc + x (x zero-extended), one instruction
 SBFT_DEV u64 mad1(u32 x, u64 acc) {
     u64 r, cc;
@@ -67,18 +76,19 @@ SBFT_DEV void mul512(u32 t[16], const fe& a, const fe& b) {
     u32 c2 = 0;
 #pragma unroll
     for (int k = 0; k < 15; ++k) {
-        bool first = true;
+        int nprod = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int j = k - i;
             if (j < 0 || j > 7) continue;
-            if (first) {
-                acc += (u64)a.v[i] * b.v[j];  // acc < 2^40 here: cannot overflow
-                first = false;
-            } else {
-                madc(acc, c2, a.v[i], b.v[j]);
-            }
+            // The carry-in can reach ~2^35, so even a column's first product may carry out
+            // (limbs near 2^32-1): every product captures its carry.
+            if (nprod == 0 && k == 0) acc = (u64)a.v[i] * b.v[j];
+            else if (nprod == 0) madc_first(acc, c2, a.v[i], b.v[j]);
+            else madc(acc, c2, a.v[i], b.v[j]);
+            ++nprod;
         }
+        if (nprod == 1 && k == 0) c2 = 0;
         t[k] = lo32(acc);
         acc = (acc >> 32) | ((u64)c2 << 32);
         c2 = 0;
@@ -96,18 +106,17 @@ SBFT_DEV void sqr512(u32 t[16], const fe& a) {
     x[0] = 0;
 #pragma unroll
     for (int k = 1; k < 14; ++k) {
-        bool first = true;
+        int nprod = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int j = k - i;
             if (j <= i || j > 7) continue;
-            if (first) {
-                acc += (u64)a.v[i] * a.v[j];
-                first = false;
-            } else {
-                madc(acc, c2, a.v[i], a.v[j]);
-            }
+            if (nprod == 0 && k == 1) acc = (u64)a.v[i] * a.v[j];
+            else if (nprod == 0) madc_first(acc, c2, a.v[i], a.v[j]);
+            else madc(acc, c2, a.v[i], a.v[j]);
+            ++nprod;
         }
+        if (nprod == 1 && k == 1) c2 = 0;
         x[k] = lo32(acc);
         acc = (acc >> 32) | ((u64)c2 << 32);
         c2 = 0;
@@ -140,6 +149,113 @@ SBFT_DEV void sqr512(u32 t[16], const fe& a) {
         t[2 * k + 1] = hi;
         cin = c1 | c3;
     }
+}
+
+
+// ------------------------------------------------------ carry-chain primitives
+// Explicit v_add_co / v_addc / v_sub_co / v_subb chains: the compiler's own lowering of
+// 64-bit C arithmetic costs ~4 instructions per limb here, these cost 1. Carries and
+// borrows leave as wave lane masks (SGPR pairs), so "any lane needs a correction" is a
+// plain scalar test.
+typedef u64 lmask;
+
+// r += b (in place), returns the carry-out lane mask
+SBFT_DEV lmask add8_ip(fe& r, const fe& b) {
+    lmask c;
+    asm("v_add_co_u32 %0, vcc, %0, %9\n\t"
+        "v_addc_co_u32 %1, vcc, %1, %10, vcc\n\t"
+        "v_addc_co_u32 %2, vcc, %2, %11, vcc\n\t"
+        "v_addc_co_u32 %3, vcc, %3, %12, vcc\n\t"
+        "v_addc_co_u32 %4, vcc, %4, %13, vcc\n\t"
+        "v_addc_co_u32 %5, vcc, %5, %14, vcc\n\t"
+        "v_addc_co_u32 %6, vcc, %6, %15, vcc\n\t"
+        "v_addc_co_u32 %7, vcc, %7, %16, vcc\n\t"
+        "s_mov_b64 %8, vcc"
+        : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+          "+v"(r.v[6]), "+v"(r.v[7]), "=s"(c)
+        : "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]),
+          "v"(b.v[7])
+        : "vcc");
+    return c;
+}
+// r -= b (in place), returns the borrow-out lane mask
+SBFT_DEV lmask sub8_ip(fe& r, const fe& b) {
+    lmask c;
+    asm("v_sub_co_u32 %0, vcc, %0, %9\n\t"
+        "v_subb_co_u32 %1, vcc, %1, %10, vcc\n\t"
+        "v_subb_co_u32 %2, vcc, %2, %11, vcc\n\t"
+        "v_subb_co_u32 %3, vcc, %3, %12, vcc\n\t"
+        "v_subb_co_u32 %4, vcc, %4, %13, vcc\n\t"
+        "v_subb_co_u32 %5, vcc, %5, %14, vcc\n\t"
+        "v_subb_co_u32 %6, vcc, %6, %15, vcc\n\t"
+        "v_subb_co_u32 %7, vcc, %7, %16, vcc\n\t"
+        "s_mov_b64 %8, vcc"
+        : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+          "+v"(r.v[6]), "+v"(r.v[7]), "=s"(c)
+        : "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]),
+          "v"(b.v[7])
+        : "vcc");
+    return c;
+}
+// r -= (lane in mask ? p : 0), in place; returns the borrow-out lane mask.
+// p = [ffffffff ffffffff ffffffff 0 0 0 1 ffffffff] (little-endian limbs).
+SBFT_DEV lmask subp_ip(fe& r, lmask mask) {
+    lmask c;
+    u32 m, t;
+    asm("v_cndmask_b32 %8, 0, -1, %11\n\t"
+        "v_cndmask_b32 %9, 0, 1, %11\n\t"
+        "v_sub_co_u32 %0, vcc, %0, %8\n\t"
+        "v_subb_co_u32 %1, vcc, %1, %8, vcc\n\t"
+        "v_subb_co_u32 %2, vcc, %2, %8, vcc\n\t"
+        "v_subb_co_u32 %3, vcc, %3, 0, vcc\n\t"
+        "v_subb_co_u32 %4, vcc, %4, 0, vcc\n\t"
+        "v_subb_co_u32 %5, vcc, %5, 0, vcc\n\t"
+        "v_subb_co_u32 %6, vcc, %6, %9, vcc\n\t"
+        "v_subb_co_u32 %7, vcc, %7, %8, vcc\n\t"
+        "s_mov_b64 %10, vcc"
+        : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+          "+v"(r.v[6]), "+v"(r.v[7]), "=&v"(m), "=&v"(t), "=s"(c)
+        : "s"(mask)
+        : "vcc");
+    return c;
+}
+// r += (lane in mask ? p : 0), in place; returns the carry-out lane mask.
+SBFT_DEV lmask addp_ip(fe& r, lmask mask) {
+    lmask c;
+    u32 m, t;
+    asm("v_cndmask_b32 %8, 0, -1, %11\n\t"
+        "v_cndmask_b32 %9, 0, 1, %11\n\t"
+        "v_add_co_u32 %0, vcc, %0, %8\n\t"
+        "v_addc_co_u32 %1, vcc, %1, %8, vcc\n\t"
+        "v_addc_co_u32 %2, vcc, %2, %8, vcc\n\t"
+        "v_addc_co_u32 %3, vcc, %3, 0, vcc\n\t"
+        "v_addc_co_u32 %4, vcc, %4, 0, vcc\n\t"
+        "v_addc_co_u32 %5, vcc, %5, 0, vcc\n\t"
+        "v_addc_co_u32 %6, vcc, %6, %9, vcc\n\t"
+        "v_addc_co_u32 %7, vcc, %7, %8, vcc\n\t"
+        "s_mov_b64 %10, vcc"
+        : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+          "+v"(r.v[6]), "+v"(r.v[7]), "=&v"(m), "=&v"(t), "=s"(c)
+        : "s"(mask)
+        : "vcc");
+    return c;
+}
+// r -= top * p for a per-lane top in {0, 1} (Montgomery reduction tail).
+SBFT_DEV void subp_top(fe& r, u32 top) {
+    u32 m;
+    asm("v_sub_u32 %8, 0, %9\n\t"
+        "v_sub_co_u32 %0, vcc, %0, %8\n\t"
+        "v_subb_co_u32 %1, vcc, %1, %8, vcc\n\t"
+        "v_subb_co_u32 %2, vcc, %2, %8, vcc\n\t"
+        "v_subb_co_u32 %3, vcc, %3, 0, vcc\n\t"
+        "v_subb_co_u32 %4, vcc, %4, 0, vcc\n\t"
+        "v_subb_co_u32 %5, vcc, %5, 0, vcc\n\t"
+        "v_subb_co_u32 %6, vcc, %6, %9, vcc\n\t"
+        "v_subb_co_u32 %7, vcc, %7, %8, vcc"
+        : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+          "+v"(r.v[6]), "+v"(r.v[7]), "=&v"(m)
+        : "v"(top)
+        : "vcc");
 }
 
 // ------------------------------------------------------------------ mod p
@@ -179,17 +295,10 @@ SBFT_DEV void fp_redc(fe& r, const u32 t[16]) {
     o[6] = lo32(c);
     c = madi1(hi32(c), mad1(m7, z64(t[15])));
     o[7] = lo32(c);
-    // value = o + top*2^256 < 2^256 + p; subtract top*p (masked constant p).
-    const u32 top = hi32(c);
-    const u32 mask = 0u - top;
-    const u32 pm[8] = {mask, mask, mask, 0, 0, 0, top, mask};
-    u64 b = 0;
+    // value = o + top*2^256 < 2^256 + p; subtract top*p.
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const u64 d = (u64)o[k] - pm[k] - b;
-        r.v[k] = lo32(d);
-        b = d >> 63;
-    }
+    for (int k = 0; k < 8; ++k) r.v[k] = o[k];
+    subp_top(r, hi32(c));
 }
 
 SBFT_DEV void fp_mul(fe& r, const fe& a, const fe& b) {
@@ -229,46 +338,25 @@ SBFT_DEV u32 sub_masked_p(fe& r, const fe& a, u32 mask) {
     return (u32)b;
 }
 
-// a + b mod p, inputs and output in [0, 2^256).
+// a + b mod p, inputs and output in [0, 2^256): 8-limb add, subtract p on carry-out, and a
+// second subtraction in the (rare) case the first did not borrow (value was >= 2^256 + p).
 SBFT_DEV void fp_add(fe& r, const fe& a, const fe& b) {
-    u64 c = 0;
-    fe s;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        c = (u64)a.v[k] + b.v[k] + c;
-        s.v[k] = lo32(c);
-        c >>= 32;
-    }
-    const u32 carry = (u32)c;
-    const u32 borrow = sub_masked_p(r, s, 0u - carry);
-    // carry and no borrow: the value was >= 2^256 + p; subtract p once more (rare).
-    const u32 again = carry & (borrow ^ 1u);
-    if (__builtin_expect(__any(again), 0)) {
-        // r + (2^256 - p) == r - p (mod 2^256) for the lanes that need it
-        fe t;
-        sub_masked_p(t, r, 0u - again);
-        r = t;
-    }
+    fe s = a;
+    const lmask c = add8_ip(s, b);
+    const lmask bw = subp_ip(s, c);
+    const lmask again = c & ~bw;
+    if (__builtin_expect(again != 0, 0)) subp_ip(s, again);
+    r = s;
 }
-// a - b mod p, inputs and output in [0, 2^256).
+// a - b mod p, inputs and output in [0, 2^256): add p back on borrow, twice if b >= p made
+// a - b + p still negative (rare).
 SBFT_DEV void fp_sub(fe& r, const fe& a, const fe& b) {
-    u64 bw = 0;
-    fe d;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const u64 x = (u64)a.v[k] - b.v[k] - bw;
-        d.v[k] = lo32(x);
-        bw = x >> 63;
-    }
-    const u32 borrow = (u32)bw;
-    const u32 carry = add_masked_p(r, d, 0u - borrow);
-    // borrow and no carry: a - b + p is still negative (b >= p); add p again (rare).
-    const u32 again = borrow & (carry ^ 1u);
-    if (__builtin_expect(__any(again), 0)) {
-        fe t;
-        add_masked_p(t, r, 0u - again);
-        r = t;
-    }
+    fe d = a;
+    const lmask bw = sub8_ip(d, b);
+    const lmask c = addp_ip(d, bw);
+    const lmask again = bw & ~c;
+    if (__builtin_expect(again != 0, 0)) addp_ip(d, again);
+    r = d;
 }
 // [0, 2^256) -> [0, p)
 SBFT_DEV void fp_canon(fe& r, const fe& a) {
@@ -324,28 +412,34 @@ SBFT_DEV void fn_mul(fe& r, const fe& a, const fe& b) {
     u32 c2 = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
+        int nprod = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int j = k - i;
             if (j < 0 || j > 7) continue;
-            madc(acc, c2, a.v[i], b.v[j]);
+            if (nprod == 0 && k == 0) acc = (u64)a.v[i] * b.v[j];
+            else if (nprod == 0) madc_first(acc, c2, a.v[i], b.v[j]);
+            else madc(acc, c2, a.v[i], b.v[j]);
+            ++nprod;
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int j = k - i;
             if (i >= k || j < 0 || j > 7) continue;
-            madc(acc, c2, m[i], P256_N[j]);
+            if (nprod == 0) madc_first(acc, c2, m[i], P256_N[j]);
+            else madc(acc, c2, m[i], P256_N[j]);
+            ++nprod;
         }
         if (k < 8) {
             m[k] = lo32(acc) * P256_N_PRIME;
-            madc(acc, c2, m[k], P256_N[0]);  // low word becomes 0
+            if (nprod == 0) madc_first(acc, c2, m[k], P256_N[0]);  // low word becomes 0
+            else madc(acc, c2, m[k], P256_N[0]);
+            ++nprod;
         } else {
             o[k - 8] = lo32(acc);
         }
-        if (k < 15) {
-            acc = (acc >> 32) | ((u64)c2 << 32);
-            c2 = 0;
-        }
+        if (nprod == 0) c2 = 0;
+        if (k < 15) acc = (acc >> 32) | ((u64)c2 << 32);  // next column's first product resets c2
     }
     // value = o + hi*2^256 (hi in {0,1}); subtract n once if hi.
     const u32 top = hi32(acc);

@@ -10,7 +10,10 @@ extern "C" {
 int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                             const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok, uint32_t n,
                             uint32_t* d_work, hipStream_t stream);
-static inline size_t sbft_verify_work_bytes(size_t n) { return 4 * (n + 1); }
+static inline size_t sbft_verify_work_bytes(size_t n) { return 4 * (n + 1); // Element-wise primitive self-test (see p256_selftest.hip for op codes).
+int sbft_launch_selftest(int op, const uint8_t* d_a, const uint8_t* d_b, uint8_t* d_out, uint32_t n,
+                         hipStream_t stream);
+}
 // SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable >= 68 bytes
 // past its last message (funnel over-read). Digests are 32-byte big-endian.
 int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
@@ -19,4 +22,7 @@ int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint3
 int sbft_launch_p256_sign(const uint8_t* d_d, const uint8_t* d_k, const uint8_t* d_e, uint8_t* d_qx,
                           uint8_t* d_qy, uint8_t* d_r, uint8_t* d_s, uint8_t* d_status, uint32_t n,
                           hipStream_t stream);
+// Element-wise primitive self-test (see p256_selftest.hip for op codes).
+int sbft_launch_selftest(int op, const uint8_t* d_a, const uint8_t* d_b, uint8_t* d_out, uint32_t n,
+                         hipStream_t stream);
 }

@@ -19,6 +19,7 @@ EXPORTS = [
     "sbft_gv_verify_p256", "sbft_gv_sha256", "sbft_gv_sha256_verify_p256",
     "sbft_gv_verify_p256_dev", "sbft_gv_sha256_dev", "sbft_gv_sha256_verify_p256_dev",
     "sbft_gv_normalize_hash", "sbft_gv_normalize_scalar", "sbft_gv_sign_p256", "sbft_gv_sign_p256_dev",
+    "sbft_gv_selftest_field",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -65,6 +66,7 @@ def load_library():
                                                 [ctypes.c_size_t, _vp, _vp, _vp]
     L.sbft_gv_sign_p256.argtypes = [_vp] + [_u8p] * 3 + [ctypes.c_size_t] + [_u8p] * 5
     L.sbft_gv_sign_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 3 + [ctypes.c_size_t] + [_vp] * 6
+    L.sbft_gv_selftest_field.argtypes = [_vp, ctypes.c_int, _u8p, _u8p, ctypes.c_size_t, _u8p]
     L.sbft_gv_normalize_hash.argtypes = [_u8p, ctypes.c_size_t, _u8p]
     L.sbft_gv_normalize_hash.restype = None
     L.sbft_gv_normalize_scalar.argtypes = [_u8p, ctypes.c_size_t, _u8p]
@@ -147,6 +149,14 @@ class GpuVerifier:
         self._check(self.L.sbft_gv_sign_p256(self.ctx, *[_p(a) for a in ins], n,
                                              *[_p(a) for a in outs], _p(st)), "sbft_gv_sign_p256")
         return (*outs, st)
+
+    def selftest_field(self, op: int, a, b) -> np.ndarray:
+        n = len(a)
+        a, b = _soa(a, n), _soa(b, n)
+        out = np.zeros((n, 32), dtype=np.uint8)
+        self._check(self.L.sbft_gv_selftest_field(self.ctx, op, _p(a), _p(b), n, _p(out)),
+                    "sbft_gv_selftest_field")
+        return out
 
     def sign_dev(self, d_d, d_k, d_e, d_qx, d_qy, d_r, d_s, d_status, stream=None):
         n = d_status.numel()
