@@ -1,0 +1,143 @@
+/*
+ * sbft_verifier.h — C ABI of the plugin-level mirror of SmartBFT's api.Verifier / api.Signer
+ * (pkg/api/dependencies.go:46-71), implemented in C++ (smartbft_amd/csrc/verifier.cpp) on top
+ * of the GPU engine (sbft_gpuverify.h). Go is absent from this image and from the GPU box,
+ * so the host side is C++ with the same method set, argument meaning and error behaviour; the
+ * cgo plugin a Go maintainer would add binds these symbols.
+ *
+ * Formats (the reference defines none):
+ *  signed request  "SBR1" | u16 len | client_id | u16 len | req_id | u32 len | payload |
+ *                  65-byte SEC1 uncompressed public key | 64-byte r||s
+ *                  signature over SHA-256(every byte before r||s); integers little-endian
+ *  proposal payload u32 count | count x (u32 len | signed request)
+ *  consenter Msg   "SBC1" | u16 len | proposal digest (hex, Proposal.Digest()) | u32 len | aux
+ *                  Signature.Value = r||s over SHA-256(Msg) by consenter ID's registered key
+ *
+ * Error convention (as the library uses the Go interface, view.go:388,637,840): a call returns
+ * 0 on success, SBFT_V_EVERIFY (-10) when verification rejects, other negative codes on bad
+ * arguments / infrastructure; err (if not NULL) receives a NUL-terminated message whose text
+ * follows the reference's log lines where one exists. Thread-safe: every entry point may be
+ * called concurrently (view.go:539-541 verifies q-1 votes from q-1 goroutines).
+ */
+#ifndef SBFT_VERIFIER_H
+#define SBFT_VERIFIER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "sbft_gpuverify.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBFT_V_EVERIFY (-10) /* a signature or binding check failed */
+#define SBFT_V_EFORMAT (-11) /* malformed request / payload / message */
+#define SBFT_V_EKEY (-12)    /* unknown consenter id */
+#define SBFT_V_ESPACE (-13)  /* caller's output buffer too small */
+
+typedef struct sbft_verifier sbft_verifier;
+
+/* Wire structs mirroring pkg/types/types.go:18-48. Byte slices are borrowed for the call. */
+typedef struct sbft_proposal {
+    const uint8_t* payload;
+    size_t payload_len;
+    const uint8_t* header;
+    size_t header_len;
+    const uint8_t* metadata;
+    size_t metadata_len;
+    int64_t verification_sequence;
+} sbft_proposal;
+
+typedef struct sbft_signature {
+    uint64_t id;
+    const uint8_t* value;
+    size_t value_len;
+    const uint8_t* msg;
+    size_t msg_len;
+} sbft_signature;
+
+/* A verifier bound to an engine context (not owned) and a verification sequence. */
+sbft_verifier* sbft_verifier_new(sbft_gv_ctx* ctx, uint64_t verification_sequence);
+void sbft_verifier_free(sbft_verifier* v);
+/* Consenter key registry (SEC1 uncompressed, 65 bytes). */
+int sbft_verifier_add_consenter(sbft_verifier* v, uint64_t id, const uint8_t pubkey65[65]);
+/* api.Verifier.VerificationSequence (dependencies.go:65-66). */
+uint64_t sbft_verifier_verification_sequence(const sbft_verifier* v);
+void sbft_verifier_set_verification_sequence(sbft_verifier* v, uint64_t seq);
+
+/* api.Verifier.VerifyProposal (dependencies.go:56-57; called view.go:555): one fused GPU
+ * launch (SHA-256 of every request body + P-256 verify). On success writes *count RequestInfo
+ * pairs into infos as "client_id\0id\0" records (infos_cap bytes); bad_index (may be NULL)
+ * receives the first failing request index on SBFT_V_EVERIFY. */
+int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char* infos,
+                                  size_t infos_cap, size_t* count, int64_t* bad_index, char* err,
+                                  size_t err_cap);
+/* api.Verifier.RequestsFromProposal (dependencies.go:67-68): parse only, same output layout. */
+int sbft_verifier_requests_from_proposal(sbft_verifier* v, const sbft_proposal* p, char* infos,
+                                         size_t infos_cap, size_t* count);
+/* api.Verifier.VerifyRequest (dependencies.go:58-59): "client_id\0id\0" into info. */
+int sbft_verifier_verify_request(sbft_verifier* v, const uint8_t* req, size_t len, char* info,
+                                 size_t info_cap, char* err, size_t err_cap);
+/* api.Verifier.VerifyConsenterSig (dependencies.go:60-62): on success copies the auxiliary
+ * data into aux (aux_cap bytes) and sets *aux_len. */
+int sbft_verifier_verify_consenter_sig(sbft_verifier* v, const sbft_signature* s, const sbft_proposal* p,
+                                       uint8_t* aux, size_t aux_cap, size_t* aux_len, char* err,
+                                       size_t err_cap);
+/* Batching hook (new): n consenter signatures over one proposal in one GPU
+ * launch. status[i] = 0 ok, else the per-signature error code; auxes are not returned (use
+ * sbft_verifier_auxiliary_data on the accepted messages). Returns 0 if the call ran. */
+int sbft_verifier_verify_consenter_sigs(sbft_verifier* v, const sbft_signature* sigs, size_t n,
+                                        const sbft_proposal* p, int32_t* status);
+/* api.Verifier.VerifySignature (dependencies.go:63-64). */
+int sbft_verifier_verify_signature(sbft_verifier* v, const sbft_signature* s, char* err, size_t err_cap);
+/* api.Verifier.AuxiliaryData (dependencies.go:69-70): returns the aux length, or -1 if msg
+ * is malformed; copies min(len, aux_cap) bytes. */
+int64_t sbft_verifier_auxiliary_data(const uint8_t* msg, size_t msg_len, uint8_t* aux, size_t aux_cap);
+
+/* types.Proposal.Digest (pkg/types/types.go:50-69): hex(SHA-256(ASN.1 DER of the proposal)),
+ * 64 characters + NUL into out65. */
+void sbft_proposal_digest(const sbft_proposal* p, char out65[65]);
+/* Host SHA-256 (no GPU), used for Proposal.Digest and small messages. */
+void sbft_sha256_host(const uint8_t* msg, size_t len, uint8_t out[32]);
+
+/* api.Signer mirror (dependencies.go:46-52) for one node key. The nonce is RFC 6979
+ * (HMAC-SHA-256), so signatures are deterministic. */
+typedef struct sbft_signer sbft_signer;
+sbft_signer* sbft_signer_new(sbft_gv_ctx* ctx, uint64_t id, const uint8_t priv32[32]);
+void sbft_signer_free(sbft_signer* s);
+int sbft_signer_public_key(const sbft_signer* s, uint8_t pubkey65[65]);
+/* Signer.Sign: 64-byte r||s over SHA-256(data). */
+int sbft_signer_sign(sbft_signer* s, const uint8_t* data, size_t len, uint8_t sig64[64]);
+/* Signer.SignProposal: builds Msg = "SBC1"|digest|aux into msg (msg_cap) and signs it. */
+int sbft_signer_sign_proposal(sbft_signer* s, const sbft_proposal* p, const uint8_t* aux, size_t aux_len,
+                              uint8_t* msg, size_t msg_cap, size_t* msg_len, uint8_t sig64[64]);
+/* Build a signed request (format above) for the given client key: returns its length or a
+ * negative code (test/bench helper; a client library's job). */
+int64_t sbft_make_request(sbft_signer* client, const char* client_id, const char* req_id,
+                          const uint8_t* payload, size_t payload_len, uint8_t* out, size_t out_cap);
+
+/* ---- batching hook: mirrors of the library's call sites (internal/bft/view.go) ----
+ * computeQuorum (util.go:176-180): f = (n-1)/3, q = ceil((n+f+1)/2). */
+void sbft_compute_quorum(uint64_t n, int* q, int* f);
+/* View.verifyPrevCommitSignatures (view.go:606-647) with one GPU launch for all signatures.
+ * Skips (returns 0, *skipped = 1) when prev->verification_sequence != curr_vseq
+ * (view.go:614-618). On failure returns SBFT_V_EVERIFY with err =
+ * "failed verifying consenter signature of <id>: <reason>" for the first failing signer. */
+int sbft_verify_prev_commit_signatures(sbft_verifier* v, const sbft_signature* sigs, size_t n,
+                                       const sbft_proposal* prev, uint64_t curr_vseq, int* skipped,
+                                       char* err, size_t err_cap);
+/* View.processCommits + voteVerifier.verifyVote (view.go:519-551, 820-849) with one GPU launch
+ * per batch of arrived votes: votes whose digest differs from the proposal's are dropped
+ * ("Got wrong digest at processCommits"), duplicates by signer are ignored (voteSet.registerVote,
+ * util.go:123-136), the rest are verified together; valid_idx receives the indices of valid
+ * votes in arrival order, at most `need` (= quorum - 1). log receives one line per rejected
+ * vote ("Couldn't verify <id>'s signature: <reason>", view.go:840). */
+int sbft_collect_commits(sbft_verifier* v, const sbft_signature* votes, const char* const* vote_digests,
+                         size_t n, const sbft_proposal* p, size_t need, size_t* valid_idx,
+                         size_t* n_valid, char* log, size_t log_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

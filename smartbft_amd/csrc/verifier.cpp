@@ -1,0 +1,809 @@
+// verifier.cpp — plugin-level mirror of SmartBFT's api.Verifier and api.Signer
+// (pkg/api/dependencies.go:46-71) on top of the GPU engine (include/sbft_verifier.h).
+//
+// Every signature check goes through the engine: a proposal is ONE fused launch (SHA-256 of
+// every request body + P-256 verify, view.go:555), a batch of consenter signatures is ONE
+// launch (view.go:631, :834). The host side only parses formats, checks bindings and builds
+// the structure-of-arrays batches; there is no CPU verification path.
+#include "../../include/sbft_verifier.h"
+
+#include <array>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+// ------------------------------------------------------------------ SHA-256 (host)
+const uint32_t K256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+struct Sha256 {
+    uint32_t h[8];
+    uint8_t buf[64];
+    uint64_t total = 0;
+    size_t fill = 0;
+    Sha256() {
+        static const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                       0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+        std::memcpy(h, iv, sizeof h);
+    }
+    void block(const uint8_t* p) {
+        uint32_t w[64];
+        for (int i = 0; i < 16; ++i)
+            w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+        for (int i = 16; i < 64; ++i)
+            w[i] = w[i - 16] + (rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3)) + w[i - 7] +
+                   (rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10));
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
+        for (int i = 0; i < 64; ++i) {
+            const uint32_t t1 = k + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + K256[i] + w[i];
+            const uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+            k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
+    }
+    void update(const uint8_t* p, size_t n) {
+        total += n;
+        while (n) {
+            if (fill == 0 && n >= 64) {
+                block(p);
+                p += 64;
+                n -= 64;
+                continue;
+            }
+            const size_t take = std::min(n, 64 - fill);
+            std::memcpy(buf + fill, p, take);
+            fill += take;
+            p += take;
+            n -= take;
+            if (fill == 64) {
+                block(buf);
+                fill = 0;
+            }
+        }
+    }
+    void final(uint8_t out[32]) {
+        const uint64_t bits = total * 8;
+        const uint8_t pad = 0x80;
+        update(&pad, 1);
+        const uint8_t zero = 0;
+        while (fill != 56) update(&zero, 1);
+        uint8_t lenb[8];
+        for (int i = 0; i < 8; ++i) lenb[i] = (uint8_t)(bits >> (56 - 8 * i));
+        update(lenb, 8);
+        for (int i = 0; i < 8; ++i) {
+            out[4 * i] = (uint8_t)(h[i] >> 24);
+            out[4 * i + 1] = (uint8_t)(h[i] >> 16);
+            out[4 * i + 2] = (uint8_t)(h[i] >> 8);
+            out[4 * i + 3] = (uint8_t)h[i];
+        }
+    }
+};
+
+void sha256(const uint8_t* p, size_t n, uint8_t out[32]) {
+    Sha256 s;
+    s.update(p, n);
+    s.final(out);
+}
+
+// HMAC-SHA-256 over the concatenation of up to four parts (RFC 2104).
+void hmac_sha256(const uint8_t key[32], std::initializer_list<std::pair<const uint8_t*, size_t>> parts,
+                 uint8_t out[32]) {
+    uint8_t ipad[64], opad[64];
+    for (int i = 0; i < 64; ++i) {
+        const uint8_t k = i < 32 ? key[i] : 0;
+        ipad[i] = k ^ 0x36;
+        opad[i] = k ^ 0x5c;
+    }
+    uint8_t inner[32];
+    Sha256 a;
+    a.update(ipad, 64);
+    for (auto& pr : parts) a.update(pr.first, pr.second);
+    a.final(inner);
+    Sha256 b;
+    b.update(opad, 64);
+    b.update(inner, 32);
+    b.final(out);
+}
+
+const uint8_t N_BE[32] = {0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x00, 0xff, 0xff, 0xff,
+                          0xff, 0xff, 0xff, 0xff, 0xff, 0xbc, 0xe6, 0xfa, 0xad, 0xa7, 0x17,
+                          0x9e, 0x84, 0xf3, 0xb9, 0xca, 0xc2, 0xfc, 0x63, 0x25, 0x51};
+
+int cmp_be32(const uint8_t* a, const uint8_t* b) { return std::memcmp(a, b, 32); }
+bool is_zero32(const uint8_t* a) {
+    for (int i = 0; i < 32; ++i)
+        if (a[i]) return false;
+    return true;
+}
+void sub_be32(uint8_t* a, const uint8_t* b) {  // a -= b (mod 2^256)
+    int borrow = 0;
+    for (int i = 31; i >= 0; --i) {
+        const int d = (int)a[i] - b[i] - borrow;
+        a[i] = (uint8_t)d;
+        borrow = d < 0;
+    }
+}
+
+// RFC 6979 3.2 deterministic nonce for P-256 with HMAC-SHA-256 (qlen = hlen = 256).
+// `attempt` > 0 continues the generator (step h.3) past nonces that produced r or s = 0.
+void rfc6979_nonce(const uint8_t x[32], const uint8_t h1[32], int attempt, uint8_t k_out[32]) {
+    uint8_t h[32];
+    std::memcpy(h, h1, 32);
+    if (cmp_be32(h, N_BE) >= 0) sub_be32(h, N_BE);  // bits2octets: bits2int(h1) mod q
+    uint8_t V[32], K[32];
+    std::memset(V, 0x01, 32);
+    std::memset(K, 0x00, 32);
+    const uint8_t z0 = 0x00, z1 = 0x01;
+    hmac_sha256(K, {{V, 32}, {&z0, 1}, {x, 32}, {h, 32}}, K);
+    hmac_sha256(K, {{V, 32}}, V);
+    hmac_sha256(K, {{V, 32}, {&z1, 1}, {x, 32}, {h, 32}}, K);
+    hmac_sha256(K, {{V, 32}}, V);
+    for (int found = 0;;) {
+        hmac_sha256(K, {{V, 32}}, V);
+        if (!is_zero32(V) && cmp_be32(V, N_BE) < 0 && found++ == attempt) {
+            std::memcpy(k_out, V, 32);
+            return;
+        }
+        hmac_sha256(K, {{V, 32}, {&z0, 1}}, K);
+        hmac_sha256(K, {{V, 32}}, V);
+    }
+}
+
+// ------------------------------------------------------------------ ASN.1 DER (Digest)
+void der_len(std::vector<uint8_t>& o, size_t n) {
+    if (n < 0x80) {
+        o.push_back((uint8_t)n);
+        return;
+    }
+    uint8_t tmp[8];
+    int k = 0;
+    while (n) {
+        tmp[k++] = (uint8_t)(n & 0xff);
+        n >>= 8;
+    }
+    o.push_back((uint8_t)(0x80 | k));
+    while (k) o.push_back(tmp[--k]);
+}
+void der_octets(std::vector<uint8_t>& o, const uint8_t* p, size_t n) {
+    o.push_back(0x04);
+    der_len(o, n);
+    if (n) o.insert(o.end(), p, p + n);
+}
+void der_int64(std::vector<uint8_t>& o, int64_t v) {
+    // minimal two's complement, as Go encoding/asn1 marshals int64
+    uint8_t b[8];
+    for (int i = 0; i < 8; ++i) b[i] = (uint8_t)((uint64_t)v >> (56 - 8 * i));
+    int start = 0;
+    while (start < 7 && ((b[start] == 0x00 && !(b[start + 1] & 0x80)) || (b[start] == 0xff && (b[start + 1] & 0x80))))
+        ++start;
+    o.push_back(0x02);
+    der_len(o, 8 - start);
+    o.insert(o.end(), b + start, b + 8);
+}
+
+// ------------------------------------------------------------------ formats
+struct Reader {
+    const uint8_t* p;
+    size_t n, pos = 0;
+    bool take(size_t k, const uint8_t*& out) {
+        if (n - pos < k) return false;
+        out = p + pos;
+        pos += k;
+        return true;
+    }
+    bool u16(uint32_t& v) {
+        const uint8_t* q;
+        if (!take(2, q)) return false;
+        v = (uint32_t)q[0] | (uint32_t)q[1] << 8;
+        return true;
+    }
+    bool u32(uint32_t& v) {
+        const uint8_t* q;
+        if (!take(4, q)) return false;
+        v = (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
+        return true;
+    }
+};
+
+struct Req {
+    std::string client_id, req_id;
+    size_t body_off = 0, body_len = 0;  // relative to the buffer handed to parse_request
+    const uint8_t* pub = nullptr;       // 65 bytes SEC1
+    const uint8_t* sig = nullptr;       // 64 bytes r||s
+};
+
+const char* REQ_MAGIC = "SBR1";
+const char* MSG_MAGIC = "SBC1";
+
+bool parse_request(const uint8_t* d, size_t len, size_t base, Req& out) {
+    Reader r{d, len};
+    const uint8_t* q;
+    uint32_t a, b, c;
+    if (!r.take(4, q) || std::memcmp(q, REQ_MAGIC, 4)) return false;
+    if (!r.u16(a) || !r.take(a, q)) return false;
+    out.client_id.assign((const char*)q, a);
+    if (!r.u16(b) || !r.take(b, q)) return false;
+    out.req_id.assign((const char*)q, b);
+    if (!r.u32(c) || !r.take(c, q)) return false;
+    if (!r.take(65, out.pub)) return false;
+    out.body_off = base;
+    out.body_len = r.pos;
+    if (!r.take(64, out.sig) || r.pos != len) return false;
+    return true;
+}
+
+bool parse_payload(const uint8_t* p, size_t len, std::vector<Req>& out) {
+    Reader r{p, len};
+    uint32_t count;
+    if (!r.u32(count)) return false;
+    if (count > len / 4) return false;
+    out.resize(count);
+    for (uint32_t i = 0; i < count; ++i) {
+        uint32_t l;
+        const uint8_t* q;
+        if (!r.u32(l)) return false;
+        const size_t at = r.pos;
+        if (!r.take(l, q)) return false;
+        if (!parse_request(q, l, at, out[i])) return false;
+    }
+    return r.pos == len;
+}
+
+struct Msg {
+    const uint8_t* digest = nullptr;
+    size_t digest_len = 0;
+    const uint8_t* aux = nullptr;
+    size_t aux_len = 0;
+};
+
+bool parse_msg(const uint8_t* m, size_t len, Msg& out) {
+    Reader r{m, len};
+    const uint8_t* q;
+    uint32_t a, b;
+    if (!m || !r.take(4, q) || std::memcmp(q, MSG_MAGIC, 4)) return false;
+    if (!r.u16(a) || !r.take(a, out.digest)) return false;
+    out.digest_len = a;
+    if (!r.u32(b) || !r.take(b, out.aux)) return false;
+    out.aux_len = b;
+    return r.pos == len;
+}
+
+void put_err(char* err, size_t cap, const char* fmt, ...) {
+    if (!err || !cap) return;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(err, cap, fmt, ap);
+    va_end(ap);
+}
+
+bool write_info(char*& w, char* end, const std::string& cid, const std::string& id) {
+    if ((size_t)(end - w) < cid.size() + id.size() + 2) return false;
+    std::memcpy(w, cid.data(), cid.size());
+    w += cid.size();
+    *w++ = 0;
+    std::memcpy(w, id.data(), id.size());
+    w += id.size();
+    *w++ = 0;
+    return true;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------- verifier
+struct sbft_verifier {
+    sbft_gv_ctx* ctx;
+    std::atomic<uint64_t> vseq;
+    std::shared_mutex keys_mu;
+    std::unordered_map<uint64_t, std::array<uint8_t, 64>> keys;  // x || y, big-endian
+    // Proposal.Digest memo (view.go:435,443,524 recompute it per proposal): exact-content key
+    std::mutex memo_mu;
+    struct Memo {
+        std::vector<uint8_t> payload, header, metadata;
+        int64_t vseq = 0;
+        char digest[65] = {0};
+        bool valid = false;
+    } memo[4];
+    int memo_next = 0;
+
+    void digest_of(const sbft_proposal* p, char out[65]) {
+        auto same = [](const std::vector<uint8_t>& v, const uint8_t* q, size_t n) {
+            return v.size() == n && (n == 0 || std::memcmp(v.data(), q, n) == 0);
+        };
+        {
+            std::lock_guard<std::mutex> g(memo_mu);
+            for (auto& m : memo)
+                if (m.valid && m.vseq == p->verification_sequence && same(m.payload, p->payload, p->payload_len) &&
+                    same(m.header, p->header, p->header_len) && same(m.metadata, p->metadata, p->metadata_len)) {
+                    std::memcpy(out, m.digest, 65);
+                    return;
+                }
+        }
+        sbft_proposal_digest(p, out);
+        std::lock_guard<std::mutex> g(memo_mu);
+        Memo& m = memo[memo_next];
+        memo_next = (memo_next + 1) % 4;
+        m.payload.assign(p->payload, p->payload + p->payload_len);
+        m.header.assign(p->header, p->header + p->header_len);
+        m.metadata.assign(p->metadata, p->metadata + p->metadata_len);
+        m.vseq = p->verification_sequence;
+        std::memcpy(m.digest, out, 65);
+        m.valid = true;
+    }
+
+    bool key_of(uint64_t id, std::array<uint8_t, 64>& k) {
+        std::shared_lock<std::shared_mutex> g(keys_mu);
+        auto it = keys.find(id);
+        if (it == keys.end()) return false;
+        k = it->second;
+        return true;
+    }
+
+    // Verify n (message, r||s, key) triples with one fused launch. ok must hold n bytes.
+    int gpu_verify_messages(const std::vector<const uint8_t*>& msgs, const std::vector<size_t>& lens,
+                            const std::vector<const uint8_t*>& sigs, const std::vector<const uint8_t*>& keys64,
+                            uint8_t* ok) {
+        const size_t n = msgs.size();
+        if (!n) return 0;
+        if (!ctx) return SBFT_GV_ENODEV;
+        std::vector<uint8_t> blob;
+        std::vector<uint64_t> off(n);
+        std::vector<uint32_t> len(n);
+        std::vector<uint8_t> r(32 * n), s(32 * n), qx(32 * n), qy(32 * n);
+        for (size_t i = 0; i < n; ++i) {
+            off[i] = blob.size();
+            len[i] = (uint32_t)lens[i];
+            blob.insert(blob.end(), msgs[i], msgs[i] + lens[i]);
+            std::memcpy(&r[32 * i], sigs[i], 32);
+            std::memcpy(&s[32 * i], sigs[i] + 32, 32);
+            std::memcpy(&qx[32 * i], keys64[i], 32);
+            std::memcpy(&qy[32 * i], keys64[i] + 32, 32);
+        }
+        if (blob.empty()) blob.push_back(0);
+        return sbft_gv_sha256_verify_p256(ctx, blob.data(), blob.size(), off.data(), len.data(), r.data(),
+                                          s.data(), qx.data(), qy.data(), n, ok, nullptr);
+    }
+
+    // Check + verify consenter signatures over one proposal. status[i]: 0 ok, <0 error;
+    // reasons[i] gets the error text.
+    int consenter_batch(const sbft_signature* sigs, size_t n, const sbft_proposal* p, int32_t* status,
+                        std::vector<std::string>* reasons) {
+        char digest[65];
+        digest_of(p, digest);
+        std::vector<const uint8_t*> msgs, sv, kv;
+        std::vector<size_t> lens, which;
+        std::vector<std::array<uint8_t, 64>> keybuf(n);
+        if (reasons) reasons->assign(n, std::string());
+        for (size_t i = 0; i < n; ++i) {
+            Msg m;
+            status[i] = 0;
+            if (!parse_msg(sigs[i].msg, sigs[i].msg_len, m)) {
+                status[i] = SBFT_V_EFORMAT;
+                if (reasons) (*reasons)[i] = "malformed signature message";
+                continue;
+            }
+            if (m.digest_len != 64 || std::memcmp(m.digest, digest, 64) != 0) {
+                status[i] = SBFT_V_EVERIFY;
+                if (reasons) (*reasons)[i] = "signature message does not bind the proposal digest";
+                continue;
+            }
+            if (!key_of(sigs[i].id, keybuf[i])) {
+                status[i] = SBFT_V_EKEY;
+                if (reasons) (*reasons)[i] = "unknown consenter " + std::to_string(sigs[i].id);
+                continue;
+            }
+            if (sigs[i].value_len != 64 || !sigs[i].value) {
+                status[i] = SBFT_V_EFORMAT;
+                if (reasons) (*reasons)[i] = "signature value must be 64 bytes r||s";
+                continue;
+            }
+            msgs.push_back(sigs[i].msg);
+            lens.push_back(sigs[i].msg_len);
+            sv.push_back(sigs[i].value);
+            kv.push_back(keybuf[i].data());
+            which.push_back(i);
+        }
+        std::vector<uint8_t> ok(which.size());
+        const int rc = gpu_verify_messages(msgs, lens, sv, kv, ok.data());
+        if (rc) return rc;
+        for (size_t k = 0; k < which.size(); ++k)
+            if (!ok[k]) {
+                status[which[k]] = SBFT_V_EVERIFY;
+                if (reasons) (*reasons)[which[k]] = "invalid signature";
+            }
+        return 0;
+    }
+};
+
+extern "C" {
+
+void sbft_sha256_host(const uint8_t* msg, size_t len, uint8_t out[32]) { sha256(msg, len, out); }
+
+void sbft_proposal_digest(const sbft_proposal* p, char out65[65]) {
+    std::vector<uint8_t> body;
+    body.reserve(p->payload_len + p->header_len + p->metadata_len + 32);
+    der_octets(body, p->payload, p->payload_len);
+    der_octets(body, p->header, p->header_len);
+    der_octets(body, p->metadata, p->metadata_len);
+    der_int64(body, p->verification_sequence);
+    std::vector<uint8_t> der;
+    der.reserve(body.size() + 8);
+    der.push_back(0x30);
+    der_len(der, body.size());
+    der.insert(der.end(), body.begin(), body.end());
+    uint8_t d[32];
+    sha256(der.data(), der.size(), d);
+    static const char* hx = "0123456789abcdef";
+    for (int i = 0; i < 32; ++i) {
+        out65[2 * i] = hx[d[i] >> 4];
+        out65[2 * i + 1] = hx[d[i] & 15];
+    }
+    out65[64] = 0;
+}
+
+sbft_verifier* sbft_verifier_new(sbft_gv_ctx* ctx, uint64_t verification_sequence) {
+    // ctx may be NULL for a parse-only verifier (RequestsFromProposal, AuxiliaryData);
+    // verification calls on it fail with SBFT_GV_ENODEV.
+    auto* v = new sbft_verifier();
+    v->ctx = ctx;
+    v->vseq = verification_sequence;
+    return v;
+}
+void sbft_verifier_free(sbft_verifier* v) { delete v; }
+
+int sbft_verifier_add_consenter(sbft_verifier* v, uint64_t id, const uint8_t pubkey65[65]) {
+    if (!v || !pubkey65 || pubkey65[0] != 0x04) return SBFT_GV_EINVAL;
+    std::array<uint8_t, 64> k;
+    std::memcpy(k.data(), pubkey65 + 1, 64);
+    std::unique_lock<std::shared_mutex> g(v->keys_mu);
+    v->keys[id] = k;
+    return 0;
+}
+
+uint64_t sbft_verifier_verification_sequence(const sbft_verifier* v) { return v ? v->vseq.load() : 0; }
+void sbft_verifier_set_verification_sequence(sbft_verifier* v, uint64_t seq) {
+    if (v) v->vseq = seq;
+}
+
+int sbft_verifier_requests_from_proposal(sbft_verifier* v, const sbft_proposal* p, char* infos,
+                                         size_t infos_cap, size_t* count) {
+    if (!v || !p || !count) return SBFT_GV_EINVAL;
+    std::vector<Req> reqs;
+    *count = 0;
+    if (!parse_payload(p->payload, p->payload_len, reqs)) return SBFT_V_EFORMAT;
+    char* w = infos;
+    char* end = infos + infos_cap;
+    for (auto& r : reqs)
+        if (!write_info(w, end, r.client_id, r.req_id)) return SBFT_V_ESPACE;
+    *count = reqs.size();
+    return 0;
+}
+
+int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char* infos, size_t infos_cap,
+                                  size_t* count, int64_t* bad_index, char* err, size_t err_cap) {
+    if (!v || !p || !count) return SBFT_GV_EINVAL;
+    *count = 0;
+    if (bad_index) *bad_index = -1;
+    std::vector<Req> reqs;
+    if (!parse_payload(p->payload, p->payload_len, reqs)) {
+        put_err(err, err_cap, "malformed proposal payload");
+        return SBFT_V_EFORMAT;
+    }
+    const size_t n = reqs.size();
+    std::vector<uint64_t> off(n);
+    std::vector<uint32_t> len(n);
+    std::vector<uint8_t> r(32 * n), s(32 * n), qx(32 * n), qy(32 * n), ok(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (reqs[i].pub[0] != 0x04) {
+            if (bad_index) *bad_index = (int64_t)i;
+            put_err(err, err_cap, "request %zu (%s:%s): public key is not SEC1 uncompressed", i,
+                    reqs[i].client_id.c_str(), reqs[i].req_id.c_str());
+            return SBFT_V_EFORMAT;
+        }
+        off[i] = reqs[i].body_off;
+        len[i] = (uint32_t)reqs[i].body_len;
+        std::memcpy(&r[32 * i], reqs[i].sig, 32);
+        std::memcpy(&s[32 * i], reqs[i].sig + 32, 32);
+        std::memcpy(&qx[32 * i], reqs[i].pub + 1, 32);
+        std::memcpy(&qy[32 * i], reqs[i].pub + 33, 32);
+    }
+    if (n && !v->ctx) {
+        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(SBFT_GV_ENODEV));
+        return SBFT_GV_ENODEV;
+    }
+    if (n) {
+        // one fused launch: the request bodies are hashed where they lie in the payload
+        const int rc = sbft_gv_sha256_verify_p256(v->ctx, p->payload, p->payload_len, off.data(), len.data(),
+                                                  r.data(), s.data(), qx.data(), qy.data(), n, ok.data(), nullptr);
+        if (rc) {
+            put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+            return rc;
+        }
+    }
+    for (size_t i = 0; i < n; ++i)
+        if (!ok[i]) {
+            if (bad_index) *bad_index = (int64_t)i;
+            put_err(err, err_cap, "request %zu (%s:%s) has an invalid signature", i, reqs[i].client_id.c_str(),
+                    reqs[i].req_id.c_str());
+            return SBFT_V_EVERIFY;
+        }
+    char* w = infos;
+    char* end = infos + infos_cap;
+    for (auto& q : reqs)
+        if (!write_info(w, end, q.client_id, q.req_id)) return SBFT_V_ESPACE;
+    *count = n;
+    return 0;
+}
+
+int sbft_verifier_verify_request(sbft_verifier* v, const uint8_t* req, size_t len, char* info, size_t info_cap,
+                                 char* err, size_t err_cap) {
+    if (!v || !req) return SBFT_GV_EINVAL;
+    Req q;
+    if (!parse_request(req, len, 0, q) || q.pub[0] != 0x04) {
+        put_err(err, err_cap, "malformed request");
+        return SBFT_V_EFORMAT;
+    }
+    std::vector<const uint8_t*> msgs{req}, sigs{q.sig}, keys{q.pub + 1};
+    std::vector<size_t> lens{q.body_len};
+    uint8_t ok = 0;
+    const int rc = v->gpu_verify_messages(msgs, lens, sigs, keys, &ok);
+    if (rc) {
+        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+        return rc;
+    }
+    if (!ok) {
+        put_err(err, err_cap, "request %s:%s has an invalid signature", q.client_id.c_str(), q.req_id.c_str());
+        return SBFT_V_EVERIFY;
+    }
+    char* w = info;
+    if (info && !write_info(w, info + info_cap, q.client_id, q.req_id)) return SBFT_V_ESPACE;
+    return 0;
+}
+
+int sbft_verifier_verify_consenter_sig(sbft_verifier* v, const sbft_signature* s, const sbft_proposal* p,
+                                       uint8_t* aux, size_t aux_cap, size_t* aux_len, char* err, size_t err_cap) {
+    if (!v || !s || !p) return SBFT_GV_EINVAL;
+    int32_t st = 0;
+    std::vector<std::string> why;
+    const int rc = v->consenter_batch(s, 1, p, &st, &why);
+    if (rc) {
+        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+        return rc;
+    }
+    if (st) {
+        put_err(err, err_cap, "%s", why[0].c_str());
+        return st;
+    }
+    Msg m;
+    parse_msg(s->msg, s->msg_len, m);
+    if (aux_len) *aux_len = m.aux_len;
+    if (aux) {
+        if (aux_cap < m.aux_len) return SBFT_V_ESPACE;
+        if (m.aux_len) std::memcpy(aux, m.aux, m.aux_len);
+    }
+    return 0;
+}
+
+int sbft_verifier_verify_consenter_sigs(sbft_verifier* v, const sbft_signature* sigs, size_t n,
+                                        const sbft_proposal* p, int32_t* status) {
+    if (!v || (n && (!sigs || !status)) || !p) return SBFT_GV_EINVAL;
+    return v->consenter_batch(sigs, n, p, status, nullptr);
+}
+
+int sbft_verifier_verify_signature(sbft_verifier* v, const sbft_signature* s, char* err, size_t err_cap) {
+    if (!v || !s) return SBFT_GV_EINVAL;
+    std::array<uint8_t, 64> key;
+    if (!v->key_of(s->id, key)) {
+        put_err(err, err_cap, "unknown signer %llu", (unsigned long long)s->id);
+        return SBFT_V_EKEY;
+    }
+    if (s->value_len != 64 || !s->value) {
+        put_err(err, err_cap, "signature value must be 64 bytes r||s");
+        return SBFT_V_EFORMAT;
+    }
+    std::vector<const uint8_t*> msgs{s->msg ? s->msg : (const uint8_t*)""}, sigs{s->value}, keys{key.data()};
+    std::vector<size_t> lens{s->msg_len};
+    uint8_t ok = 0;
+    const int rc = v->gpu_verify_messages(msgs, lens, sigs, keys, &ok);
+    if (rc) {
+        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+        return rc;
+    }
+    if (!ok) {
+        put_err(err, err_cap, "invalid signature from %llu", (unsigned long long)s->id);
+        return SBFT_V_EVERIFY;
+    }
+    return 0;
+}
+
+int64_t sbft_verifier_auxiliary_data(const uint8_t* msg, size_t msg_len, uint8_t* aux, size_t aux_cap) {
+    Msg m;
+    if (!parse_msg(msg, msg_len, m)) return -1;
+    if (aux && m.aux_len) std::memcpy(aux, m.aux, std::min(aux_cap, m.aux_len));
+    return (int64_t)m.aux_len;
+}
+
+// ---------------------------------------------------------------------- batching hook
+void sbft_compute_quorum(uint64_t n, int* q, int* f) {
+    const int ff = ((int)n - 1) / 3;
+    const int num = (int)n + ff + 1;
+    if (f) *f = ff;
+    if (q) *q = (num + 1) / 2;  // ceil(num / 2)
+}
+
+int sbft_verify_prev_commit_signatures(sbft_verifier* v, const sbft_signature* sigs, size_t n,
+                                       const sbft_proposal* prev, uint64_t curr_vseq, int* skipped, char* err,
+                                       size_t err_cap) {
+    if (!v || !prev || (n && !sigs)) return SBFT_GV_EINVAL;
+    if (skipped) *skipped = 0;
+    if ((uint64_t)prev->verification_sequence != curr_vseq) {
+        if (skipped) *skipped = 1;
+        return 0;
+    }
+    std::vector<int32_t> st(n);
+    std::vector<std::string> why;
+    const int rc = v->consenter_batch(sigs, n, prev, st.data(), &why);
+    if (rc) {
+        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+        return rc;
+    }
+    for (size_t i = 0; i < n; ++i)
+        if (st[i]) {
+            put_err(err, err_cap, "failed verifying consenter signature of %llu: %s", (unsigned long long)sigs[i].id,
+                    why[i].c_str());
+            return SBFT_V_EVERIFY;
+        }
+    return 0;
+}
+
+int sbft_collect_commits(sbft_verifier* v, const sbft_signature* votes, const char* const* vote_digests, size_t n,
+                         const sbft_proposal* p, size_t need, size_t* valid_idx, size_t* n_valid, char* log,
+                         size_t log_cap) {
+    if (!v || !p || !n_valid || (n && (!votes || !vote_digests || !valid_idx))) return SBFT_GV_EINVAL;
+    *n_valid = 0;
+    char expected[65];
+    v->digest_of(p, expected);
+    std::string lg;
+    std::vector<size_t> cand;
+    std::vector<sbft_signature> batch;
+    std::unordered_map<uint64_t, bool> seen;
+    for (size_t i = 0; i < n; ++i) {
+        if (seen.count(votes[i].id)) continue;  // voteSet.registerVote: one vote per signer
+        seen[votes[i].id] = true;
+        if (!vote_digests[i] || std::strcmp(vote_digests[i], expected) != 0) {
+            lg += "Got wrong digest at processCommits\n";
+            continue;
+        }
+        cand.push_back(i);
+        batch.push_back(votes[i]);
+    }
+    std::vector<int32_t> st(batch.size());
+    std::vector<std::string> why;
+    const int rc = v->consenter_batch(batch.data(), batch.size(), p, st.data(), &why);
+    if (rc) return rc;
+    for (size_t k = 0; k < batch.size(); ++k) {
+        if (st[k]) {
+            lg += "Couldn't verify " + std::to_string(batch[k].id) + "'s signature: " + why[k] + "\n";
+            continue;
+        }
+        if (*n_valid < need) valid_idx[(*n_valid)++] = cand[k];
+    }
+    if (log && log_cap) {
+        const size_t m = std::min(log_cap - 1, lg.size());
+        std::memcpy(log, lg.data(), m);
+        log[m] = 0;
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------- signer
+struct sbft_signer {
+    sbft_gv_ctx* ctx;
+    uint64_t id;
+    uint8_t d[32];
+    uint8_t qx[32], qy[32];
+};
+
+sbft_signer* sbft_signer_new(sbft_gv_ctx* ctx, uint64_t id, const uint8_t priv32[32]) {
+    if (!ctx || !priv32 || is_zero32(priv32) || cmp_be32(priv32, N_BE) >= 0) return nullptr;
+    auto* s = new sbft_signer();
+    s->ctx = ctx;
+    s->id = id;
+    std::memcpy(s->d, priv32, 32);
+    uint8_t k[32] = {0}, e[32] = {0}, r[32], sg[32], st = 0;
+    k[31] = 1;
+    if (sbft_gv_sign_p256(ctx, s->d, k, e, 1, s->qx, s->qy, r, sg, &st) || !st) {
+        delete s;
+        return nullptr;
+    }
+    return s;
+}
+void sbft_signer_free(sbft_signer* s) { delete s; }
+
+int sbft_signer_public_key(const sbft_signer* s, uint8_t pubkey65[65]) {
+    if (!s || !pubkey65) return SBFT_GV_EINVAL;
+    pubkey65[0] = 0x04;
+    std::memcpy(pubkey65 + 1, s->qx, 32);
+    std::memcpy(pubkey65 + 33, s->qy, 32);
+    return 0;
+}
+
+int sbft_signer_sign(sbft_signer* s, const uint8_t* data, size_t len, uint8_t sig64[64]) {
+    if (!s || (!data && len) || !sig64) return SBFT_GV_EINVAL;
+    uint8_t e[32];
+    sha256(data ? data : (const uint8_t*)"", len, e);
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        uint8_t k[32], qx[32], qy[32], st = 0;
+        rfc6979_nonce(s->d, e, attempt, k);
+        const int rc = sbft_gv_sign_p256(s->ctx, s->d, k, e, 1, qx, qy, sig64, sig64 + 32, &st);
+        if (rc) return rc;
+        if (st) return 0;
+    }
+    return SBFT_V_EVERIFY;
+}
+
+int sbft_signer_sign_proposal(sbft_signer* s, const sbft_proposal* p, const uint8_t* aux, size_t aux_len,
+                              uint8_t* msg, size_t msg_cap, size_t* msg_len, uint8_t sig64[64]) {
+    if (!s || !p || !msg || !msg_len || (aux_len && !aux)) return SBFT_GV_EINVAL;
+    const size_t need = 4 + 2 + 64 + 4 + aux_len;
+    if (msg_cap < need) return SBFT_V_ESPACE;
+    char digest[65];
+    sbft_proposal_digest(p, digest);
+    uint8_t* w = msg;
+    std::memcpy(w, MSG_MAGIC, 4);
+    w += 4;
+    *w++ = 64;
+    *w++ = 0;
+    std::memcpy(w, digest, 64);
+    w += 64;
+    for (int i = 0; i < 4; ++i) *w++ = (uint8_t)(aux_len >> (8 * i));
+    if (aux_len) std::memcpy(w, aux, aux_len);
+    *msg_len = need;
+    return sbft_signer_sign(s, msg, need, sig64);
+}
+
+int64_t sbft_make_request(sbft_signer* client, const char* client_id, const char* req_id, const uint8_t* payload,
+                          size_t payload_len, uint8_t* out, size_t out_cap) {
+    if (!client || !client_id || !req_id || (payload_len && !payload) || !out) return SBFT_GV_EINVAL;
+    const size_t a = std::strlen(client_id), b = std::strlen(req_id);
+    if (a > 0xffff || b > 0xffff || payload_len > 0xffffffffu) return SBFT_GV_EINVAL;
+    const size_t body = 4 + 2 + a + 2 + b + 4 + payload_len + 65;
+    if (out_cap < body + 64) return SBFT_V_ESPACE;
+    uint8_t* w = out;
+    std::memcpy(w, REQ_MAGIC, 4);
+    w += 4;
+    *w++ = (uint8_t)a;
+    *w++ = (uint8_t)(a >> 8);
+    std::memcpy(w, client_id, a);
+    w += a;
+    *w++ = (uint8_t)b;
+    *w++ = (uint8_t)(b >> 8);
+    std::memcpy(w, req_id, b);
+    w += b;
+    for (int i = 0; i < 4; ++i) *w++ = (uint8_t)(payload_len >> (8 * i));
+    if (payload_len) std::memcpy(w, payload, payload_len);
+    w += payload_len;
+    sbft_signer_public_key(client, w);
+    w += 65;
+    const int rc = sbft_signer_sign(client, out, body, w);
+    if (rc) return rc;
+    return (int64_t)(body + 64);
+}
+
+}  // extern "C"

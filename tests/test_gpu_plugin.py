@@ -1,0 +1,172 @@
+"""GPU tests of the api.Verifier / api.Signer mirror: every verification goes through the
+engine (one fused launch per proposal / per consenter batch). Expectations follow the
+reference's own tests where they pin behaviour: any bad request rejects the whole proposal
+(view.go:386-393, TestBadPrePrepare), the prev-commit error text (view.go:637), the
+commit-vote log text (view.go:840, TestBadCommit), dedupe per signer (util.go:123-136)."""
+import hashlib
+import hmac
+
+import numpy as np
+import pytest
+
+import oracle
+from smartbft_amd import plugin
+
+pytestmark = pytest.mark.gpu
+
+
+def _priv(tag):
+    return (int.from_bytes(hashlib.sha256(b"node" + str(tag).encode()).digest(), "big") % oracle.N).to_bytes(32, "big")
+
+
+@pytest.fixture(scope="module")
+def net(gpu):
+    nodes = [plugin.Signer(gpu, i, _priv(i)) for i in range(1, 5)]
+    v = plugin.Verifier(gpu, verification_sequence=3)
+    for s in nodes:
+        v.add_consenter(s.id, s.public_key())
+    clients = [plugin.Signer(gpu, 1000 + i, _priv(("client", i))) for i in range(8)]
+    return v, nodes, clients
+
+
+def _proposal(clients, n, tamper=None):
+    reqs = []
+    for i in range(n):
+        r = clients[i % len(clients)].make_request(f"client{i % len(clients)}", f"tx{i}", b"payload-%d" % i)
+        if tamper == i:
+            r = r[:30] + bytes([r[30] ^ 1]) + r[31:]
+        reqs.append(r)
+    return plugin.Proposal(plugin.encode_payload(reqs), b"header", b"metadata", 3), reqs
+
+
+def test_verify_proposal_accepts_and_lists_requests(net):
+    v, nodes, clients = net
+    p, reqs = _proposal(clients, 300)
+    infos = v.VerifyProposal(p)
+    assert [(i.ClientID, i.ID) for i in infos] == [(f"client{i % 8}", f"tx{i}") for i in range(300)]
+    assert v.RequestsFromProposal(p) == infos
+
+
+def test_verify_proposal_rejects_any_bad_request(net):
+    v, nodes, clients = net
+    p, _ = _proposal(clients, 100, tamper=37)
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(p)
+    assert ei.value.index == 37 and "has an invalid signature" in str(ei.value)
+    assert ei.value.code == plugin.EVERIFY
+
+
+def test_verify_request(net):
+    v, nodes, clients = net
+    r = clients[0].make_request("alice", "42", b"hello")
+    info = v.VerifyRequest(r)
+    assert (info.ClientID, info.ID) == ("alice", "42")
+    with pytest.raises(plugin.VerifyError):
+        v.VerifyRequest(r[:-1] + bytes([r[-1] ^ 0x80]))
+    with pytest.raises(plugin.VerifyError):
+        v.VerifyRequest(r[:10])
+
+
+def test_requests_signatures_verify_under_oracle(net):
+    """The engine's RFC 6979 signatures are valid ECDSA under the independent oracle."""
+    v, nodes, clients = net
+    r = clients[3].make_request("c3", "x", b"abc")
+    body, sig = r[:-64], r[-64:]
+    pub = clients[3].public_key()
+    assert oracle.verify(hashlib.sha256(body).digest(), sig[:32], sig[32:], pub[1:33], pub[33:])
+
+
+def _rfc6979_k(x: bytes, h1: bytes) -> int:
+    """Independent restatement of RFC 6979 3.2 with Python's hmac."""
+    q = oracle.N
+    h = (int.from_bytes(h1, "big") % q).to_bytes(32, "big")
+    V, K = b"\x01" * 32, b"\x00" * 32
+    K = hmac.new(K, V + b"\x00" + x + h, hashlib.sha256).digest()
+    V = hmac.new(K, V, hashlib.sha256).digest()
+    K = hmac.new(K, V + b"\x01" + x + h, hashlib.sha256).digest()
+    V = hmac.new(K, V, hashlib.sha256).digest()
+    while True:
+        V = hmac.new(K, V, hashlib.sha256).digest()
+        k = int.from_bytes(V, "big")
+        if 1 <= k < q:
+            return k
+        K = hmac.new(K, V + b"\x00", hashlib.sha256).digest()
+        V = hmac.new(K, V, hashlib.sha256).digest()
+
+
+def test_signer_rfc6979_known_answer(gpu):
+    # RFC 6979 A.2.5, P-256 with SHA-256, message "sample"
+    x = bytes.fromhex("C9AFA9D845BA75166B5C215767B1D6934E50C3DB36E89B127B8A622B120F6721")
+    s = plugin.Signer(gpu, 9, x)
+    pub = s.public_key()
+    assert pub[1:].hex().upper() == (
+        "60FED4BA255A9D31C961EB74C6356D68C049B8923B61FA6CE669622E60F29FB6"
+        "7903FE1008B8BC99A41AE9E95628BC64F2F1B20C2D7E9F5177A3C294D4462299")
+    sig = s.Sign(b"sample")
+    k = _rfc6979_k(x, hashlib.sha256(b"sample").digest())
+    assert k == 0xA6E3C57DD01ABE90086538398355DD4C3B17AA873382B0F24D6129493D8AAD60
+    assert sig.hex().upper() == (
+        "EFD48B2AACB6A8FD1140DD9CD45E81D69D2C877B56AAF991C34D0EA84EAF3716"
+        "F7CB1C942D657C41D436C7A1B6E29F65F3E900DBB9AFF4064DC4AB2F843ACDA8")
+
+
+def test_consenter_sig_roundtrip_and_binding(net):
+    v, nodes, clients = net
+    p, _ = _proposal(clients, 10)
+    other, _ = _proposal(clients, 11)
+    sig = nodes[1].SignProposal(p, b"aux-bytes")
+    assert v.VerifyConsenterSig(sig, p) == b"aux-bytes"
+    assert plugin.AuxiliaryData(sig.Msg) == b"aux-bytes"
+    with pytest.raises(plugin.VerifyError, match="does not bind"):
+        v.VerifyConsenterSig(sig, other)
+    bad = plugin.Signature(sig.ID, sig.Value[:-1] + bytes([sig.Value[-1] ^ 1]), sig.Msg)
+    with pytest.raises(plugin.VerifyError, match="invalid signature"):
+        v.VerifyConsenterSig(bad, p)
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyConsenterSig(plugin.Signature(77, sig.Value, sig.Msg), p)
+    assert ei.value.code == plugin.EKEY
+    v.VerifySignature(plugin.Signature(nodes[2].id, nodes[2].Sign(b"view-data"), b"view-data"))
+    with pytest.raises(plugin.VerifyError):
+        v.VerifySignature(plugin.Signature(nodes[2].id, nodes[2].Sign(b"view-data"), b"view-datA"))
+
+
+def test_consenter_batch_statuses(net):
+    v, nodes, clients = net
+    p, _ = _proposal(clients, 5)
+    sigs = [n.SignProposal(p, b"a%d" % n.id) for n in nodes]
+    sigs[2] = plugin.Signature(sigs[2].ID, sigs[1].Value, sigs[2].Msg)  # wrong value
+    st = v.VerifyConsenterSigs(sigs, p)
+    assert st == [0, 0, plugin.EVERIFY, 0]
+
+
+def test_prev_commit_signatures_mirror(net):
+    v, nodes, clients = net
+    prev, _ = _proposal(clients, 7)
+    sigs = [n.SignProposal(prev, b"") for n in nodes[:3]]
+    assert v.verify_prev_commit_signatures(sigs, prev, curr_vseq=3) is False
+    assert v.verify_prev_commit_signatures(sigs, prev, curr_vseq=4) is True  # skipped: seq advanced
+    sigs[1] = plugin.Signature(sigs[1].ID, sigs[0].Value, sigs[1].Msg)
+    with pytest.raises(plugin.VerifyError,
+                       match=f"failed verifying consenter signature of {sigs[1].ID}: invalid signature"):
+        v.verify_prev_commit_signatures(sigs, prev, curr_vseq=3)
+
+
+def test_collect_commits_quorum_n100(gpu):
+    """Commit collection at n = 100 (q = 67, 66 votes needed besides our own), one launch."""
+    q, f = plugin.compute_quorum(100)
+    assert (q, f) == (67, 33)
+    nodes = [plugin.Signer(gpu, i, _priv(("n100", i))) for i in range(1, 101)]
+    v = plugin.Verifier(gpu, 1)
+    for s in nodes:
+        v.add_consenter(s.id, s.public_key())
+    p = plugin.Proposal(b"block", b"h", b"m", 1)
+    dig = p.Digest()
+    votes = [(n.SignProposal(p, b""), dig) for n in nodes[1:80]]
+    votes[3] = (plugin.Signature(votes[3][0].ID, votes[4][0].Value, votes[3][0].Msg), dig)  # bad sig
+    votes[7] = (votes[7][0], "ff" * 32)                                                      # wrong digest
+    votes.insert(10, votes[9])                                                              # duplicate
+    idx, log = v.collect_commits(votes, p, need=q - 1)
+    assert len(idx) == q - 1
+    assert 3 not in idx and 7 not in idx and 10 not in idx
+    assert f"Couldn't verify {votes[3][0].ID}'s signature: invalid signature" in log
+    assert "Got wrong digest at processCommits" in log

@@ -1,0 +1,85 @@
+"""CPU tests of the plugin-level mirror (include/sbft_verifier.h) that need no GPU: quorum
+math (TestQuorum, internal/bft/util_test.go:135-163), Proposal.Digest (pkg/types/types.go:50-69)
+against an independent restatement of Go encoding/asn1, and the parse-only paths."""
+import hashlib
+
+import pytest
+
+from smartbft_amd import plugin
+
+
+@pytest.mark.parametrize("n,f,q", [(4, 1, 3), (5, 1, 4), (6, 1, 4), (7, 2, 5), (8, 2, 6), (9, 2, 6),
+                                   (10, 3, 7), (11, 3, 8), (12, 3, 8), (100, 33, 67)])
+def test_quorum(n, f, q):
+    assert plugin.compute_quorum(n) == (q, f)
+
+
+def _der_len(n):
+    if n < 0x80:
+        return bytes([n])
+    b = n.to_bytes((n.bit_length() + 7) // 8, "big")
+    return bytes([0x80 | len(b)]) + b
+
+
+def _go_int64(v):
+    # encoding/asn1 int64Length + big-endian two's complement
+    n = 1
+    i = v
+    while i > 127:
+        n += 1
+        i >>= 8
+    while i < -128:
+        n += 1
+        i >>= 8
+    return (v & ((1 << (8 * n)) - 1)).to_bytes(n, "big")
+
+
+def _go_digest(p):
+    body = b""
+    for f in (p.Payload, p.Header, p.Metadata):
+        body += b"\x04" + _der_len(len(f)) + f
+    iv = _go_int64(p.VerificationSequence)
+    body += b"\x02" + _der_len(len(iv)) + iv
+    return hashlib.sha256(b"\x30" + _der_len(len(body)) + body).hexdigest()
+
+
+@pytest.mark.parametrize("size", [0, 1, 127, 128, 255, 256, 65535, 65536, 1 << 20])
+@pytest.mark.parametrize("vseq", [0, 1, 127, 128, 255, 256, -1, -128, -129, (1 << 63) - 1, -(1 << 63)])
+def test_proposal_digest_matches_go_asn1(size, vseq):
+    p = plugin.Proposal(bytes(i % 251 for i in range(size)), b"hdr" * (size % 5), b"m" * (size % 300), vseq)
+    assert p.Digest() == _go_digest(p)
+
+
+def test_host_sha256():
+    for n in (0, 1, 55, 56, 63, 64, 65, 1000):
+        m = bytes(range(256)) * 4
+        assert plugin.sha256_host(m[:n]) == hashlib.sha256(m[:n]).digest()
+
+
+def _fake_request(cid, rid, payload):
+    """Format-only request (garbage key/signature): enough for the parse-only paths."""
+    body = b"SBR1" + len(cid).to_bytes(2, "little") + cid.encode() + len(rid).to_bytes(2, "little") + \
+        rid.encode() + len(payload).to_bytes(4, "little") + payload + b"\x04" + b"\x11" * 64
+    return body + b"\x22" * 64
+
+
+def test_requests_from_proposal_parse_only():
+    v = plugin.Verifier(None)
+    reqs = [_fake_request(f"client{i}", f"req{i}", bytes([i]) * i) for i in range(50)]
+    p = plugin.Proposal(plugin.encode_payload(reqs))
+    infos = v.RequestsFromProposal(p)
+    assert [(r.ClientID, r.ID) for r in infos] == [(f"client{i}", f"req{i}") for i in range(50)]
+    # malformed payloads parse to nothing (the reference stub returns nil on unmarshal errors)
+    assert v.RequestsFromProposal(plugin.Proposal(p.Payload[:-1])) == []
+    assert v.RequestsFromProposal(plugin.Proposal(b"\x05\x00\x00\x00")) == []
+    # verification without an engine fails loudly, never silently accepts
+    with pytest.raises(plugin.VerifyError):
+        v.VerifyProposal(p)
+
+
+def test_auxiliary_data():
+    aux = b"prepares-from"
+    msg = b"SBC1" + (64).to_bytes(2, "little") + b"a" * 64 + len(aux).to_bytes(4, "little") + aux
+    assert plugin.AuxiliaryData(msg) == aux
+    assert plugin.AuxiliaryData(msg[:-1]) is None
+    assert plugin.AuxiliaryData(b"") is None
