@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=131072)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true", help="skip configs 3/4 latency")
+    ap.add_argument("--latency-calls", type=int, default=200)
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_verify_latest.json"))
     return ap.parse_args()
 
@@ -90,6 +92,49 @@ def cpu_baseline(wl, sample: int, threads: int):
     return port, go_proxy, ok_cpu
 
 
+def latency_configs(gv, calls: int):
+    """BASELINE configs 3 and 4 through the plugin mirror (host buffers, PCIe included):
+    VerifyProposal on 10k-request proposals (view.go:555) and a 67-signature commit quorum at
+    n = 100 (view.go:631). Reports p50/p99 wall latency per call."""
+    from smartbft_amd import plugin
+    from smartbft_amd.workload import make_signed_requests
+    out = {}
+    reqs = make_signed_requests(gv, 10_000)
+    prop = plugin.Proposal(plugin.encode_payload(reqs), b"header", b"metadata", 1)
+    v = plugin.Verifier(gv, 1)
+    assert len(v.VerifyProposal(prop)) == 10_000
+    ts = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        v.VerifyProposal(prop)
+        ts.append(time.perf_counter() - t0)
+    ts = np.array(ts) * 1e3
+    out["verify_proposal_10k"] = {"p50_ms": round(float(np.percentile(ts, 50)), 3),
+                                  "p99_ms": round(float(np.percentile(ts, 99)), 3), "calls": calls,
+                                  "requests": 10_000, "path": "plugin VerifyProposal, host buffers (PCIe incl.)"}
+    # n = 100 replicas: q = 67 signatures per decision
+    import hashlib
+    q, f = plugin.compute_quorum(100)
+    signers = [plugin.Signer(gv, i, (int.from_bytes(hashlib.sha256(b"n100-%d" % i).digest(), "big") %
+                                     0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551).to_bytes(32, "big"))
+               for i in range(1, q + 1)]
+    for sg in signers:
+        v.add_consenter(sg.id, sg.public_key())
+    block = plugin.Proposal(b"block-payload" * 100, b"h", b"m", 1)
+    sigs = [sg.SignProposal(block, b"") for sg in signers]
+    assert v.VerifyConsenterSigs(sigs, block) == [0] * q
+    ts = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        v.VerifyConsenterSigs(sigs, block)
+        ts.append(time.perf_counter() - t0)
+    ts = np.array(ts) * 1e3
+    out["commit_quorum_n100"] = {"p50_ms": round(float(np.percentile(ts, 50)), 3),
+                                 "p99_ms": round(float(np.percentile(ts, 99)), 3), "calls": calls,
+                                 "signatures": q, "path": "plugin VerifyConsenterSigs, host buffers"}
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,9 +150,12 @@ def main():
     from smartbft_amd import GpuVerifier
     from smartbft_amd.workload import make_workload
 
+    from smartbft_amd.dist import reduce_timing, shard_range
+
     gv = GpuVerifier(device_mask=1 << local)
     n = args.n
-    wl = make_workload(gv, n, start=rank * n, device=local)
+    lo, _ = shard_range(rank, world, n)
+    wl = make_workload(gv, n, start=lo, device=local)
     ok = torch.empty(n, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -135,12 +183,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        mm = torch.tensor([mismatches], dtype=torch.int64, device=dev)
-        dist.all_reduce(mm)
-        mismatches = int(mm.item())
+        elapsed, mismatches = reduce_timing(elapsed, mismatches, device=dev)
     kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
 
@@ -190,6 +233,13 @@ def main():
             rec["speedup_vs_cpu_baseline"] = round(value / port["value"], 1)
             if go_proxy:
                 rec["speedup_vs_go_proxy"] = round(value / go_proxy["value"], 1)
+        if world == 1 and not args.no_latency:
+            lat = latency_configs(gv, args.latency_calls)
+            if "cpu_baseline_go_proxy" in rec:
+                thr = rec["cpu_baseline_go_proxy"]["value"]
+                lat["verify_proposal_10k"]["cpu_go_proxy_ms_estimate"] = round(10_000 / thr * 1e3, 3)
+                lat["commit_quorum_n100"]["cpu_go_proxy_ms_estimate"] = round(67 / thr * 1e3, 3)
+            rec["latency"] = lat
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -80,6 +80,11 @@ int sbft_gv_sha256_verify_p256(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blo
                                const uint8_t* s, const uint8_t* qx, const uint8_t* qy, size_t n,
                                uint8_t* ok_out, uint8_t* dig_out);
 
+/* Bytes of device workspace the verify pipeline uses for a batch of n tuples (fixup list +
+ * batched-inversion arrays, ~65 B per tuple). The device-resident entry points keep one such
+ * workspace per caller stream inside the context. */
+size_t sbft_gv_verify_workspace_bytes(size_t n);
+
 /* Device-resident variants (inputs already in HBM on `device`; stream = hipStream_t). */
 int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, const void* d_r,
                             const void* d_s, const void* d_qx, const void* d_qy, size_t n,

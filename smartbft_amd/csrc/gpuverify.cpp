@@ -136,6 +136,8 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
     delete ctx;
 }
 
+size_t sbft_gv_verify_workspace_bytes(size_t n) { return sbft_verify_work_bytes(n); }
+
 int sbft_gv_device_count(const sbft_gv_ctx* ctx) { return ctx ? (int)ctx->slots.size() : 0; }
 
 void sbft_gv_normalize_hash(const uint8_t* hash, size_t len, uint8_t out32[32]) {

@@ -2,7 +2,16 @@
 // host runtime (gpuverify.cpp). Not part of the public C ABI (include/sbft_gpuverify.h).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
+
+// Device workspace the verify pipeline needs for n tuples (see sbft_launch_p256_verify):
+// fixup counter + list (4(n+1) B, rounded to 256), then the batched-inversion arrays
+// pre | suf (32 B per tuple) and tot | kb (32 B per 256-tuple workgroup).
+static inline size_t sbft_verify_work_bytes(size_t n) {
+    const size_t blocks = (n + 255) / 256;
+    return ((4 * (n + 1) + 255) & ~(size_t)255) + 64 * n + 64 * blocks;
+}
 
 extern "C" {
 // P-256 verify of n SoA tuples (32-byte big-endian fields) -> n verdict bytes.
@@ -10,10 +19,6 @@ extern "C" {
 int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                             const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok, uint32_t n,
                             uint32_t* d_work, hipStream_t stream);
-static inline size_t sbft_verify_work_bytes(size_t n) { return 4 * (n + 1); // Element-wise primitive self-test (see p256_selftest.hip for op codes).
-int sbft_launch_selftest(int op, const uint8_t* d_a, const uint8_t* d_b, uint8_t* d_out, uint32_t n,
-                         hipStream_t stream);
-}
 // SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable >= 68 bytes
 // past its last message (funnel over-read). Digests are 32-byte big-endian.
 int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,

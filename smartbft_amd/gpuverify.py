@@ -19,7 +19,7 @@ EXPORTS = [
     "sbft_gv_verify_p256", "sbft_gv_sha256", "sbft_gv_sha256_verify_p256",
     "sbft_gv_verify_p256_dev", "sbft_gv_sha256_dev", "sbft_gv_sha256_verify_p256_dev",
     "sbft_gv_normalize_hash", "sbft_gv_normalize_scalar", "sbft_gv_sign_p256", "sbft_gv_sign_p256_dev",
-    "sbft_gv_selftest_field",
+    "sbft_gv_selftest_field", "sbft_gv_verify_workspace_bytes",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -66,6 +66,8 @@ def load_library():
                                                 [ctypes.c_size_t, _vp, _vp, _vp]
     L.sbft_gv_sign_p256.argtypes = [_vp] + [_u8p] * 3 + [ctypes.c_size_t] + [_u8p] * 5
     L.sbft_gv_sign_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 3 + [ctypes.c_size_t] + [_vp] * 6
+    L.sbft_gv_verify_workspace_bytes.argtypes = [ctypes.c_size_t]
+    L.sbft_gv_verify_workspace_bytes.restype = ctypes.c_size_t
     L.sbft_gv_selftest_field.argtypes = [_vp, ctypes.c_int, _u8p, _u8p, ctypes.c_size_t, _u8p]
     L.sbft_gv_normalize_hash.argtypes = [_u8p, ctypes.c_size_t, _u8p]
     L.sbft_gv_normalize_hash.restype = None

@@ -120,3 +120,38 @@ def make_workload(gv, n: int, start: int = 0, device: int = 0, corrupt: bool = T
         # make the swap a no-op only if two tuples shared d, which distinct hashes exclude.
     torch.cuda.synchronize(dev)
     return Workload(e, r, s, qx, qy, corrupted, start)
+
+
+def make_signed_requests(gv, n: int, start: int = 0, device: int = 0) -> list[bytes]:
+    """BASELINE config 3 requests in the engine's signed-request format (include/sbft_verifier.h):
+    distinct client key per request, seeded 64-256 B payloads, signed on the GPU. Request i:
+    client_id "client<i>", req_id "tx<i>", payload = SHA-256 stream of seed|"pl"|le64(i)."""
+    import hashlib
+    dev = torch.device(f"cuda:{device}")
+    d = _reduce_mod_n(_gpu_sha(gv, *_tag_messages(b"rkey", start, n), dev))
+    k = _reduce_mod_n(_gpu_sha(gv, *_tag_messages(b"rk", start, n), dev))
+    zero = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    one = zero.clone()
+    one[:, 31] = 1
+    qx, qy, r, s = (torch.empty_like(zero) for _ in range(4))
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    gv.sign_dev(d, one, zero, qx, qy, r, s, st)  # pass 1: public keys
+    torch.cuda.synchronize(dev)
+    qxh, qyh = qx.cpu().numpy(), qy.cpu().numpy()
+    rng = np.random.default_rng(start + 12345)
+    lens = rng.integers(64, 257, size=n)
+    bodies = []
+    for i in range(n):
+        cid, rid = f"client{start + i}".encode(), f"tx{start + i}".encode()
+        pl = (hashlib.sha256(SEED + b"pl" + int(start + i).to_bytes(8, "little")).digest() * 9)[:lens[i]]
+        bodies.append(b"SBR1" + len(cid).to_bytes(2, "little") + cid + len(rid).to_bytes(2, "little") + rid +
+                      len(pl).to_bytes(4, "little") + pl + b"\x04" + qxh[i].tobytes() + qyh[i].tobytes())
+    ln = np.array([len(b) for b in bodies], dtype=np.uint32)
+    off = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
+    e = torch.from_numpy(gv.sha256(np.frombuffer(b"".join(bodies), dtype=np.uint8), off, ln)).to(dev)
+    gv.sign_dev(d, k, e, qx, qy, r, s, st)  # pass 2: signatures over SHA-256(body)
+    torch.cuda.synchronize(dev)
+    if not bool((st == 1).all()):
+        raise RuntimeError("signer rejected a synthetic request key")
+    rh, sh = r.cpu().numpy(), s.cpu().numpy()
+    return [bodies[i] + rh[i].tobytes() + sh[i].tobytes() for i in range(n)]
