@@ -89,12 +89,16 @@ size_t sbft_gv_verify_workspace_bytes(size_t n);
 int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, const void* d_r,
                             const void* d_s, const void* d_qx, const void* d_qy, size_t n,
                             void* d_ok, void* stream);
+/* d_order (may be NULL): u32 permutation of [0, n) — lane t hashes message d_order[t]. Pass the
+ * messages sorted by length so a wavefront's lanes finish together (the host-buffer calls
+ * sort internally). Digests land at their message's index either way. */
 int sbft_gv_sha256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob, const void* d_off,
-                       const void* d_len, size_t n, void* d_dig, void* stream);
+                       const void* d_len, const void* d_order, size_t n, void* d_dig, void* stream);
 int sbft_gv_sha256_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob,
-                                   const void* d_off, const void* d_len, const void* d_r,
-                                   const void* d_s, const void* d_qx, const void* d_qy, size_t n,
-                                   void* d_ok, void* d_dig, void* stream);
+                                   const void* d_off, const void* d_len, const void* d_order,
+                                   const void* d_r, const void* d_s, const void* d_qx,
+                                   const void* d_qy, size_t n, void* d_ok, void* d_dig,
+                                   void* stream);
 
 /* Batched key derivation + ECDSA signing with caller-supplied nonces (the api.Signer side,
  * pkg/api/dependencies.go:46-52; also the synthetic-workload generator). For each k:

@@ -185,23 +185,24 @@ int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, 
 }
 
 int sbft_gv_sha256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob, const void* d_off,
-                       const void* d_len, size_t n, void* d_dig, void* stream) {
+                       const void* d_len, const void* d_order, size_t n, void* d_dig, void* stream) {
     if (!ctx || (n && (!d_blob || !d_off || !d_len || !d_dig))) return SBFT_GV_EINVAL;
     if (n > 0xffffffffu) return SBFT_GV_EINVAL;
     if (!slot_for(ctx, device)) return SBFT_GV_ENODEV;
     if (hipSetDevice(device) != hipSuccess) return SBFT_GV_EDEVICE;
     return sbft_launch_sha256((const uint8_t*)d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len,
-                              (uint8_t*)d_dig, (uint32_t)n, (hipStream_t)stream)
+                              (const uint32_t*)d_order, (uint8_t*)d_dig, (uint32_t)n, (hipStream_t)stream)
                ? SBFT_GV_ELAUNCH
                : SBFT_GV_OK;
 }
 
 int sbft_gv_sha256_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob,
-                                   const void* d_off, const void* d_len, const void* d_r,
-                                   const void* d_s, const void* d_qx, const void* d_qy, size_t n,
-                                   void* d_ok, void* d_dig, void* stream) {
+                                   const void* d_off, const void* d_len, const void* d_order,
+                                   const void* d_r, const void* d_s, const void* d_qx,
+                                   const void* d_qy, size_t n, void* d_ok, void* d_dig,
+                                   void* stream) {
     if (!d_dig) return SBFT_GV_EINVAL;  // the digest scratch is caller-provided here
-    int rc = sbft_gv_sha256_dev(ctx, device, d_blob, d_off, d_len, n, d_dig, stream);
+    int rc = sbft_gv_sha256_dev(ctx, device, d_blob, d_off, d_len, d_order, n, d_dig, stream);
     if (rc) return rc;
     return sbft_gv_verify_p256_dev(ctx, device, d_dig, d_r, d_s, d_qx, d_qy, n, d_ok, stream);
 }
@@ -289,23 +290,31 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
     if (c.count == 0) return SBFT_GV_OK;
     rebased.resize(c.count);
     for (size_t k = 0; k < c.count; ++k) rebased[k] = off[c.begin + k] - lo;
+    // lanes take messages in length order (descending) so each wavefront's lanes finish together
+    std::vector<uint32_t> order(c.count);
+    for (size_t k = 0; k < c.count; ++k) order[k] = (uint32_t)k;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return len[c.begin + a] > len[c.begin + b]; });
     const size_t span = hi - lo;
     const size_t fb = align_up(span + 128, 256);  // funnel over-read padding
     const size_t fo = align_up(8 * c.count, 256), fl = align_up(4 * c.count, 256);
     const size_t fd = align_up(32 * c.count, 256);
     const bool verify = ok_out != nullptr;
-    const size_t need = fb + fo + fl + fd +
+    const size_t need = fb + fo + 2 * fl + fd +
                         (verify ? 4 * fd + align_up(c.count, 256) + sbft_verify_work_bytes(c.count) : 0);
     HIPCHK(hipSetDevice(sl->device));
     int rc = sl->reserve(need);
     if (rc) return rc;
     uint8_t* b = sl->dbuf;
-    uint8_t *d_blob = b, *d_off = b + fb, *d_len = d_off + fo, *d_dig = d_len + fl;
+    uint8_t *d_blob = b, *d_off = b + fb, *d_len = d_off + fo, *d_order = d_len + fl, *d_dig = d_order + fl;
     HIPCHK(hipMemcpyAsync(d_blob, blob + lo, span, hipMemcpyHostToDevice, sl->stream));
     HIPCHK(hipMemcpyAsync(d_off, rebased.data(), 8 * c.count, hipMemcpyHostToDevice, sl->stream));
     HIPCHK(hipMemcpyAsync(d_len, len + c.begin, 4 * c.count, hipMemcpyHostToDevice, sl->stream));
-    if (sbft_launch_sha256(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len, d_dig,
-                           (uint32_t)c.count, sl->stream))
+    HIPCHK(hipMemcpyAsync(d_order, order.data(), 4 * c.count, hipMemcpyHostToDevice, sl->stream));
+    // pageable-source copies are staged before hipMemcpyAsync returns, so `order` may go out
+    // of scope; `rebased` is owned by the caller until the stream is synchronised anyway.
+    if (sbft_launch_sha256(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len,
+                           (const uint32_t*)d_order, d_dig, (uint32_t)c.count, sl->stream))
         return SBFT_GV_ELAUNCH;
     if (verify) {
         uint8_t* v = d_dig + fd;

@@ -20,9 +20,10 @@ int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const u
                             const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok, uint32_t n,
                             uint32_t* d_work, hipStream_t stream);
 // SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable >= 68 bytes
-// past its last message (funnel over-read). Digests are 32-byte big-endian.
+// past its last message (funnel over-read). Digests are 32-byte big-endian. d_order (may be
+// NULL): lane t hashes message d_order[t] — pass the messages sorted by length.
 int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
-                       uint8_t* d_dig, uint32_t n, hipStream_t stream);
+                       const uint32_t* d_order, uint8_t* d_dig, uint32_t n, hipStream_t stream);
 // Key derivation + ECDSA sign with caller nonces: Q = d*G, (r, s); status 1 = ok.
 int sbft_launch_p256_sign(const uint8_t* d_d, const uint8_t* d_k, const uint8_t* d_e, uint8_t* d_qx,
                           uint8_t* d_qy, uint8_t* d_r, uint8_t* d_s, uint8_t* d_status, uint32_t n,

@@ -125,12 +125,16 @@ __device__ void sha256_one(const uint8_t* msg, uint32_t len, uint32_t h[8]) {
     }
 }
 
+// order (optional): lane i hashes message order[i]. With order sorted by length, the lanes of
+// a wave walk messages of similar length, so no lane idles while its wave finishes a long one.
 __global__ __launch_bounds__(256) void sha256_kernel(const uint8_t* __restrict__ blob,
                                                      const uint64_t* __restrict__ off,
                                                      const uint32_t* __restrict__ len,
+                                                     const uint32_t* __restrict__ order,
                                                      uint8_t* __restrict__ dig, uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t i = order ? order[t] : t;
     uint32_t h[8];
     sha256_one(blob + off[i], len[i], h);
     uint4* out = reinterpret_cast<uint4*>(dig + 32ull * i);
@@ -143,11 +147,11 @@ __global__ __launch_bounds__(256) void sha256_kernel(const uint8_t* __restrict__
 }  // namespace sbft
 
 extern "C" int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
-                                  uint8_t* d_dig, uint32_t n, hipStream_t stream) {
+                                  const uint32_t* d_order, uint8_t* d_dig, uint32_t n, hipStream_t stream) {
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned blocks = (n + threads - 1) / threads;
     hipLaunchKernelGGL(sbft::sha256_kernel, dim3(blocks), dim3(threads), 0, stream, d_blob, d_off, d_len,
-                       d_dig, n);
+                       d_order, d_dig, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

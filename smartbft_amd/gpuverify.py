@@ -61,8 +61,8 @@ def load_library():
                                              ctypes.POINTER(ctypes.c_uint32)] + [_u8p] * 4 + \
                                             [ctypes.c_size_t, _u8p, _u8p]
     L.sbft_gv_verify_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 5 + [ctypes.c_size_t, _vp, _vp]
-    L.sbft_gv_sha256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 3 + [ctypes.c_size_t, _vp, _vp]
-    L.sbft_gv_sha256_verify_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 7 + \
+    L.sbft_gv_sha256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 4 + [ctypes.c_size_t, _vp, _vp]
+    L.sbft_gv_sha256_verify_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 8 + \
                                                 [ctypes.c_size_t, _vp, _vp, _vp]
     L.sbft_gv_sign_p256.argtypes = [_vp] + [_u8p] * 3 + [ctypes.c_size_t] + [_u8p] * 5
     L.sbft_gv_sign_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 3 + [ctypes.c_size_t] + [_vp] * 6
@@ -208,9 +208,10 @@ class GpuVerifier:
             self.ctx, dev, d_digest.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), d_qx.data_ptr(),
             d_qy.data_ptr(), n, d_ok.data_ptr(), self._stream(stream)), "sbft_gv_verify_p256_dev")
 
-    def sha256_dev(self, d_blob, d_off, d_len, d_dig, stream=None):
+    def sha256_dev(self, d_blob, d_off, d_len, d_dig, stream=None, d_order=None):
         n = d_off.numel()
         self._check(self.L.sbft_gv_sha256_dev(self.ctx, d_dig.device.index, d_blob.data_ptr(),
-                                              d_off.data_ptr(), d_len.data_ptr(), n,
-                                              d_dig.data_ptr(), self._stream(stream)),
+                                              d_off.data_ptr(), d_len.data_ptr(),
+                                              d_order.data_ptr() if d_order is not None else None,
+                                              n, d_dig.data_ptr(), self._stream(stream)),
                     "sbft_gv_sha256_dev")

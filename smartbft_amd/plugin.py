@@ -62,9 +62,10 @@ class RequestInfo:
 
 
 def _buf(b: bytes, keep: list):
+    """Borrowed read-only pointer into b (no copy; the C side never writes through it)."""
     if not b:
         return None
-    a = (ctypes.c_uint8 * len(b)).from_buffer_copy(b)
+    a = ctypes.c_char_p(bytes(b))
     keep.append(a)
     return ctypes.cast(a, _u8p)
 
@@ -79,7 +80,7 @@ def _sig(s: Signature, keep: list) -> _Signature:
 
 
 def _infos(buf, count: int) -> list[RequestInfo]:
-    parts = buf.raw.split(b"\0")
+    parts = buf.raw.split(b"\0", 2 * count)  # bounded: the rest of the buffer is unused
     return [RequestInfo(parts[2 * i].decode(), parts[2 * i + 1].decode()) for i in range(count)]
 
 
@@ -198,7 +199,7 @@ class Verifier:
 
     def VerifyProposal(self, p: Proposal) -> list[RequestInfo]:
         keep = []
-        cap = 64 + 2 * len(p.Payload)
+        cap = 64 + len(p.Payload)  # each request's two ids + NULs fit inside its own record
         infos = ctypes.create_string_buffer(cap)
         count, bad = ctypes.c_size_t(), ctypes.c_int64()
         err = ctypes.create_string_buffer(512)
@@ -210,7 +211,7 @@ class Verifier:
 
     def RequestsFromProposal(self, p: Proposal) -> list[RequestInfo]:
         keep = []
-        cap = 64 + 2 * len(p.Payload)
+        cap = 64 + len(p.Payload)
         infos = ctypes.create_string_buffer(cap)
         count = ctypes.c_size_t()
         rc = self.L.sbft_verifier_requests_from_proposal(self.h, ctypes.byref(_prop(p, keep)), infos, cap,

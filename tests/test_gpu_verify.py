@@ -132,6 +132,28 @@ def test_sha256_random_lengths_and_alignment(gpu):
     assert np.array_equal(got, exp)
 
 
+def test_sha256_dev_explicit_order(gpu):
+    """Device entry with a caller permutation (lane t hashes message order[t]): digests still
+    land at their own message's index, for an arbitrary (not length-sorted) permutation too."""
+    import torch
+    rng = np.random.default_rng(4)
+    n = 1500
+    lens = rng.integers(0, 5000, size=n).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
+    blob = rng.integers(0, 256, size=int(lens.sum()) + 128, dtype=np.uint8)
+    exp = oracle.sha256_batch(blob, off, lens)
+    dev = torch.device("cuda:0")
+    d_blob = torch.from_numpy(blob).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    for order in (np.argsort(-lens.astype(np.int64), kind="stable"), rng.permutation(n)):
+        d_dig = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+        d_ord = torch.from_numpy(order.astype(np.int32)).to(dev)
+        gpu.sha256_dev(d_blob, d_off, d_len, d_dig, d_order=d_ord)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_dig.cpu().numpy(), exp)
+
+
 def test_fused_hash_then_verify(gpu):
     rng = np.random.default_rng(9)
     n = 600

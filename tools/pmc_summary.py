@@ -1,0 +1,44 @@
+"""Summarise the rocprofv3 --pmc passes of tools/gpu_round.sh for the verify kernel into
+profiles/pmc_verify_latest.json (read by bench.py for roofline.traffic).
+
+Each counter comes from its own pass (gpurun_out/pmc_*/run_counter_collection.csv). Values are
+averaged over the kernel's dispatches. FETCH_SIZE / WRITE_SIZE are in KiB."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(src=os.path.join(ROOT, "gpurun_out"), dst=os.path.join(ROOT, "profiles", "pmc_verify_latest.json"),
+         kernel="sbft::p256_verify_kernel", n=1_000_000):
+    per = defaultdict(lambda: defaultdict(float))  # counter -> dispatch -> value
+    for f in glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv")):
+        for row in csv.DictReader(open(f)):
+            if not row["Kernel_Name"].startswith(kernel + "("):
+                continue
+            per[row["Counter_Name"]][(f, row["Dispatch_Id"])] += float(row["Counter_Value"])
+    raw = {c: sum(d.values()) / len(d) for c, d in per.items() if d}
+    if not raw:
+        sys.exit(f"no {kernel} dispatches under {src}/pmc_*")
+    out = {"kernel": kernel, "n": n, "source": "rocprofv3 --pmc, separate passes (gpurun_out/pmc_*), "
+           "mean over the kernel's dispatches", "counters_raw": raw}
+    if "SQ_INSTS_VALU" in raw and "SQ_WAVES" in raw:
+        out["valu_instructions_per_verify"] = raw["SQ_INSTS_VALU"] * 64 / n
+    if "FETCH_SIZE" in raw and "WRITE_SIZE" in raw:
+        out["hbm_bytes_per_launch"] = (raw["FETCH_SIZE"] + raw["WRITE_SIZE"]) * 1024
+        out["hbm_bytes_per_verify"] = out["hbm_bytes_per_launch"] / n
+    out["algorithmic_bytes_per_launch"] = 161 * n
+    out["note"] = ("FETCH_SIZE+WRITE_SIZE (KiB) x 1024, uncorrected: the x2 gfx950 correction in "
+                   "MI355X_MICROARCH.md is calibrated for 16-B/lane streaming reads, while most of these "
+                   "bytes are 4-B/lane scratch accesses (per-lane Q table + register spills). Algorithmic "
+                   "input+output is 161 B/verify.")
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
