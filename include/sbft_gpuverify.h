@@ -111,6 +111,28 @@ int sbft_gv_sign_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_d, const v
                           const void* d_digest, size_t n, void* d_qx, void* d_qy, void* d_r,
                           void* d_s, void* d_status, void* stream);
 
+/* Registered keys (fixed-base comb tables; smartbft_amd/csrc/p256_keyed.hip).
+ * Precomputes table[w][j] = j 2^(8w) Q (32 x 256 affine points, 512 KiB of HBM per key and
+ * device) so a signature under this key verifies with 64 table lookups and no doublings.
+ * Meant for the consenter keys of the configuration, which every VerifyConsenterSig /
+ * VerifySignature call checks against (view.go:631, :834; viewchanger.go:598, :718): the
+ * plugin registers them when it learns the membership (sbft_verifier_add_consenter).
+ * Returns SBFT_GV_EINVAL for a key that is not a valid P-256 point (such a key can only
+ * fail verification: use the unkeyed calls, which reject it). Registering the same key
+ * twice returns the same id. Ids start at 1. */
+int sbft_gv_register_key(sbft_gv_ctx* ctx, const uint8_t qx[32], const uint8_t qy[32], uint32_t* key_id);
+
+/* Verify n tuples (digest, r, s) against registered keys key_id[k]. Same verdict semantics
+ * as sbft_gv_verify_p256 (an unknown key id verifies false). Small batches run one
+ * wavefront per signature (latency path: one H2D, one launch, one D2H). */
+int sbft_gv_verify_p256_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* r, const uint8_t* s,
+                              const uint32_t* key_id, size_t n, uint8_t* ok_out);
+/* Same with digest_k = SHA-256(blob[off[k] .. off[k]+len[k])) computed inside the launch
+ * (consenter Signature.Msg hashing, A5 in SURVEY.md 8(a)). */
+int sbft_gv_sha256_verify_p256_keyed(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, const uint64_t* off,
+                                     const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint32_t* key_id,
+                                     size_t n, uint8_t* ok_out);
+
 /* Element-wise self-test of the device primitives (diagnostics; op codes in
  * smartbft_amd/csrc/p256_selftest.hip). a, b, out: n x 32 bytes big-endian. */
 int sbft_gv_selftest_field(sbft_gv_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, size_t n,

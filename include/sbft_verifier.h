@@ -60,7 +60,11 @@ typedef struct sbft_signature {
 /* A verifier bound to an engine context (not owned) and a verification sequence. */
 sbft_verifier* sbft_verifier_new(sbft_gv_ctx* ctx, uint64_t verification_sequence);
 void sbft_verifier_free(sbft_verifier* v);
-/* Consenter key registry (SEC1 uncompressed, 65 bytes). */
+/* Consenter key registry (SEC1 uncompressed, 65 bytes). With an engine context the key's
+ * fixed-base comb tables are precomputed here (sbft_gv_register_key), so VerifyConsenterSig /
+ * VerifySignature under it take the keyed launch (no doublings, one wavefront per signature).
+ * Returns a negative SBFT_GV_E* only on an engine failure; an invalid point is stored and
+ * every signature under it is rejected. */
 int sbft_verifier_add_consenter(sbft_verifier* v, uint64_t id, const uint8_t pubkey65[65]);
 /* api.Verifier.VerificationSequence (dependencies.go:65-66). */
 uint64_t sbft_verifier_verification_sequence(const sbft_verifier* v);

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cstring>
 #include <map>
@@ -55,6 +56,29 @@ struct Slot {
         return (uint32_t*)w.ptr;
     }
 
+    // registered-key comb tables (p256_keyed.hip): comb[id] is key id's table on this device,
+    // comb[0] the generator's; d_keytab mirrors comb for the kernels. Tables never move; a
+    // grown pointer array retires the old one only at destroy (kernels may still read it).
+    std::vector<void*> comb;
+    void** d_keytab = nullptr;
+    size_t keytab_cap = 0;
+    std::vector<void*> retired;
+    // pinned host staging for the small-batch (latency) path: one H2D and one D2H per call
+    uint8_t* pin = nullptr;
+    size_t pin_cap = 0;
+
+    int reserve_pinned(size_t bytes) {
+        if (bytes <= pin_cap) return SBFT_GV_OK;
+        if (pin) (void)hipHostFree(pin);
+        pin = nullptr;
+        pin_cap = 0;
+        size_t want = std::max(bytes, (size_t)1 << 20);
+        want = (want + 4095) & ~(size_t)4095;
+        if (hipHostMalloc((void**)&pin, want, hipHostMallocDefault) != hipSuccess) return SBFT_GV_ENOMEM;
+        pin_cap = want;
+        return SBFT_GV_OK;
+    }
+
     int reserve(size_t bytes) {
         if (bytes <= dcap) return SBFT_GV_OK;
         if (dbuf) (void)hipFree(dbuf);
@@ -76,6 +100,10 @@ struct sbft_gv_ctx {
     std::vector<Slot*> slots;
     uint32_t min_split = 65536;
     std::atomic<uint32_t> rr{0};
+    // registered public keys (x || y big-endian); index = key id, entry 0 = the generator
+    std::mutex keys_mu;
+    std::vector<std::array<uint8_t, 64>> keys;
+    std::atomic<uint32_t> nkeys{1};
 };
 
 extern "C" {
@@ -116,6 +144,15 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
         delete ctx;
         return SBFT_GV_ENODEV;
     }
+    // key id 0: the generator G (its comb table serves u1*G on the keyed path)
+    static const uint8_t GXY[64] = {
+        0x6b, 0x17, 0xd1, 0xf2, 0xe1, 0x2c, 0x42, 0x47, 0xf8, 0xbc, 0xe6, 0xe5, 0x63, 0xa4, 0x40, 0xf2,
+        0x77, 0x03, 0x7d, 0x81, 0x2d, 0xeb, 0x33, 0xa0, 0xf4, 0xa1, 0x39, 0x45, 0xd8, 0x98, 0xc2, 0x96,
+        0x4f, 0xe3, 0x42, 0xe2, 0xfe, 0x1a, 0x7f, 0x9b, 0x8e, 0xe7, 0xeb, 0x4a, 0x7c, 0x0f, 0x9e, 0x16,
+        0x2b, 0xce, 0x33, 0x57, 0x6b, 0x31, 0x5e, 0xce, 0xcb, 0xb6, 0x40, 0x68, 0x37, 0xbf, 0x51, 0xf5};
+    std::array<uint8_t, 64> g;
+    std::memcpy(g.data(), GXY, 64);
+    ctx->keys.push_back(g);
     *out = ctx;
     return SBFT_GV_OK;
 }
@@ -126,6 +163,11 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
         (void)hipSetDevice(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         if (s->dbuf) (void)hipFree(s->dbuf);
+        for (void* t : s->comb)
+            if (t) (void)hipFree(t);
+        if (s->d_keytab) (void)hipFree(s->d_keytab);
+        for (void* t : s->retired) (void)hipFree(t);
+        if (s->pin) (void)hipHostFree(s->pin);
         for (auto& kv : s->ws) {
             (void)hipStreamSynchronize(kv.first);
             if (kv.second.ptr) (void)hipFree(kv.second.ptr);
@@ -230,6 +272,7 @@ namespace {
 struct Chunk {
     Slot* slot;
     size_t begin, count;
+    size_t out_off = 0;  // keyed path: verdict offset inside the slot's pinned staging
 };
 
 std::vector<Chunk> plan(sbft_gv_ctx* ctx, size_t n) {
@@ -237,12 +280,12 @@ std::vector<Chunk> plan(sbft_gv_ctx* ctx, size_t n) {
     const size_t nd = ctx->slots.size();
     if (n < ctx->min_split || nd == 1) {
         const uint32_t k = ctx->rr.fetch_add(1) % nd;
-        out.push_back({ctx->slots[k], 0, n});
+        out.push_back({ctx->slots[k], 0, n, 0});
         return out;
     }
     for (size_t d = 0; d < nd; ++d) {
         const size_t b = n * d / nd, e = n * (d + 1) / nd;
-        if (e > b) out.push_back({ctx->slots[d], b, e - b});
+        if (e > b) out.push_back({ctx->slots[d], b, e - b, 0});
     }
     return out;
 }
@@ -417,7 +460,7 @@ int sbft_gv_selftest_field(sbft_gv_ctx* ctx, int op, const uint8_t* a, const uin
                            uint8_t* out) {
     if (!ctx) return SBFT_GV_EINVAL;
     if (n == 0) return SBFT_GV_OK;
-    if (!a || !b || !out || op < 0 || op > 9 || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    if (!a || !b || !out || op < 0 || op > 10 || n > 0xffffffffu) return SBFT_GV_EINVAL;
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) { return enqueue_selftest(c, op, a, b, out); });
 }
 
@@ -445,6 +488,202 @@ int sbft_gv_sha256_verify_p256(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blo
     return run_chunks(ctx, n, [&](const Chunk& c, size_t i) {
         return enqueue_hash(c, blob, blob_len, off, len, r, s, qx, qy, ok_out, dig_out, rebased[i]);
     });
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- registered keys
+namespace {
+
+// Build the comb tables of keys [sl->comb.size(), upto) on sl's device and refresh its device
+// pointer array. Caller holds sl->mu. valid_out (optional) receives the last key's status.
+int build_tables(Slot* sl, const std::vector<std::array<uint8_t, 64>>& keys, size_t upto, bool* valid_out) {
+    HIPCHK(hipSetDevice(sl->device));
+    const size_t tb = sbft_comb_table_bytes();
+    if (sl->comb.size() >= upto) return SBFT_GV_OK;
+    uint8_t* tmp = nullptr;  // qx | qy | status
+    HIPCHK(hipMalloc(&tmp, 256));
+    int rc = SBFT_GV_OK;
+    while (sl->comb.size() < upto && rc == SBFT_GV_OK) {
+        const size_t id = sl->comb.size();
+        void* t = nullptr;
+        if (hipMalloc(&t, tb) != hipSuccess) {
+            rc = SBFT_GV_ENOMEM;
+            break;
+        }
+        uint32_t st = 0;
+        if (hipMemcpyAsync(tmp, keys[id].data(), 64, hipMemcpyHostToDevice, sl->stream) != hipSuccess ||
+            sbft_launch_comb_build(tmp, tmp + 32, t, (uint32_t*)(tmp + 64), sl->stream) ||
+            hipMemcpyAsync(&st, tmp + 64, 4, hipMemcpyDeviceToHost, sl->stream) != hipSuccess ||
+            hipStreamSynchronize(sl->stream) != hipSuccess) {
+            (void)hipFree(t);
+            rc = SBFT_GV_EDEVICE;
+            break;
+        }
+        sl->comb.push_back(t);
+        if (valid_out) *valid_out = st == 1;
+    }
+    (void)hipFree(tmp);
+    if (rc) return rc;
+    if (sl->keytab_cap < sl->comb.size()) {
+        if (sl->d_keytab) sl->retired.push_back(sl->d_keytab);
+        sl->d_keytab = nullptr;
+        const size_t cap = std::max<size_t>(64, 2 * sl->comb.size());
+        HIPCHK(hipMalloc((void**)&sl->d_keytab, cap * sizeof(void*)));
+        sl->keytab_cap = cap;
+    }
+    HIPCHK(hipMemcpyAsync(sl->d_keytab, sl->comb.data(), sl->comb.size() * sizeof(void*), hipMemcpyHostToDevice,
+                          sl->stream));
+    HIPCHK(hipStreamSynchronize(sl->stream));
+    return SBFT_GV_OK;
+}
+
+// Small-batch keyed verify on one device through pinned staging: one H2D, one launch, one D2H.
+// Messages (blob != null) are hashed in the launch; otherwise digest holds 32-byte digests.
+int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t blob_len, const uint64_t* off,
+                  const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint32_t* key, uint32_t nkeys) {
+    Slot* sl = c.slot;
+    const size_t n = c.count, b = c.begin;
+    uint64_t lo = UINT64_MAX, hi = 0;
+    if (blob) {
+        for (size_t k = b; k < b + n; ++k) {
+            if (off[k] + len[k] > blob_len) return SBFT_GV_EINVAL;
+            lo = std::min(lo, off[k]);
+            hi = std::max(hi, off[k] + len[k]);
+        }
+        if (n == 0 || hi < lo) lo = hi = 0;
+    }
+    const size_t span = blob ? hi - lo : 0;
+    // staging layout (all 256-B aligned): r | s | key | (digest | blob+pad, off, len) | ok
+    const size_t f32 = align_up(32 * n, 256), fk = align_up(4 * n, 256);
+    const size_t fmsg = blob ? align_up(span + 128, 256) + align_up(8 * n, 256) + fk : f32;
+    const size_t fok = align_up(n, 256);
+    const size_t in_bytes = 2 * f32 + fk + fmsg;
+    HIPCHK(hipSetDevice(sl->device));
+    int rc = sl->reserve(in_bytes + fok);
+    if (rc) return rc;
+    rc = sl->reserve_pinned(in_bytes + fok);
+    if (rc) return rc;
+    uint8_t* h = sl->pin;
+    std::memcpy(h, r + 32 * b, 32 * n);
+    std::memcpy(h + f32, s + 32 * b, 32 * n);
+    std::memcpy(h + 2 * f32, key + b, 4 * n);
+    uint8_t* m = h + 2 * f32 + fk;
+    if (blob) {
+        std::memcpy(m, blob + lo, span);
+        std::memset(m + span, 0, 128);
+        uint64_t* o = (uint64_t*)(m + align_up(span + 128, 256));
+        for (size_t k = 0; k < n; ++k) o[k] = off[b + k] - lo;
+        std::memcpy((uint8_t*)o + align_up(8 * n, 256), len + b, 4 * n);
+    } else {
+        std::memcpy(m, digest + 32 * b, 32 * n);
+    }
+    uint8_t* d = sl->dbuf;
+    HIPCHK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, sl->stream));
+    const uint8_t* dm = d + 2 * f32 + fk;
+    const uint8_t* d_blob = blob ? dm : nullptr;
+    const uint64_t* d_off = blob ? (const uint64_t*)(dm + align_up(span + 128, 256)) : nullptr;
+    const uint32_t* d_len = blob ? (const uint32_t*)((const uint8_t*)d_off + align_up(8 * n, 256)) : nullptr;
+    uint8_t* d_ok = d + in_bytes;
+    if (sbft_launch_p256_verify_keyed(blob ? nullptr : dm, d_blob, d_off, d_len, d, d + f32,
+                                      (const uint32_t*)(d + 2 * f32), (const void* const*)sl->d_keytab, nkeys, d_ok,
+                                      (uint32_t)n, sl->stream))
+        return SBFT_GV_ELAUNCH;
+    HIPCHK(hipMemcpyAsync(h + in_bytes, d_ok, n, hipMemcpyDeviceToHost, sl->stream));
+    c.out_off = in_bytes;
+    return SBFT_GV_OK;
+}
+
+int run_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* blob, size_t blob_len, const uint64_t* off,
+              const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint32_t* key, size_t n,
+              uint8_t* ok_out) {
+    // snapshot of the published keys (a registration holds keys_mu until it is published)
+    std::vector<std::array<uint8_t, 64>> keys;
+    {
+        std::lock_guard<std::mutex> g(ctx->keys_mu);
+        keys.assign(ctx->keys.begin(), ctx->keys.begin() + ctx->nkeys.load());
+    }
+    const uint32_t nkeys = (uint32_t)keys.size();
+    std::vector<Chunk> chunks = plan(ctx, n);
+    std::vector<std::unique_lock<std::mutex>> locks;
+    locks.reserve(chunks.size());
+    for (auto& c : chunks) locks.emplace_back(c.slot->mu);
+    int rc = SBFT_GV_OK;
+    for (size_t i = 0; i < chunks.size() && rc == SBFT_GV_OK; ++i) {
+        rc = build_tables(chunks[i].slot, keys, nkeys, nullptr);
+        if (rc == SBFT_GV_OK)
+            rc = enqueue_keyed(chunks[i], digest, blob, blob_len, off, len, r, s, key, nkeys);
+    }
+    for (auto& c : chunks) {
+        (void)hipSetDevice(c.slot->device);
+        if (hipStreamSynchronize(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
+    }
+    if (rc == SBFT_GV_OK)
+        for (auto& c : chunks) std::memcpy(ok_out + c.begin, c.slot->pin + c.out_off, c.count);
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sbft_gv_register_key(sbft_gv_ctx* ctx, const uint8_t qx[32], const uint8_t qy[32], uint32_t* key_id) {
+    if (!ctx || !qx || !qy || !key_id) return SBFT_GV_EINVAL;
+    *key_id = 0;
+    std::array<uint8_t, 64> k;
+    std::memcpy(k.data(), qx, 32);
+    std::memcpy(k.data() + 32, qy, 32);
+    std::lock_guard<std::mutex> g(ctx->keys_mu);
+    for (size_t i = 1; i < ctx->keys.size(); ++i)
+        if (ctx->keys[i] == k) {
+            *key_id = (uint32_t)i;
+            return SBFT_GV_OK;
+        }
+    ctx->keys.push_back(k);
+    const size_t upto = ctx->keys.size();
+    int rc = SBFT_GV_OK;
+    for (Slot* sl : ctx->slots) {
+        std::lock_guard<std::mutex> lk(sl->mu);
+        bool valid = true;
+        rc = build_tables(sl, ctx->keys, upto, &valid);
+        if (rc == SBFT_GV_OK && !valid) rc = SBFT_GV_EINVAL;
+        if (rc) break;
+    }
+    if (rc) {
+        // roll the key back on every device that built it
+        for (Slot* sl : ctx->slots) {
+            std::lock_guard<std::mutex> lk(sl->mu);
+            if (sl->comb.size() == upto) {
+                (void)hipSetDevice(sl->device);
+                (void)hipFree(sl->comb.back());
+                sl->comb.pop_back();
+            }
+        }
+        ctx->keys.pop_back();
+        return rc;
+    }
+    ctx->nkeys = (uint32_t)upto;
+    *key_id = (uint32_t)(upto - 1);
+    return SBFT_GV_OK;
+}
+
+int sbft_gv_verify_p256_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* r, const uint8_t* s,
+                              const uint32_t* key_id, size_t n, uint8_t* ok_out) {
+    if (!ctx) return SBFT_GV_EINVAL;
+    if (n == 0) return SBFT_GV_OK;
+    if (!digest || !r || !s || !key_id || !ok_out || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    return run_keyed(ctx, digest, nullptr, 0, nullptr, nullptr, r, s, key_id, n, ok_out);
+}
+
+int sbft_gv_sha256_verify_p256_keyed(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, const uint64_t* off,
+                                     const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint32_t* key_id,
+                                     size_t n, uint8_t* ok_out) {
+    if (!ctx) return SBFT_GV_EINVAL;
+    if (n == 0) return SBFT_GV_OK;
+    if ((!blob && blob_len) || !off || !len || !r || !s || !key_id || !ok_out || n > 0xffffffffu)
+        return SBFT_GV_EINVAL;
+    static const uint8_t empty = 0;
+    return run_keyed(ctx, nullptr, blob ? blob : &empty, blob_len, off, len, r, s, key_id, n, ok_out);
 }
 
 }  // extern "C"

@@ -1,0 +1,234 @@
+// p256_inv.hpp — variable-time modular inversion mod the P-256 group order n by batched
+// divsteps (Bernstein–Yang "safegcd", 30 divsteps per batch on 32-bit words).
+//
+// Used where one inversion sits on a latency path: the keyed single-signature verify
+// (p256_keyed.hip), where a Fermat chain (~250 sequential squarings mod n, ~95k VALU
+// instructions) would dominate the launch. Verification data is public, so a variable-time
+// inversion is acceptable (crypto/ecdsa.Verify's own inversion is variable time too).
+//
+// Header-only and free of HIP types so that tests/native can compile the same code for the
+// CPU with g++ and check it against Python's pow(x, -1, n).
+//
+// Algorithm (restated from Bernstein & Yang, "Fast constant-time gcd computation and modular
+// inversion", 2019, sections 8-10; original divstep with delta starting at 1):
+//   f = n, g = x, d = 0, e = 1; invariant d*x = f, e*x = g (mod n).
+//   repeat: take the low 32 bits of f, g; run 30 divsteps on them (5 per table lookup), accumulating the 2x2
+//   transition matrix T (entries bounded by 2^30); then (f, g) <- T (f, g) / 2^30 exactly and
+//   (d, e) <- T (d, e) / 2^30 mod n; until g == 0. Then f = +-1 and x^-1 = +-d.
+//   At most 741 divsteps (25 batches) for 256-bit inputs (BY19 Theorem 11.2 bound).
+// Numbers are signed radix-2^30: 9 limbs, limbs 0..7 in [0, 2^30), limb 8 signed.
+#pragma once
+#include <stdint.h>
+
+#include "p256_inv_table.inc"
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#endif
+
+#if defined(__HIPCC__)
+#define SBFT_HD __host__ __device__ __forceinline__
+#else
+#define SBFT_HD static inline
+#endif
+#if defined(__HIPCC__)
+#define SBFT_UNROLL1 _Pragma("unroll 1")
+#else
+#define SBFT_UNROLL1
+#endif
+
+namespace sbft {
+namespace inv {
+
+// acc + a*b (signed 32 x 32 -> 64): one v_mad_i64_i32 on the device
+SBFT_HD int64_t mac(int64_t acc, int32_t a, int32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int64_t r;
+    uint64_t cc;
+    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "v"(b), "v"(acc));
+    return r;
+#else
+    return acc + (int64_t)a * b;
+#endif
+}
+
+struct s30 {
+    int32_t v[9];
+};
+
+#define SBFT_M30 0x3fffffff
+// n in radix 2^30 and n^-1 mod 2^30
+#define SBFT_N30_INIT {0x3c632551, 0x0ee72b0b, 0x3179e84f, 0x39beab69, 0x3fffffbc, 0x3fffffff, 0x00000fff, 0x3fffc000, 0x0000ffff}
+#define SBFT_NINV30 0x11ff43b1u  // n^-1 mod 2^30 (so that d + md*n = 0 mod 2^30 for md = -d * NINV30)
+
+SBFT_HD void pack30(s30& r, const uint32_t a[8]) {
+    // 8 x 32-bit little-endian limbs -> 9 x 30-bit limbs (value < 2^256)
+    for (int i = 0; i < 9; ++i) {
+        const int bit = 30 * i, w = bit >> 5, sh = bit & 31;
+        uint64_t x = (uint64_t)a[w] >> sh;
+        if (w + 1 < 8) x |= (uint64_t)a[w + 1] << (32 - sh);
+        r.v[i] = (int32_t)(x & SBFT_M30);
+    }
+}
+
+// 30 original divsteps on the low words of f (odd) and g, 5 at a time through the transition
+// table (p256_inv_table.inc, tools/gen_inv_table.py): a step's outcome depends only on
+// delta > 0 and the parity of g, so 5 steps depend on clamp(delta, -4, 5) and the low 5 bits
+// of f and g. Returns delta; T = [u v; q r] with 2^30 (f', g') = T (f, g). `tab` is the table
+// (in LDS on the device: one ~70-cycle ds_read per 5 divsteps on the dependent chain).
+SBFT_HD int32_t divsteps30(int32_t delta, uint32_t f, uint32_t g, const uint32_t* tab, int32_t& u, int32_t& v,
+                           int32_t& q, int32_t& r) {
+    int32_t uu = 1, vv = 0, qq = 0, rr = 1;
+    for (int j = 0; j < 6; ++j) {
+        const int32_t dc = delta < -4 ? -4 : (delta > 5 ? 5 : delta);
+        const uint32_t idx = ((uint32_t)(dc + 4) << 9) | (((f >> 1) & 15u) << 5) | (g & 31u);
+        const uint32_t w0 = tab[2 * idx], w1 = tab[2 * idx + 1];
+        const int32_t a = (int32_t)(w0 << 24) >> 24, b = (int32_t)(w0 << 16) >> 24;
+        const int32_t c = (int32_t)(w0 << 8) >> 24, d = (int32_t)w0 >> 24;
+        // low words advance by 5 divsteps (the low 5 bits of a f + b g and c f + d g are zero)
+        const uint32_t nf = ((uint32_t)a * f + (uint32_t)b * g) >> 5;
+        const uint32_t ng = ((uint32_t)c * f + (uint32_t)d * g) >> 5;
+        f = nf;
+        g = ng;
+        // T <- M T
+        const int32_t nu = a * uu + b * qq, nv = a * vv + b * rr;
+        const int32_t nq = c * uu + d * qq, nr = c * vv + d * rr;
+        uu = nu;
+        vv = nv;
+        qq = nq;
+        rr = nr;
+        const int32_t cst = (int32_t)(w1 << 16) >> 24;
+        delta = ((w1 & 1u) ? -delta : delta) + cst;
+    }
+    u = uu;
+    v = vv;
+    q = qq;
+    r = rr;
+    return delta;
+}
+
+// (f, g) <- T (f, g) / 2^30 (exact)
+SBFT_HD void update_fg(s30& f, s30& g, int32_t u, int32_t v, int32_t q, int32_t r) {
+    int64_t cf = mac(mac(0, u, f.v[0]), v, g.v[0]);
+    int64_t cg = mac(mac(0, q, f.v[0]), r, g.v[0]);
+    cf >>= 30;
+    cg >>= 30;
+    for (int i = 1; i < 9; ++i) {
+        cf = mac(mac(cf, u, f.v[i]), v, g.v[i]);
+        cg = mac(mac(cg, q, f.v[i]), r, g.v[i]);
+        f.v[i - 1] = (int32_t)(cf & SBFT_M30);
+        g.v[i - 1] = (int32_t)(cg & SBFT_M30);
+        cf >>= 30;
+        cg >>= 30;
+    }
+    f.v[8] = (int32_t)cf;
+    g.v[8] = (int32_t)cg;
+}
+
+// (d, e) <- (T (d, e) + (md, me) n) / 2^30 with md, me chosen to clear the low 30 bits.
+// |d|, |e| grow by at most n per batch (|u| + |v| <= 2^30), so 25 batches stay below 2^262.
+SBFT_HD void update_de(s30& d, s30& e, int32_t u, int32_t v, int32_t q, int32_t r) {
+    const int32_t N30[9] = SBFT_N30_INIT;
+    int64_t cd = mac(mac(0, u, d.v[0]), v, e.v[0]);
+    int64_t ce = mac(mac(0, q, d.v[0]), r, e.v[0]);
+    const int32_t md = (int32_t)((0u - (uint32_t)cd * SBFT_NINV30) & SBFT_M30);
+    const int32_t me = (int32_t)((0u - (uint32_t)ce * SBFT_NINV30) & SBFT_M30);
+    cd = mac(cd, md, N30[0]);
+    ce = mac(ce, me, N30[0]);
+    cd >>= 30;
+    ce >>= 30;
+    for (int i = 1; i < 9; ++i) {
+        cd = mac(mac(mac(cd, u, d.v[i]), v, e.v[i]), md, N30[i]);
+        ce = mac(mac(mac(ce, q, d.v[i]), r, e.v[i]), me, N30[i]);
+        d.v[i - 1] = (int32_t)(cd & SBFT_M30);
+        e.v[i - 1] = (int32_t)(ce & SBFT_M30);
+        cd >>= 30;
+        ce >>= 30;
+    }
+    d.v[8] = (int32_t)cd;
+    e.v[8] = (int32_t)ce;
+}
+
+SBFT_HD bool is_zero30(const s30& a) {
+    int32_t o = 0;
+    for (int i = 0; i < 9; ++i) o |= a.v[i];
+    return o == 0;
+}
+
+// a += k * n for a small signed k, renormalising limbs 0..7 to [0, 2^30)
+SBFT_HD void add_kn(s30& a, int32_t k) {
+    const int32_t N30[9] = SBFT_N30_INIT;
+    int64_t c = 0;
+    for (int i = 0; i < 8; ++i) {
+        c += (int64_t)a.v[i] + (int64_t)k * N30[i];
+        a.v[i] = (int32_t)(c & SBFT_M30);
+        c >>= 30;
+    }
+    a.v[8] = (int32_t)(c + a.v[8] + (int64_t)k * N30[8]);
+}
+
+// a (normalised, |a| < 2^262) -> [0, n), then 8 x 32-bit limbs
+SBFT_HD void reduce_unpack(uint32_t out[8], s30 a) {
+    // a = t * 2^240 + low with t = a.v[8]; n = 2^256 - small, so k = -floor(a / 2^256) gets
+    // within a few n of [0, n)
+    add_kn(a, -(a.v[8] >> 16));
+    for (int it = 0; it < 4 && a.v[8] < 0; ++it) add_kn(a, 1);
+    const int32_t N30[9] = SBFT_N30_INIT;
+    for (int it = 0; it < 4; ++it) {
+        // a >= n ?
+        bool ge = true;
+        for (int i = 8; i >= 0; --i) {
+            if (a.v[i] != N30[i]) {
+                ge = a.v[i] > N30[i];
+                break;
+            }
+        }
+        if (!ge) break;
+        add_kn(a, -1);
+    }
+    for (int w = 0; w < 8; ++w) {
+        const int bit = 32 * w, i = bit / 30, sh = bit % 30;
+        uint64_t x = (uint64_t)(uint32_t)a.v[i] >> sh;
+        if (i + 1 < 9) x |= (uint64_t)(uint32_t)a.v[i + 1] << (30 - sh);
+        if (i + 2 < 9 && 60 - sh < 64) x |= (uint64_t)(uint32_t)a.v[i + 2] << (60 - sh);
+        out[w] = (uint32_t)x;
+    }
+}
+
+// out = x^-1 mod n for 0 < x < n (8 x 32-bit little-endian limbs). x = 0 gives 0.
+// tab: SBFT_DIVSTEP5_TABLE (p256_inv_table.inc).
+SBFT_HD void inv_mod_n(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) {
+    s30 f = {SBFT_N30_INIT}, g, d, e;
+    pack30(g, x);
+    for (int i = 0; i < 9; ++i) {
+        d.v[i] = 0;
+        e.v[i] = 0;
+    }
+    e.v[0] = 1;
+    int32_t delta = 1;
+SBFT_UNROLL1
+    for (int batch = 0; batch < 26 && !is_zero30(g); ++batch) {
+        int32_t u, v, q, r;
+        delta = divsteps30(delta, (uint32_t)f.v[0], (uint32_t)g.v[0], tab, u, v, q, r);
+        update_de(d, e, u, v, q, r);
+        update_fg(f, g, u, v, q, r);
+    }
+    // f = +-1: x^-1 = f * d
+    if (f.v[8] < 0) {
+        for (int i = 0; i < 9; ++i) d.v[i] = -d.v[i];
+        add_kn(d, 0);  // renormalise limbs
+    }
+    reduce_unpack(out, d);
+}
+
+#if defined(__HIPCC__)
+__device__ __constant__ static const uint32_t C_DIVSTEP5[SBFT_DIVSTEP5_WORDS] = SBFT_DIVSTEP5_TABLE;
+// Copy the transition table into LDS (all threads of the block; ends with a barrier).
+__device__ __forceinline__ void stage_divstep_table(uint32_t* lds) {
+    for (uint32_t i = threadIdx.x; i < SBFT_DIVSTEP5_WORDS / 4; i += blockDim.x)
+        reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(C_DIVSTEP5)[i];
+    __syncthreads();
+}
+#endif
+
+}  // namespace inv
+}  // namespace sbft

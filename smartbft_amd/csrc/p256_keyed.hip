@@ -1,0 +1,379 @@
+// p256_keyed.hip — P-256 verification against REGISTERED public keys (consenter keys), gfx950.
+//
+// SmartBFT's consenter signatures (VerifyConsenterSig at internal/bft/view.go:631 and :834,
+// viewchanger.go:718; VerifySignature at viewchanger.go:598) are always checked against one of
+// the n consenter keys of the configuration. Those keys are known before any signature
+// arrives, so the engine precomputes a fixed-base comb table per key when it is registered
+// (the plugin's key registry, include/sbft_verifier.h sbft_verifier_add_consenter), exactly
+// as every P-256 implementation does for the generator G:
+//
+//   table[w][j] = j * 2^(8w) * Q   (w = 0..31, j = 1..255), affine, Montgomery form mod p
+//
+// 32 windows x 256 entries x 64 B = 512 KiB per key in HBM (100 consenters = 51 MiB; the
+// generator's table is key slot 0). Then u1*G + u2*Q = sum_w table_G[w][byte_w(u1)] +
+// sum_w table_Q[w][byte_w(u2)]: 64 table points and NO doublings.
+//
+// p256_verify_keyed_wave_kernel (latency path, one wavefront per signature):
+//   all lanes: [optional SHA-256 of the message] ; range checks ; w = s^-1 (safegcd,
+//   p256_inv.hpp) ; u1 = e w, u2 = r w
+//   lane l: loads ONE table point (l < 32: G window l of u1; l >= 32: Q window l-32 of u2)
+//   6-level butterfly reduction over the wave (ds_swizzle/bpermute exchanges), every
+//   addition the general one (infinity on either side, doubling, cancellation)
+//   lane 0: accept iff R != infinity and x(R) = r (mod n), projectively against r and r + n.
+// The dependent chain is ~6 point additions + one inversion instead of 256 doublings, which
+// is what makes a 67-signature commit quorum a ~100 us launch instead of a ~2 ms one.
+//
+// Verdicts are bit-exact with Go crypto/ecdsa.Verify (same semantics as p256_verify.hip;
+// oracle/p256_oracle.c is the parity reference). An unregistered/invalid key id verifies false.
+#include "p256_inv.hpp"
+#include "p256_point.hpp"
+#include "sbft_kernels.h"
+#include "sha256_dev.hpp"
+
+namespace sbft {
+
+#define COMB_WINDOWS 32
+#define COMB_ENTRIES 256
+// uint4 units per entry (64 B: x limbs 0..7, y limbs 0..7) and per key table
+#define COMB_ENTRY_U4 4
+#define COMB_KEY_U4 (COMB_WINDOWS * COMB_ENTRIES * COMB_ENTRY_U4)
+
+SBFT_DEV void to_affine_mont(fe& x, fe& y, const jp& p) {
+    fe zi, zi2, zi3;
+    fp_inv(zi, p.z);
+    fp_sqr(zi2, zi);
+    fp_mul(zi3, zi2, zi);
+    fp_mul(x, p.x, zi2);
+    fp_mul(y, p.y, zi3);
+    fp_canon(x, x);
+    fp_canon(y, y);
+}
+
+// One lane per table entry (w, j): j * 2^(8w) * Q. status[0] = 1 iff Q is a valid key
+// (canonical coordinates on the curve); the table is written either way.
+__global__ __launch_bounds__(256) void p256_comb_build_kernel(const uint8_t* __restrict__ qxb,
+                                                              const uint8_t* __restrict__ qyb,
+                                                              uint4* __restrict__ table,
+                                                              uint32_t* __restrict__ status) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= COMB_WINDOWS * COMB_ENTRIES) return;
+    const uint32_t w = t / COMB_ENTRIES, j = t % COMB_ENTRIES;
+    const fe qx = load_be32(qxb), qy = load_be32(qyb);
+    bool valid = fe_lt(qx, P256_P) && fe_lt(qy, P256_P);
+    const fe r2p = fe_const(C_R2P);
+    jp base;
+    fp_mul(base.x, qx, r2p);
+    fp_mul(base.y, qy, r2p);
+    base.z = fe_const(C_ONEP);
+    {
+        fe lhs, rhs, tt;
+        fp_sqr(lhs, base.y);
+        fp_sqr(rhs, base.x);
+        fp_mul(rhs, rhs, base.x);
+        fp_add(tt, base.x, base.x);
+        fp_add(tt, tt, base.x);
+        fp_sub(rhs, rhs, tt);
+        fp_add(rhs, rhs, fe_const(C_BM));
+        fp_canon(lhs, lhs);
+        fp_canon(rhs, rhs);
+        valid = valid && fe_eq(lhs, rhs);
+    }
+    if (t == 0) status[0] = valid ? 1u : 0u;
+    uint4* out = table + (size_t)t * COMB_ENTRY_U4;
+    if (!valid || j == 0) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        out[0] = z;
+        out[1] = z;
+        out[2] = z;
+        out[3] = z;
+        return;
+    }
+#pragma unroll 1
+    for (uint32_t i = 0; i < 8 * w; ++i) pt_dbl(base, base);  // 2^(8w) Q (never infinity: n is prime)
+    jp acc;
+    bool inf = true;
+    acc = base;
+#pragma unroll 1
+    for (int b = 7; b >= 0; --b) {
+        if (!inf) pt_dbl(acc, acc);
+        pt_add_jac(acc, inf, base, ((j >> b) & 1u) != 0);
+    }
+    fe x, y;
+    to_affine_mont(x, y, acc);  // j < n, so j 2^(8w) Q is never infinity
+    out[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+    out[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+    out[2] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
+    out[3] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
+}
+
+SBFT_DEV u32 shfl_xor_u32(u32 v, int mask) { return (u32)__shfl_xor((int)v, mask, 64); }
+SBFT_DEV void shfl_xor_fe(fe& o, const fe& a, int mask) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = shfl_xor_u32(a.v[k], mask);
+}
+
+// byte w (0..31, little-endian) of a 256-bit value, w lane-varying
+SBFT_DEV u32 byte_of(const fe& a, u32 w) {
+    const u32 limb_i = w >> 2;
+    u32 limb = a.v[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) limb = (limb_i == (u32)k) ? a.v[k] : limb;
+    return (limb >> (8 * (w & 3))) & 255u;
+}
+
+
+// ---- cooperative point additions (latency path) ----
+// In the butterfly, every lane of an aligned group holds the same pair of points, so the
+// group splits ONE addition's independent field multiplications over its lanes (lane & 3 in
+// quads, lane & 1 in pairs) and re-broadcasts the products with DPP quad permutes: the
+// dependent chain of a Jacobian addition drops from 16 multiplications to 5.
+template <int CTRL>
+SBFT_DEV fe dpp_fe(const fe& a) {
+    fe o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)a.v[k], CTRL, 0xf, 0xf, false);
+    return o;
+}
+#define QB(J) ((J) * 0x55)               // quad_perm [J,J,J,J]
+#define PB0 0xA0                         // quad_perm [0,0,2,2]
+#define PB1 0xF5                         // quad_perm [1,1,3,3]
+SBFT_DEV fe sel4(u32 j, const fe& a0, const fe& a1, const fe& a2, const fe& a3) {
+    fe o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = j == 0 ? a0.v[k] : (j == 1 ? a1.v[k] : (j == 2 ? a2.v[k] : a3.v[k]));
+    return o;
+}
+SBFT_DEV fe sel2(u32 j, const fe& a0, const fe& a1) {
+    fe o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = j == 0 ? a0.v[k] : a1.v[k];
+    return o;
+}
+
+// Resolve the special cases of P1 + P2 given the generic result (x3, y3, z3) computed from
+// H = U2 - U1 and R = S2 - S1: infinity operands, P1 = P2 (doubling), P1 = -P2 (infinity).
+SBFT_DEV void finish_add(jp& acc, bool& inf, const jp& p1, bool i1, const jp& p2, bool i2, const fe& H,
+                         const fe& R, const fe& x3, const fe& y3, const fe& z3) {
+    const bool hz = fp_is_zero(H), rz = fp_is_zero(R);
+    const bool both = !i1 && !i2;
+    jp out;
+    out.x = x3;
+    out.y = y3;
+    out.z = z3;
+    bool oinf = hz && !rz;
+    const bool need_dbl = both && hz && rz;
+    if (__builtin_expect(__any(need_dbl), 0)) {
+        jp d;
+        pt_dbl(d, p1);
+        jp_sel(out, need_dbl, d);
+        if (need_dbl) oinf = false;
+    }
+    jp_sel(out, i1, p2);
+    jp_sel(out, i2 && !i1, p1);
+    acc = out;
+    inf = both ? oinf : (i1 && i2);
+}
+
+// Level 0: P1, P2 affine (Z = 1), lane pairs (2m, 2m+1); P1 is the even lane's point.
+SBFT_DEV void coop_add_affine_pair(jp& acc, bool& inf, u32 lane) {
+    jp o;
+    o.x = dpp_fe<0xB1>(acc.x);  // quad_perm [1,0,3,2]: the partner lane
+    o.y = dpp_fe<0xB1>(acc.y);
+    const bool oinf = __builtin_amdgcn_mov_dpp(inf ? 1 : 0, 0xB1, 0xf, 0xf, false) != 0;
+    const u32 j = lane & 1u;
+    jp p1, p2;
+    p1.x = sel2(j, acc.x, o.x);
+    p1.y = sel2(j, acc.y, o.y);
+    p2.x = sel2(j, o.x, acc.x);
+    p2.y = sel2(j, o.y, acc.y);
+    p1.z = p2.z = fe_const(C_ONEP);
+    const bool i1 = j ? oinf : inf, i2 = j ? inf : oinf;
+    fe H, R, t;
+    fp_sub(H, p2.x, p1.x);
+    fp_sub(R, p2.y, p1.y);
+    // S1: HH = H^2 (j0), RR = R^2 (j1)
+    {
+        const fe a = sel2(j, H, R);
+        fp_mul(t, a, a);
+    }
+    const fe HH = dpp_fe<PB0>(t), RR = dpp_fe<PB1>(t);
+    // S2: HHH = H HH (j0), V = X1 HH (j1)
+    fp_mul(t, sel2(j, H, p1.x), HH);
+    const fe HHH = dpp_fe<PB0>(t), V = dpp_fe<PB1>(t);
+    fe X3, VX;
+    fp_sub(X3, RR, HHH);
+    fp_sub(X3, X3, V);
+    fp_sub(X3, X3, V);
+    fp_sub(VX, V, X3);
+    // S3: Y1 HHH (j0), R (V - X3) (j1)
+    fp_mul(t, sel2(j, p1.y, R), sel2(j, HHH, VX));
+    fe Y3;
+    fp_sub(Y3, dpp_fe<PB1>(t), dpp_fe<PB0>(t));
+    finish_add(acc, inf, p1, i1, p2, i2, H, R, X3, Y3, H);
+}
+
+// Level lvl >= 1: Jacobian P1 (lower half-group) + P2 (upper), computed by each quad.
+SBFT_DEV void coop_add_jac_quad(jp& acc, bool& inf, u32 lane, int lvl) {
+    const int m = 1 << lvl;
+    jp o;
+    shfl_xor_fe(o.x, acc.x, m);
+    shfl_xor_fe(o.y, acc.y, m);
+    shfl_xor_fe(o.z, acc.z, m);
+    const bool oinf = shfl_xor_u32(inf ? 1u : 0u, m) != 0;
+    const bool hi = ((lane >> lvl) & 1u) != 0;
+    jp p1, p2;
+    p1.x = sel2(hi, acc.x, o.x);
+    p1.y = sel2(hi, acc.y, o.y);
+    p1.z = sel2(hi, acc.z, o.z);
+    p2.x = sel2(hi, o.x, acc.x);
+    p2.y = sel2(hi, o.y, acc.y);
+    p2.z = sel2(hi, o.z, acc.z);
+    const bool i1 = hi ? oinf : inf, i2 = hi ? inf : oinf;
+    const u32 j = lane & 3u;
+    fe t;
+    // S1: A = Z1^2 (j0), B = Z2^2 (j1), C = Z1 Z2 (j2)
+    fp_mul(t, sel4(j, p1.z, p2.z, p1.z, p1.z), sel4(j, p1.z, p2.z, p2.z, p1.z));
+    const fe A = dpp_fe<QB(0)>(t), B = dpp_fe<QB(1)>(t), C = dpp_fe<QB(2)>(t);
+    // S2: U1 = X1 B (j0), U2 = X2 A (j1), T1 = Z1 A (j2), T2 = Z2 B (j3)
+    fp_mul(t, sel4(j, p1.x, p2.x, p1.z, p2.z), sel4(j, B, A, A, B));
+    const fe U1 = dpp_fe<QB(0)>(t), U2 = dpp_fe<QB(1)>(t), T1 = dpp_fe<QB(2)>(t), T2 = dpp_fe<QB(3)>(t);
+    fe H;
+    fp_sub(H, U2, U1);
+    // S3: S1 = Y1 T2 (j0), S2 = Y2 T1 (j1), Z3 = C H (j2), HH = H^2 (j3)
+    fp_mul(t, sel4(j, p1.y, p2.y, C, H), sel4(j, T2, T1, H, H));
+    const fe S1 = dpp_fe<QB(0)>(t), S2 = dpp_fe<QB(1)>(t), Z3 = dpp_fe<QB(2)>(t), HH = dpp_fe<QB(3)>(t);
+    fe R;
+    fp_sub(R, S2, S1);
+    // S4: RR = R^2 (j0), HHH = H HH (j1), V = U1 HH (j2)
+    fp_mul(t, sel4(j, R, H, U1, R), sel4(j, R, HH, HH, R));
+    const fe RR = dpp_fe<QB(0)>(t), HHH = dpp_fe<QB(1)>(t), V = dpp_fe<QB(2)>(t);
+    fe X3, VX;
+    fp_sub(X3, RR, HHH);
+    fp_sub(X3, X3, V);
+    fp_sub(X3, X3, V);
+    fp_sub(VX, V, X3);
+    // S5: S1 HHH (j0), R (V - X3) (j1)
+    fp_mul(t, sel2(j & 1u, S1, R), sel2(j & 1u, HHH, VX));
+    fe Y3;
+    fp_sub(Y3, dpp_fe<QB(1)>(t), dpp_fe<QB(0)>(t));
+    finish_add(acc, inf, p1, i1, p2, i2, H, R, X3, Y3, Z3);
+}
+
+// x(R) mod n == r, projectively; r is the plain (non-Montgomery) 256-bit value in [1, n)
+SBFT_DEV bool x_matches_r(const jp& R, const fe& r) {
+    const fe r2p = fe_const(C_R2P);
+    fe z2, lhs, xc, rm;
+    fp_sqr(z2, R.z);
+    fp_canon(xc, R.x);
+    fp_mul(rm, r, r2p);
+    fp_mul(lhs, rm, z2);
+    fp_canon(lhs, lhs);
+    bool accept = fe_eq(lhs, xc);
+    fe rn;
+    u64 c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        c = (u64)r.v[k] + P256_N[k] + c;
+        rn.v[k] = lo32(c);
+        c >>= 32;
+    }
+    if (c == 0 && fe_lt(rn, P256_P)) {
+        fp_mul(rm, rn, r2p);
+        fp_mul(lhs, rm, z2);
+        fp_canon(lhs, lhs);
+        accept = accept || fe_eq(lhs, xc);
+    }
+    return accept;
+}
+
+// One wavefront per tuple. Digests come either precomputed (digest != null) or as messages
+// blob[off[t] .. +len[t]) hashed here (digest == null). key[t] indexes keytab (slot 0 is G's
+// table, so registered keys are 1 .. nkeys-1).
+__global__ __launch_bounds__(64) void p256_verify_keyed_wave_kernel(
+    const uint8_t* __restrict__ digest, const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint8_t* __restrict__ rr, const uint8_t* __restrict__ ss,
+    const uint32_t* __restrict__ key, const uint4* const* __restrict__ keytab, uint32_t nkeys,
+    uint8_t* __restrict__ ok, uint32_t n) {
+    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    inv::stage_divstep_table(dtab);
+    const uint32_t t = blockIdx.x;
+    const u32 lane = threadIdx.x;
+    if (t >= n) return;  // uniform per wave
+
+    fe e_raw;
+    if (digest) {
+        e_raw = load_be32(digest + 32ull * t);
+    } else {
+        uint32_t h[8];
+        sha256_one(blob + off[t], len[t], h);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e_raw.v[k] = h[7 - k];
+    }
+    const fe r = load_be32(rr + 32ull * t);
+    const fe s = load_be32(ss + 32ull * t);
+    const uint32_t kid = key[t];
+    const bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
+                       kid >= 1 && kid < nkeys;
+
+    // w = s^-1 (plain), then u1 = e w, u2 = r w (plain, canonical)
+    fe w;
+    {
+        fe sv = s;
+        if (!valid) {
+            sv = fe_zero();
+            sv.v[0] = 1;
+        }
+        // wave-uniform: the compiler runs it on the scalar unit (~37k cycles, tools/phase_timer.hip)
+        inv::inv_mod_n(w.v, sv.v, dtab);
+    }
+    fe e, wm, u1, u2;
+    fn_canon(e, e_raw);
+    fn_mul(wm, w, fe_const(C_R2N));  // w R
+    fn_mul(u1, e, wm);
+    fn_mul(u2, r, wm);
+    fn_canon(u1, u1);
+    fn_canon(u2, u2);
+
+    // this lane's table point
+    const u32 win = lane & 31u;
+    const u32 digit = byte_of(lane < 32 ? u1 : u2, win);
+    const uint4* tab = keytab[lane < 32 ? 0u : (valid ? kid : 0u)];
+    const uint4* ent = tab + (size_t)(win * COMB_ENTRIES + digit) * COMB_ENTRY_U4;
+    jp acc;
+    bool inf = digit == 0;
+    {
+        const uint4 a = ent[0], b = ent[1], c = ent[2], d = ent[3];
+        acc.x = {{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+        acc.y = {{c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w}};
+        acc.z = fe_const(C_ONEP);
+    }
+    // butterfly: after level k every lane holds the sum of its aligned group of 2^(k+1) points
+    // (the same representation on every lane of the group: the additions are cooperative)
+    coop_add_affine_pair(acc, inf, lane);
+#pragma unroll 1
+    for (int lvl = 1; lvl < 6; ++lvl) coop_add_jac_quad(acc, inf, lane, lvl);
+    if (lane == 0) ok[t] = (valid && !inf && x_matches_r(acc, r)) ? 1 : 0;
+}
+
+}  // namespace sbft
+
+extern "C" int sbft_launch_comb_build(const uint8_t* d_qx, const uint8_t* d_qy, void* d_table,
+                                      uint32_t* d_status, hipStream_t stream) {
+    const unsigned threads = 256, blocks = (COMB_WINDOWS * COMB_ENTRIES) / threads;
+    hipLaunchKernelGGL(sbft::p256_comb_build_kernel, dim3(blocks), dim3(threads), 0, stream, d_qx, d_qy,
+                       (uint4*)d_table, d_status);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" size_t sbft_comb_table_bytes(void) { return (size_t)COMB_KEY_U4 * 16; }
+
+extern "C" int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint8_t* d_blob, const uint64_t* d_off,
+                                             const uint32_t* d_len, const uint8_t* d_r, const uint8_t* d_s,
+                                             const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
+                                             uint8_t* d_ok, uint32_t n, hipStream_t stream) {
+    if (n == 0) return 0;
+    if (!d_digest && (!d_blob || !d_off || !d_len)) return -1;
+    hipLaunchKernelGGL(sbft::p256_verify_keyed_wave_kernel, dim3(n), dim3(64), 0, stream, d_digest, d_blob, d_off,
+                       d_len, d_r, d_s, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -2,6 +2,7 @@
 // verify and sign kernels are built from (exposed as sbft_gv_selftest_field). Tests compare
 // each op against Python big integers on edge values (0, 1, p-1, p, 2^256-1, ...), which
 // the end-to-end ECDSA vectors do not all reach.
+#include "p256_inv.hpp"
 #include "p256_point.hpp"
 #include "sbft_kernels.h"
 
@@ -10,6 +11,8 @@ namespace sbft {
 __global__ __launch_bounds__(256) void selftest_kernel(int op, const uint8_t* __restrict__ a,
                                                        const uint8_t* __restrict__ b,
                                                        uint8_t* __restrict__ out, uint32_t n) {
+    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    if (op == 10) inv::stage_divstep_table(dtab);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const fe x = load_be32(a + 32ull * i), y = load_be32(b + 32ull * i);
@@ -25,6 +28,7 @@ __global__ __launch_bounds__(256) void selftest_kernel(int op, const uint8_t* __
     case 7: fp_canon(r, x); break;            // x mod p for x < 2^256
     case 8: fn_canon(r, x); break;            // x mod n for x < 2^256
     case 9: fn_add(r, x, y); break;           // x+y mod n, inputs < n
+    case 10: inv::inv_mod_n(r.v, x.v, dtab); break; // x^-1 mod n (plain, safegcd), 0 < x < n
     default: break;
     }
     store_be32(out + 32ull * i, r);

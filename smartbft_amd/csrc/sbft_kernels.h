@@ -32,3 +32,18 @@ int sbft_launch_p256_sign(const uint8_t* d_d, const uint8_t* d_k, const uint8_t*
 int sbft_launch_selftest(int op, const uint8_t* d_a, const uint8_t* d_b, uint8_t* d_out, uint32_t n,
                          hipStream_t stream);
 }
+
+extern "C" {
+// Registered-key (comb table) path, p256_keyed.hip.
+size_t sbft_comb_table_bytes(void);
+// table[w][j] = j 2^(8w) Q for the key (qx, qy) (32-byte big-endian, device memory);
+// d_status[0] = 1 iff the key is valid.
+int sbft_launch_comb_build(const uint8_t* d_qx, const uint8_t* d_qy, void* d_table, uint32_t* d_status,
+                           hipStream_t stream);
+// Verify n tuples against registered keys: d_key[t] in [1, nkeys) indexes d_keytab (slot 0 = G).
+// Either d_digest (n x 32 B) or the messages (d_blob, d_off, d_len) hashed in the launch.
+int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint8_t* d_blob, const uint64_t* d_off,
+                                  const uint32_t* d_len, const uint8_t* d_r, const uint8_t* d_s,
+                                  const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
+                                  uint8_t* d_ok, uint32_t n, hipStream_t stream);
+}

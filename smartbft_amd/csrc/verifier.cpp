@@ -311,7 +311,12 @@ struct sbft_verifier {
     sbft_gv_ctx* ctx;
     std::atomic<uint64_t> vseq;
     std::shared_mutex keys_mu;
-    std::unordered_map<uint64_t, std::array<uint8_t, 64>> keys;  // x || y, big-endian
+    // consenter id -> x || y (big-endian) and its engine key id (comb tables, 0 = none)
+    struct KeyEnt {
+        std::array<uint8_t, 64> xy;
+        uint32_t kid = 0;
+    };
+    std::unordered_map<uint64_t, KeyEnt> keys;
     // Proposal.Digest memo (view.go:435,443,524 recompute it per proposal): exact-content key
     std::mutex memo_mu;
     struct Memo {
@@ -347,12 +352,39 @@ struct sbft_verifier {
         m.valid = true;
     }
 
-    bool key_of(uint64_t id, std::array<uint8_t, 64>& k) {
+    bool key_of(uint64_t id, std::array<uint8_t, 64>& k, uint32_t* kid = nullptr) {
         std::shared_lock<std::shared_mutex> g(keys_mu);
         auto it = keys.find(id);
         if (it == keys.end()) return false;
-        k = it->second;
+        k = it->second.xy;
+        if (kid) *kid = it->second.kid;
         return true;
+    }
+
+    // Verify n (message, r||s, registered key id) triples with one keyed launch
+    // (p256_keyed.hip: comb tables, no doublings; the messages are hashed in the launch).
+    int gpu_verify_keyed(const std::vector<const uint8_t*>& msgs, const std::vector<size_t>& lens,
+                         const std::vector<const uint8_t*>& sigs, const std::vector<uint32_t>& kids, uint8_t* ok) {
+        const size_t n = msgs.size();
+        if (!n) return 0;
+        if (!ctx) return SBFT_GV_ENODEV;
+        size_t total = 0;
+        for (size_t l : lens) total += l;
+        std::vector<uint8_t> blob(total ? total : 1);
+        std::vector<uint64_t> off(n);
+        std::vector<uint32_t> len(n);
+        std::vector<uint8_t> r(32 * n), s(32 * n);
+        size_t at = 0;
+        for (size_t i = 0; i < n; ++i) {
+            off[i] = at;
+            len[i] = (uint32_t)lens[i];
+            if (lens[i]) std::memcpy(&blob[at], msgs[i], lens[i]);
+            at += lens[i];
+            std::memcpy(&r[32 * i], sigs[i], 32);
+            std::memcpy(&s[32 * i], sigs[i] + 32, 32);
+        }
+        return sbft_gv_sha256_verify_p256_keyed(ctx, blob.data(), total, off.data(), len.data(), r.data(), s.data(),
+                                                kids.data(), n, ok);
     }
 
     // Verify n (message, r||s, key) triples with one fused launch. ok must hold n bytes.
@@ -386,8 +418,9 @@ struct sbft_verifier {
                         std::vector<std::string>* reasons) {
         char digest[65];
         digest_of(p, digest);
-        std::vector<const uint8_t*> msgs, sv, kv;
-        std::vector<size_t> lens, which;
+        std::vector<const uint8_t*> msgs, sv, kv, kmsgs, ksv;
+        std::vector<size_t> lens, which, klens, kwhich;
+        std::vector<uint32_t> kids;
         std::vector<std::array<uint8_t, 64>> keybuf(n);
         if (reasons) reasons->assign(n, std::string());
         for (size_t i = 0; i < n; ++i) {
@@ -403,7 +436,8 @@ struct sbft_verifier {
                 if (reasons) (*reasons)[i] = "signature message does not bind the proposal digest";
                 continue;
             }
-            if (!key_of(sigs[i].id, keybuf[i])) {
+            uint32_t kid = 0;
+            if (!key_of(sigs[i].id, keybuf[i], &kid)) {
                 status[i] = SBFT_V_EKEY;
                 if (reasons) (*reasons)[i] = "unknown consenter " + std::to_string(sigs[i].id);
                 continue;
@@ -413,20 +447,34 @@ struct sbft_verifier {
                 if (reasons) (*reasons)[i] = "signature value must be 64 bytes r||s";
                 continue;
             }
+            if (kid) {  // registered consenter key: comb-table launch
+                kmsgs.push_back(sigs[i].msg);
+                klens.push_back(sigs[i].msg_len);
+                ksv.push_back(sigs[i].value);
+                kids.push_back(kid);
+                kwhich.push_back(i);
+                continue;
+            }
             msgs.push_back(sigs[i].msg);
             lens.push_back(sigs[i].msg_len);
             sv.push_back(sigs[i].value);
             kv.push_back(keybuf[i].data());
             which.push_back(i);
         }
-        std::vector<uint8_t> ok(which.size());
-        const int rc = gpu_verify_messages(msgs, lens, sv, kv, ok.data());
+        std::vector<uint8_t> ok(which.size()), kok(kwhich.size());
+        int rc = gpu_verify_keyed(kmsgs, klens, ksv, kids, kok.data());
         if (rc) return rc;
-        for (size_t k = 0; k < which.size(); ++k)
-            if (!ok[k]) {
-                status[which[k]] = SBFT_V_EVERIFY;
-                if (reasons) (*reasons)[which[k]] = "invalid signature";
-            }
+        rc = gpu_verify_messages(msgs, lens, sv, kv, ok.data());
+        if (rc) return rc;
+        auto mark = [&](const std::vector<size_t>& w, const std::vector<uint8_t>& o) {
+            for (size_t k = 0; k < w.size(); ++k)
+                if (!o[k]) {
+                    status[w[k]] = SBFT_V_EVERIFY;
+                    if (reasons) (*reasons)[w[k]] = "invalid signature";
+                }
+        };
+        mark(kwhich, kok);
+        mark(which, ok);
         return 0;
     }
 };
@@ -469,8 +517,15 @@ void sbft_verifier_free(sbft_verifier* v) { delete v; }
 
 int sbft_verifier_add_consenter(sbft_verifier* v, uint64_t id, const uint8_t pubkey65[65]) {
     if (!v || !pubkey65 || pubkey65[0] != 0x04) return SBFT_GV_EINVAL;
-    std::array<uint8_t, 64> k;
-    std::memcpy(k.data(), pubkey65 + 1, 64);
+    sbft_verifier::KeyEnt k;
+    std::memcpy(k.xy.data(), pubkey65 + 1, 64);
+    if (v->ctx) {
+        // precompute the key's comb tables on every device; an invalid point keeps kid = 0
+        // (its signatures then take the generic path, which rejects them like Go does)
+        const int rc = sbft_gv_register_key(v->ctx, pubkey65 + 1, pubkey65 + 33, &k.kid);
+        if (rc && rc != SBFT_GV_EINVAL) return rc;
+        if (rc) k.kid = 0;
+    }
     std::unique_lock<std::shared_mutex> g(v->keys_mu);
     v->keys[id] = k;
     return 0;
@@ -609,7 +664,8 @@ int sbft_verifier_verify_consenter_sigs(sbft_verifier* v, const sbft_signature* 
 int sbft_verifier_verify_signature(sbft_verifier* v, const sbft_signature* s, char* err, size_t err_cap) {
     if (!v || !s) return SBFT_GV_EINVAL;
     std::array<uint8_t, 64> key;
-    if (!v->key_of(s->id, key)) {
+    uint32_t kid = 0;
+    if (!v->key_of(s->id, key, &kid)) {
         put_err(err, err_cap, "unknown signer %llu", (unsigned long long)s->id);
         return SBFT_V_EKEY;
     }
@@ -620,7 +676,8 @@ int sbft_verifier_verify_signature(sbft_verifier* v, const sbft_signature* s, ch
     std::vector<const uint8_t*> msgs{s->msg ? s->msg : (const uint8_t*)""}, sigs{s->value}, keys{key.data()};
     std::vector<size_t> lens{s->msg_len};
     uint8_t ok = 0;
-    const int rc = v->gpu_verify_messages(msgs, lens, sigs, keys, &ok);
+    const int rc = kid ? v->gpu_verify_keyed(msgs, lens, sigs, {kid}, &ok)
+                       : v->gpu_verify_messages(msgs, lens, sigs, keys, &ok);
     if (rc) {
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
         return rc;

@@ -20,6 +20,7 @@ EXPORTS = [
     "sbft_gv_verify_p256_dev", "sbft_gv_sha256_dev", "sbft_gv_sha256_verify_p256_dev",
     "sbft_gv_normalize_hash", "sbft_gv_normalize_scalar", "sbft_gv_sign_p256", "sbft_gv_sign_p256_dev",
     "sbft_gv_selftest_field", "sbft_gv_verify_workspace_bytes",
+    "sbft_gv_register_key", "sbft_gv_verify_p256_keyed", "sbft_gv_sha256_verify_p256_keyed",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -72,6 +73,12 @@ def load_library():
     L.sbft_gv_normalize_hash.argtypes = [_u8p, ctypes.c_size_t, _u8p]
     L.sbft_gv_normalize_hash.restype = None
     L.sbft_gv_normalize_scalar.argtypes = [_u8p, ctypes.c_size_t, _u8p]
+    _u32p = ctypes.POINTER(ctypes.c_uint32)
+    L.sbft_gv_register_key.argtypes = [_vp, _u8p, _u8p, _u32p]
+    L.sbft_gv_verify_p256_keyed.argtypes = [_vp] + [_u8p] * 3 + [_u32p, ctypes.c_size_t, _u8p]
+    L.sbft_gv_sha256_verify_p256_keyed.argtypes = [_vp, _u8p, ctypes.c_size_t,
+                                                   ctypes.POINTER(ctypes.c_uint64), _u32p, _u8p, _u8p,
+                                                   _u32p, ctypes.c_size_t, _u8p]
     _LIB = L
     return L
 
@@ -140,6 +147,40 @@ class GpuVerifier:
         ok = np.zeros(n, dtype=np.uint8)
         self._check(self.L.sbft_gv_verify_p256(self.ctx, *[_p(a) for a in arrs], n, _p(ok)),
                     "sbft_gv_verify_p256")
+        return ok
+
+    def register_key(self, qx: bytes, qy: bytes) -> int:
+        """Precompute the comb tables of a (consenter) key; returns its key id (>= 1). Raises
+        GpuVerifyError for a key that is not a valid P-256 point."""
+        kx = (ctypes.c_uint8 * 32).from_buffer_copy(bytes(qx))
+        ky = (ctypes.c_uint8 * 32).from_buffer_copy(bytes(qy))
+        kid = ctypes.c_uint32()
+        self._check(self.L.sbft_gv_register_key(self.ctx, kx, ky, ctypes.byref(kid)), "sbft_gv_register_key")
+        return kid.value
+
+    def verify_keyed(self, digest, r, s, key_ids) -> np.ndarray:
+        n = len(digest)
+        arrs = [_soa(a, n) for a in (digest, r, s)]
+        kid = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        ok = np.zeros(n, dtype=np.uint8)
+        self._check(self.L.sbft_gv_verify_p256_keyed(
+            self.ctx, *[_p(a) for a in arrs], kid.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n, _p(ok)),
+            "sbft_gv_verify_p256_keyed")
+        return ok
+
+    def sha256_verify_keyed(self, blob, off, ln, r, s, key_ids) -> np.ndarray:
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(ln, dtype=np.uint32)
+        n = off.shape[0]
+        arrs = [_soa(a, n) for a in (r, s)]
+        kid = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        ok = np.zeros(n, dtype=np.uint8)
+        self._check(self.L.sbft_gv_sha256_verify_p256_keyed(
+            self.ctx, _p(blob) if blob.size else None, blob.size,
+            off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), ln.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+            *[_p(a) for a in arrs], kid.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n, _p(ok)),
+            "sbft_gv_sha256_verify_p256_keyed")
         return ok
 
     def sign(self, d, k, digest):

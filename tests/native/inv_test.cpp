@@ -1,0 +1,27 @@
+// CPU build of smartbft_amd/csrc/p256_inv.hpp (the device inversion) for tests/test_native.py:
+// reads hex x per line on stdin, prints hex x^-1 mod n.
+#include <cstdio>
+#include <cstring>
+
+#include "../../smartbft_amd/csrc/p256_inv.hpp"
+
+static const uint32_t TAB[SBFT_DIVSTEP5_WORDS] = SBFT_DIVSTEP5_TABLE;
+
+int main() {
+    char line[256];
+    while (fgets(line, sizeof line, stdin)) {
+        uint32_t x[8] = {0}, out[8];
+        size_t L = strcspn(line, "\r\n");
+        line[L] = 0;
+        // big-endian hex, 64 digits
+        for (int w = 0; w < 8; ++w) {
+            unsigned v = 0;
+            sscanf(line + 8 * (7 - w), "%8x", &v);
+            x[w] = v;
+        }
+        sbft::inv::inv_mod_n(out, x, TAB);
+        for (int w = 7; w >= 0; --w) printf("%08x", out[w]);
+        printf("\n");
+    }
+    return 0;
+}
