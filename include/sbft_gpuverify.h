@@ -89,9 +89,10 @@ size_t sbft_gv_verify_workspace_bytes(size_t n);
 int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, const void* d_r,
                             const void* d_s, const void* d_qx, const void* d_qy, size_t n,
                             void* d_ok, void* stream);
-/* d_order (may be NULL): u32 permutation of [0, n) — lane t hashes message d_order[t]. Pass the
- * messages sorted by length so a wavefront's lanes finish together (the host-buffer calls
- * sort internally). Digests land at their message's index either way. */
+/* d_order (may be NULL): u32 permutation of [0, n): the messages are taken in that sequence.
+ * NULL (index order) is the fast choice: the kernel load-balances messages of any lengths over
+ * its lanes and index order keeps each wavefront's streams adjacent in memory. Digests land at
+ * their message's index either way. */
 int sbft_gv_sha256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob, const void* d_off,
                        const void* d_len, const void* d_order, size_t n, void* d_dig, void* stream);
 int sbft_gv_sha256_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob,

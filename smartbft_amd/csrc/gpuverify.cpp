@@ -94,6 +94,7 @@ struct Slot {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+
 }  // namespace
 
 struct sbft_gv_ctx {
@@ -230,10 +231,14 @@ int sbft_gv_sha256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob, const v
                        const void* d_len, const void* d_order, size_t n, void* d_dig, void* stream) {
     if (!ctx || (n && (!d_blob || !d_off || !d_len || !d_dig))) return SBFT_GV_EINVAL;
     if (n > 0xffffffffu) return SBFT_GV_EINVAL;
-    if (!slot_for(ctx, device)) return SBFT_GV_ENODEV;
+    Slot* sl = slot_for(ctx, device);
+    if (!sl) return SBFT_GV_ENODEV;
+    if (n == 0) return SBFT_GV_OK;
     if (hipSetDevice(device) != hipSuccess) return SBFT_GV_EDEVICE;
+    uint32_t* ctr = sl->stream_workspace((hipStream_t)stream, 256);  // the stream's work counter
+    if (!ctr) return SBFT_GV_ENOMEM;
     return sbft_launch_sha256((const uint8_t*)d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len,
-                              (const uint32_t*)d_order, (uint8_t*)d_dig, (uint32_t)n, (hipStream_t)stream)
+                              (const uint32_t*)d_order, (uint8_t*)d_dig, (uint32_t)n, ctr, (hipStream_t)stream)
                ? SBFT_GV_ELAUNCH
                : SBFT_GV_OK;
 }
@@ -333,31 +338,25 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
     if (c.count == 0) return SBFT_GV_OK;
     rebased.resize(c.count);
     for (size_t k = 0; k < c.count; ++k) rebased[k] = off[c.begin + k] - lo;
-    // lanes take messages in length order (descending) so each wavefront's lanes finish together
-    std::vector<uint32_t> order(c.count);
-    for (size_t k = 0; k < c.count; ++k) order[k] = (uint32_t)k;
-    std::stable_sort(order.begin(), order.end(),
-                     [&](uint32_t a, uint32_t b) { return len[c.begin + a] > len[c.begin + b]; });
     const size_t span = hi - lo;
     const size_t fb = align_up(span + 128, 256);  // funnel over-read padding
     const size_t fo = align_up(8 * c.count, 256), fl = align_up(4 * c.count, 256);
     const size_t fd = align_up(32 * c.count, 256);
     const bool verify = ok_out != nullptr;
-    const size_t need = fb + fo + 2 * fl + fd +
+    // blob | off | len | work counter | digests [| r | s | qx | qy | ok | verify workspace]
+    const size_t need = fb + fo + fl + 256 + fd +
                         (verify ? 4 * fd + align_up(c.count, 256) + sbft_verify_work_bytes(c.count) : 0);
     HIPCHK(hipSetDevice(sl->device));
     int rc = sl->reserve(need);
     if (rc) return rc;
     uint8_t* b = sl->dbuf;
-    uint8_t *d_blob = b, *d_off = b + fb, *d_len = d_off + fo, *d_order = d_len + fl, *d_dig = d_order + fl;
+    uint8_t *d_blob = b, *d_off = b + fb, *d_len = d_off + fo, *d_ctr = d_len + fl, *d_dig = d_ctr + 256;
     HIPCHK(hipMemcpyAsync(d_blob, blob + lo, span, hipMemcpyHostToDevice, sl->stream));
     HIPCHK(hipMemcpyAsync(d_off, rebased.data(), 8 * c.count, hipMemcpyHostToDevice, sl->stream));
     HIPCHK(hipMemcpyAsync(d_len, len + c.begin, 4 * c.count, hipMemcpyHostToDevice, sl->stream));
-    HIPCHK(hipMemcpyAsync(d_order, order.data(), 4 * c.count, hipMemcpyHostToDevice, sl->stream));
-    // pageable-source copies are staged before hipMemcpyAsync returns, so `order` may go out
-    // of scope; `rebased` is owned by the caller until the stream is synchronised anyway.
-    if (sbft_launch_sha256(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len,
-                           (const uint32_t*)d_order, d_dig, (uint32_t)c.count, sl->stream))
+    // `rebased` is owned by the caller until the stream is synchronised
+    if (sbft_launch_sha256(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len, nullptr, d_dig,
+                           (uint32_t)c.count, (uint32_t*)d_ctr, sl->stream))
         return SBFT_GV_ELAUNCH;
     if (verify) {
         uint8_t* v = d_dig + fd;

@@ -21,9 +21,11 @@ int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const u
                             uint32_t* d_work, hipStream_t stream);
 // SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable >= 68 bytes
 // past its last message (funnel over-read). Digests are 32-byte big-endian. d_order (may be
-// NULL): lane t hashes message d_order[t] — pass the messages sorted by length.
+// NULL): the messages are taken in the order d_order[0], d_order[1], ... (load-balanced;
+// NULL = index order, which keeps each wavefront's streams adjacent in memory). d_ctr: one
+// device u32 of scratch private to the stream (zeroed by the launch).
 int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
-                       const uint32_t* d_order, uint8_t* d_dig, uint32_t n, hipStream_t stream);
+                       const uint32_t* d_order, uint8_t* d_dig, uint32_t n, uint32_t* d_ctr, hipStream_t stream);
 // Key derivation + ECDSA sign with caller nonces: Q = d*G, (r, s); status 1 = ok.
 int sbft_launch_p256_sign(const uint8_t* d_d, const uint8_t* d_k, const uint8_t* d_e, uint8_t* d_qx,
                           uint8_t* d_qy, uint8_t* d_r, uint8_t* d_s, uint8_t* d_status, uint32_t n,

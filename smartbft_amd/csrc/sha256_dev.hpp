@@ -20,6 +20,10 @@ __device__ __constant__ static const uint32_t K256[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+// x ^ y ^ z in one v_bitop3_b32 (truth table 0x96); the compiler emits two v_xor_b32 otherwise
+__device__ __forceinline__ uint32_t xor3(uint32_t x, uint32_t y, uint32_t z) {
+    return __builtin_amdgcn_bitop3_b32(x, y, z, 0x96);
+}
 
 __device__ __forceinline__ void compress(uint32_t h[8], uint32_t w[16]) {
     uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
@@ -30,16 +34,16 @@ __device__ __forceinline__ void compress(uint32_t h[8], uint32_t w[16]) {
             wi = w[i];
         } else {
             const uint32_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-            const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-            const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
             wi = w[i & 15] + s0 + w[(i + 9) & 15] + s1;
             w[i & 15] = wi;
         }
-        const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
-        const uint32_t ch = (e & f) ^ (~e & g);
+        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+        const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);  // (e & f) | (~e & g)
         const uint32_t t1 = hh + S1 + ch + K256[i] + wi;
-        const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
-        const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
+        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+        const uint32_t maj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);  // majority
         const uint32_t t2 = S0 + maj;
         hh = g;
         g = f;
@@ -62,8 +66,9 @@ __device__ __forceinline__ void compress(uint32_t h[8], uint32_t w[16]) {
 
 // Message words of the block starting at byte address p (any alignment), big-endian.
 __device__ __forceinline__ void load_block(const uint8_t* p, uint32_t w[16]) {
+    typedef const __attribute__((address_space(1))) uint32_t gu32;  // global, not flat, loads
     const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
-    const uint32_t* base = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+    gu32* base = (gu32*)(addr & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(addr & 3);
     uint32_t raw[17];
 #pragma unroll
@@ -119,6 +124,40 @@ __device__ __forceinline__ void sha256_one(const uint8_t* msg, uint32_t len, uin
         w[14] = (uint32_t)(bits >> 32);
         w[15] = (uint32_t)bits;
         compress(h, w);
+    }
+}
+
+// Block b (0-based) of the FIPS 180-4 padded message (msg, len): data blocks, then the tail
+// block(s) with 0x80, zeros and the 64-bit bit length. The tail masking runs under a
+// wave-uniform branch, so lanes of one wavefront may sit at different blocks of different
+// messages (sha256_stream_kernel) without diverging.
+__device__ __forceinline__ uint32_t sha256_nblocks(uint32_t len) { return (len >> 6) + ((len & 63) < 56 ? 1 : 2); }
+__device__ __forceinline__ void sha256_block_at(const uint8_t* msg, uint32_t len, uint32_t b, uint32_t w[16]) {
+    const uint32_t full = len >> 6;
+    const bool tail = b >= full;
+    load_block(msg + 64ull * (tail ? full : b), w);  // the blob is padded past its last message
+    if (__builtin_expect(__any(tail), 0)) {
+        if (tail) {
+            const uint32_t rem = len & 63;
+            const bool first = b == full;
+            const uint32_t krem = first ? rem : 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t b0 = 4 * i;
+                uint32_t keep_mask;
+                if (b0 + 4 <= krem) keep_mask = 0xffffffffu;
+                else if (b0 >= krem) keep_mask = 0;
+                else keep_mask = 0xffffffffu << (8 * (4 - (krem - b0)));
+                uint32_t v = w[i] & keep_mask;
+                if (first && rem >= b0 && rem < b0 + 4) v |= 0x80u << (8 * (3 - (rem - b0)));
+                w[i] = v;
+            }
+            if (b + 1 == sha256_nblocks(len)) {
+                const uint64_t bits = (uint64_t)len * 8;
+                w[14] = (uint32_t)(bits >> 32);
+                w[15] = (uint32_t)bits;
+            }
+        }
     }
 }
 
