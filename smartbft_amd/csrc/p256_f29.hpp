@@ -1,0 +1,317 @@
+// p256_f29.hpp — P-256 field arithmetic in radix 2^29 (9 signed limbs) for the verify hot loop.
+//
+// Why a second representation. With 8 x 32-bit limbs every v_mad_u64_u32 of a product column
+// can carry out of its 64-bit accumulator, so each product costs a second instruction (v_addc)
+// to catch the carry, and additions need 8-long carry chains plus a conditional subtraction
+// of p. With 29-bit limbs a column of up to 9 products (each < 2^58) plus carries stays far
+// below 2^63: every product is ONE v_mad_i64_i32 with no carry handling, and additions and
+// subtractions are 9 independent v_add/v_sub (no carries, no reduction) because the limbs are
+// signed and carry headroom is left in each 32-bit word.
+//
+// Value:  x = sum_i v[i] * 2^(29 i), v[i] signed 32-bit. Montgomery form mod p with R = 2^261.
+// Normal form (every f29_mul / f29_sqr output): v[0..7] in [0, 2^29), v[8] signed, and
+// |x| < 2^258 (see the bound in f29_mul).
+//
+// Reduction. p = 2^256 - 2^224 + 2^192 + 2^96 - 1 in radix 2^29 with non-negative digits above
+// digit 0:  p = -1 + 2^9 * B^3 + 2^18 * B^6 + (2^29 - 2^21) * B^7 + (2^24 - 1) * B^8, B = 2^29.
+// -p^-1 = 1 (mod 2^29), so the Montgomery multiplier of a column is its own low 29 bits m, and
+// m*p adds four single-mad terms to columns k+3, k+6, k+7, k+8 (the -m at column k just
+// clears the low bits that the arithmetic shift drops anyway).
+//
+// Caller contract (checked by the bound comments at each use in p256_verify.hip): for
+// f29_mul(a, b) with |a.v[i]| <= A and |b.v[i]| <= B, 9*A*B + 2^60 < 2^63 (A*B <= 2^59.7:
+// e.g. 2^29 x 2^30.6), and |a| * |b| < 2^517 so that the output is normal.
+#pragma once
+#include "p256_field.hpp"
+#include "p256_tables.inc"
+
+namespace sbft {
+
+typedef int32_t i32;
+typedef int64_t i64;
+
+struct f29 {
+    u32 v[9];
+};
+
+#define F29_MASK 0x1FFFFFFFu
+
+// acc + a*b (signed 32 x 32 + 64), one v_mad_i64_i32. Written as asm: the compiler lowers the C
+// expression through v_mad_u64_u32 plus sign fix-ups.
+SBFT_DEV i64 smad(u32 a, u32 b, i64 acc) {
+    i64 r;
+    u64 cc;
+    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "v"(b), "v"(acc));
+    return r;
+}
+
+// Montgomery product a*b*2^-261 mod p (normal form out, see the contract above).
+SBFT_DEV void f29_mul(f29& r, const f29& a, const f29& b) {
+    u32 m[9];
+    i64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const int j = k - i;
+            if (j < 0 || j > 8) continue;
+            acc = smad(a.v[i], b.v[j], acc);
+        }
+        if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], 1u << 9, acc);
+        if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], 1u << 18, acc);
+        if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], 0x1FE00000u, acc);
+        if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], 0x00FFFFFFu, acc);
+        if (k < 9) m[k] = (u32)acc & F29_MASK;
+        else r.v[k - 9] = (u32)acc & F29_MASK;
+        acc >>= 29;
+    }
+    r.v[8] = (u32)acc;
+}
+
+// a^2: off-diagonal products against the doubled operand (one mad each), then the squares.
+SBFT_DEV void f29_sqr(f29& r, const f29& a) {
+    u32 d[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
+    u32 m[9];
+    i64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const int j = k - i;
+            if (j <= i || j > 8) continue;
+            acc = smad(a.v[i], d[j], acc);
+        }
+        if ((k & 1) == 0) acc = smad(a.v[k >> 1], a.v[k >> 1], acc);
+        if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], 1u << 9, acc);
+        if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], 1u << 18, acc);
+        if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], 0x1FE00000u, acc);
+        if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], 0x00FFFFFFu, acc);
+        if (k < 9) m[k] = (u32)acc & F29_MASK;
+        else r.v[k - 9] = (u32)acc & F29_MASK;
+        acc >>= 29;
+    }
+    r.v[8] = (u32)acc;
+}
+
+SBFT_DEV void f29_add(f29& r, const f29& a, const f29& b) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + b.v[i];
+}
+SBFT_DEV void f29_sub(f29& r, const f29& a, const f29& b) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] - b.v[i];
+}
+SBFT_DEV void f29_neg(f29& r, const f29& a) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = 0u - a.v[i];
+}
+// r = c * a for a small constant c (limbs grow by c)
+SBFT_DEV void f29_muls(f29& r, const f29& a, u32 c) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] * c;
+}
+// Value-reducing normalisation for a sum like 3u - 4v (|limb| < 2^31, |x| < 2^260) -> N:
+//  1. one parallel carry pass: limbs 0..7 into [-4, 2^29 + 4) (limb 8 takes limb 7's carry);
+//  2. fold: h = limb8 >> 24 are the bits at 2^256 and up; drop them and add
+//     h * (2^256 mod p) = h * (2^224 - 2^192 - 2^96 + 1), i.e. +h<<21 at limb 7, -h<<18 at
+//     limb 6, -h<<9 at limb 3, +h at limb 0 (|h| <= 2^5 here, so the limbs move by < 2^26).
+// Out: limbs 0..7 in (-2^26, 2^29 + 2^26), limb 8 in [0, 2^24), |x| < 2^257.
+SBFT_DEV void f29_normalize(f29& r, const f29& a) {
+    u32 c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = (u32)((i32)a.v[i] >> 29);
+    f29 t;
+    t.v[0] = a.v[0] & F29_MASK;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) t.v[i] = (a.v[i] & F29_MASK) + c[i - 1];
+    const u32 top = a.v[8] + c[7];
+    const i32 h = (i32)top >> 24;
+    t.v[8] = top & 0x00FFFFFFu;
+    t.v[7] += (u32)h << 21;
+    t.v[6] = (u32)((i32)t.v[6] + h * -(1 << 18));
+    t.v[3] = (u32)((i32)t.v[3] + h * -(1 << 9));
+    t.v[0] += (u32)h;
+    r = t;
+}
+
+// ---------------------------------------------------------------- points
+struct jp29 {
+    f29 x, y, z;
+};
+
+__device__ __constant__ static const u32 C29_R2[9] = P256_F29_R2;
+__device__ __constant__ static const u32 C29_ONE[9] = P256_F29_ONE;
+__device__ __constant__ static const u32 C29_2P[9] = P256_F29_2P;
+__device__ __constant__ static const u32 C29_G2X[9] = P256_F29_G2X;
+__device__ __constant__ static const u32 C29_G2Y[9] = P256_F29_G2Y;
+__device__ __constant__ static const u32 C29_GODD8[P256_GODD8_F29_WORDS] = P256_GODD8_F29_DATA;
+
+SBFT_DEV f29 f29_const(const u32* c) {
+    f29 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = c[i];
+    return r;
+}
+
+// Limb-bound bookkeeping below: N = f29_mul/f29_sqr output (limbs 0..7 in [0, 2^29)) or
+// f29_normalize output (limbs 0..7 in (-2^26, 2^29 + 2^26)); N+- = difference of two mul
+// outputs (|limb| < 2^29). Every product states its A x B limb bound (<= 2^59.83 allowed).
+
+// Doubling, a = -3, in the form
+//   d = Z^2, g = Y^2, b2 = 2XY^2, a' = (X - d)(X + d), u = 3a'^2
+//   X3 = 3u - 4 b2 (= 9a'^2 - 8XY^2), Y3 = 3a'(2 b2 - X3) - 4 * 2g^2, Z3 = 2Y Z
+// 6M + 2S, every intermediate inside the signed 32-bit limbs. In: X in N, Y in N or N+-,
+// Z in N. Out: N (X3, Y3 normalised; Z3 a mul output).
+// Z = 0 maps to Z3 = 0 (the caller's exceptional-case detector relies on it).
+SBFT_DEV void p29_dbl(jp29& r, const jp29& p) {
+    f29 d, g, b2, t0, t1, a1, a3, u, m;
+    f29_sqr(d, p.z);                 // 2^29.2^2
+    f29_sqr(g, p.y);
+    f29_add(t0, g, g);               // 2g < 2^30
+    f29_mul(b2, p.x, t0);            // 2^29.2 x 2^30
+    f29_sub(t1, p.x, d);             // (-2^29, 2^29.2)
+    f29_add(a1, p.x, d);             // < 2^30.1
+    f29_mul(a1, t1, a1);             // a'  (2^29.2 x 2^30.1)
+    f29_add(t1, p.y, p.y);           // 2Y < 2^30.2
+    f29_mul(r.z, t1, p.z);           // Z3 = 2YZ (2^30.2 x 2^29.2)
+    f29_muls(a3, a1, 3);             // 3a' < 2^30.6
+    f29_mul(u, a1, a3);              // u = 3a'^2 (2^29 x 2^30.6)
+    f29_mul(g, g, t0);               // 2g^2 (2^29 x 2^30)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t1.v[i] = 3 * u.v[i] - (b2.v[i] << 2);  // (-2^31, 2^30.6)
+    f29_normalize(r.x, t1);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t0.v[i] = (b2.v[i] << 1) - r.x.v[i];  // (-2^29.2, 2^30)
+    f29_mul(m, a1, t0);              // a'(2 b2 - X3) (2^29 x 2^30)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t1.v[i] = 3 * m.v[i] - (g.v[i] << 2);  // (-2^31, 2^30.6)
+    f29_normalize(r.y, t1);
+}
+
+// acc += b (b Jacobian, N; b.y may be N+-) with no case analysis (12M + 4S). If H == 0
+// (acc == +-b) the result has Z3 = 0, which every later doubling and addition keeps at 0:
+// the caller checks Z once at the end and re-verifies such tuples on the general path.
+SBFT_DEV void p29_add_jac_lean(jp29& acc, const jp29& b) {
+    f29 z1z1, z2z2, u1, u2, s1, s2, t, h, rr, hh, hhh;
+    f29_sqr(z1z1, acc.z);
+    f29_mul(u2, b.x, z1z1);
+    f29_mul(t, acc.z, z1z1);
+    f29_mul(s2, b.y, t);
+    f29_sqr(z2z2, b.z);
+    f29_mul(u1, acc.x, z2z2);
+    f29_mul(t, b.z, z2z2);
+    f29_mul(s1, acc.y, t);
+    f29_sub(h, u2, u1);              // N+-
+    f29_sub(rr, s2, s1);             // N+-
+    f29_sqr(hh, h);
+    f29_mul(hhh, hh, h);
+    f29_mul(u1, u1, hh);             // V = U1 H^2
+    f29_mul(t, acc.z, b.z);
+    f29_mul(acc.z, t, h);
+    f29_sqr(t, rr);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] = t.v[i] - hhh.v[i] - (u1.v[i] << 1);  // (-3 2^29, 2^29)
+    f29_normalize(acc.x, t);
+    f29_sub(t, u1, acc.x);           // (-2^29.2, 2^29 + 2^26)
+    f29_mul(t, rr, t);
+    f29_mul(s1, s1, hhh);
+    f29_sub(acc.y, t, s1);           // N+-
+}
+
+// acc += (x2, y2) affine (N; y2 may be N+-), same structure: 8M + 3S.
+SBFT_DEV void p29_add_aff_lean(jp29& acc, const f29& x2, const f29& y2) {
+    f29 z1z1, u2, s2, h, rr, hh, hhh, t;
+    f29_sqr(z1z1, acc.z);
+    f29_mul(u2, x2, z1z1);
+    f29_mul(s2, acc.z, z1z1);
+    f29_mul(s2, y2, s2);
+    f29_sub(h, u2, acc.x);           // (-2^29.2, 2^29 + 2^4)
+    f29_sub(rr, s2, acc.y);          // (-2^29.2, 2^29.2)
+    f29_sqr(hh, h);
+    f29_mul(hhh, hh, h);
+    f29_mul(u2, acc.x, hh);          // V = X1 H^2
+    f29_mul(acc.z, acc.z, h);
+    f29_sqr(t, rr);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] = t.v[i] - hhh.v[i] - (u2.v[i] << 1);
+    f29_normalize(acc.x, t);
+    f29_sub(t, u2, acc.x);
+    f29_mul(t, rr, t);
+    f29_mul(s2, acc.y, hhh);
+    f29_sub(acc.y, t, s2);           // N+-
+}
+
+// ---------------------------------------------------------------- conversions
+// 8 x 32-bit limbs (a value < 2^256) -> 9 x 29-bit limbs (plain integer, not Montgomery).
+SBFT_DEV f29 f29_from_u256(const fe& a) {
+    f29 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
+        const u32 lo = a.v[w];
+        const u32 hi = (w + 1 < 8) ? a.v[w + 1] : 0u;
+        r.v[i] = __builtin_amdgcn_alignbit(hi, lo, s) & F29_MASK;
+    }
+    return r;
+}
+// Full normalisation to [0, 2^261) limbs-in-range form via a carry chain; |x| < 2^260 in,
+// value x mod 2^261 out (callers add a multiple of p first when x may be negative).
+SBFT_DEV void f29_norm_chain(f29& r, const f29& a) {
+    i32 c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const i32 t = (i32)a.v[i] + c;
+        r.v[i] = (u32)t & F29_MASK;
+        c = t >> 29;
+    }
+    r.v[8] = a.v[8] + (u32)c;
+}
+// limbs in range (after f29_norm_chain, value in [0, 2^256+...)) -> 8 x 32-bit limbs (low 256 bits)
+SBFT_DEV fe f29_to_u256(const f29& a) {
+    fe r;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const int bit = 32 * w, i = bit / 29, s = bit % 29;
+        u64 x = (u64)a.v[i] >> s;
+        x |= (u64)a.v[i + 1] << (29 - s);
+        if (i + 2 < 9) x |= (u64)a.v[i + 2] << (58 - s);
+        r.v[w] = (u32)x;
+    }
+    return r;
+}
+
+// Canonical plain value of a Montgomery f29 element: a * 2^-261 mod p in [0, p), as 8 x 32
+// limbs. Once per verify (final comparison), so written for clarity, not speed.
+SBFT_DEV fe f29_canon_plain(const f29& a) {
+    f29 one;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) one.v[i] = i == 0 ? 1u : 0u;
+    f29 t;
+    f29_mul(t, a, one);              // plain value, |t| < 2^256 + 2^1
+    f29 p2 = f29_const(C29_2P);
+    f29_add(t, t, p2);               // positive: (0, 2^258)
+    f29_norm_chain(t, t);            // limbs 0..7 in [0, 2^29), limb 8 in [0, 2^26)
+    // 8 low words + bits 256.. (top < 4), then subtract p while the value is >= p
+    fe lo = f29_to_u256(t);
+    u32 top = t.v[8] >> 24;
+#pragma unroll 1
+    for (int it = 0; it < 4; ++it) {
+        fe d;
+        u64 bw = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const u64 x = (u64)lo.v[k] - P256_P[k] - bw;
+            d.v[k] = lo32(x);
+            bw = x >> 63;
+        }
+        if (top >= (u32)bw) {  // value - p >= 0
+            top -= (u32)bw;
+            lo = d;
+        }
+    }
+    return lo;
+}
+
+}  // namespace sbft

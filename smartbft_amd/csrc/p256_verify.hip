@@ -16,6 +16,7 @@
 // Inputs: SoA, 32-byte big-endian fields. Output: one verdict byte per tuple.
 #include <cstdio>
 
+#include "p256_f29.hpp"
 #include "p256_point.hpp"
 #include "sbft_kernels.h"
 
@@ -334,8 +335,8 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
                                                           const uint8_t* __restrict__ qyy,
                                                           uint8_t* __restrict__ ok, uint32_t n,
                                                           uint32_t* __restrict__ work, sinv_ws ws) {
-    __shared__ u32 gtab[GODD8_WORDS];
-    for (int i = threadIdx.x; i < GODD8_WORDS; i += blockDim.x) gtab[i] = C_GODD8[i];
+    __shared__ u32 gtab[P256_GODD8_F29_WORDS];
+    for (int i = threadIdx.x; i < P256_GODD8_F29_WORDS; i += blockDim.x) gtab[i] = C29_GODD8[i];
     __syncthreads();
     const int tid = threadIdx.x;
 
@@ -353,19 +354,17 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
                  fe_lt(qx, P256_P) && fe_lt(qy, P256_P);
 
-    // Q to Montgomery form and on-curve check y^2 == x^3 - 3x + b
-    const fe r2p = fe_const(C_R2P);
-    jp q;
-    fp_mul(q.x, qx, r2p);
-    fp_mul(q.y, qy, r2p);
-    q.z = fe_const(C_ONEP);
+    // on-curve check y^2 == x^3 - 3x + b (8 x 32 Montgomery domain, once per verify)
     {
-        fe lhs, rhs, t;
-        fp_sqr(lhs, q.y);
-        fp_sqr(rhs, q.x);
-        fp_mul(rhs, rhs, q.x);
-        fp_add(t, q.x, q.x);
-        fp_add(t, t, q.x);
+        const fe r2p = fe_const(C_R2P);
+        fe x, y, lhs, rhs, t;
+        fp_mul(x, qx, r2p);
+        fp_mul(y, qy, r2p);
+        fp_sqr(lhs, y);
+        fp_sqr(rhs, x);
+        fp_mul(rhs, rhs, x);
+        fp_add(t, x, x);
+        fp_add(t, t, x);
         fp_sub(rhs, rhs, t);
         fp_add(rhs, rhs, fe_const(C_BM));
         fp_canon(lhs, lhs);
@@ -373,24 +372,27 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
         valid = valid && fe_eq(lhs, rhs);
     }
 
-    // Invalid lanes run a harmless stand-in (Q = 2G, s = 1, u1 = u2 = 1) so they never take the
-    // exceptional path; their verdict is masked by `valid` at the end.
-    if (!valid) {
-        q.x = fe_const(C_G2X);
-        q.y = fe_const(C_G2Y);
-    }
-
-    // 2. odd multiples [1,3,...,15]Q in Jacobian form (scratch)
-    jp tq[8];
-    tq[0] = q;
+    // Q in the radix-2^29 Montgomery domain of the ladder (p256_f29.hpp). Invalid lanes run a
+    // harmless stand-in (Q = 2G, u1 = u2 = 1); their verdict is masked by `valid` at the end.
+    jp29 tq[8];  // odd multiples [1,3,...,15]Q, Jacobian (scratch)
     {
-        jp q2;
-        pt_dbl(q2, q);
-        bool texc = false;  // (2k+1)Q == +-2Q is impossible for a point of prime order n
+        jp29 q;
+        const f29 r2 = f29_const(C29_R2);
+        f29_mul(q.x, f29_from_u256(qx), r2);
+        f29_mul(q.y, f29_from_u256(qy), r2);
+        q.z = f29_const(C29_ONE);
+        if (!valid) {
+            q.x = f29_const(C29_G2X);
+            q.y = f29_const(C29_G2Y);
+        }
+        tq[0] = q;
+        jp29 q2;
+        p29_dbl(q2, q);
+        // (2k+1)Q == +-2Q is impossible for a point of prime order n: no exceptional case here
 #pragma unroll 1
         for (int k = 1; k < 8; ++k) {
-            jp t = tq[k - 1];
-            pt_add_jac_lean(t, texc, q2);
+            jp29 t = tq[k - 1];
+            p29_add_jac_lean(t, q2);
             tq[k] = t;
         }
     }
@@ -437,26 +439,17 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     // u = sum_{i<64} d_i 16^i + 16^64 with d_i = 2*((u >> (4i+1)) & 15) - 15 (odd, nonzero);
     // likewise radix 256 for u1 over the [1,3,...,255]G table. The top digits are 1, so the
     // accumulator starts at Q + G, never at infinity.
-    jp acc = tq[0];  // reload from scratch: keeps q out of registers during the setup
-    bool exc = false;
-    if (neg2) {
-        fe ny;
-        fp_sub(ny, fe_zero(), acc.y);
-        acc.y = ny;
-    }
+    jp29 acc = tq[0];  // reload from scratch: keeps q out of registers during the setup
+    if (neg2) f29_neg(acc.y, acc.y);
     {
-        fe gx, gy;
+        f29 gx, gy;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < 9; ++k) {
             gx.v[k] = gtab[k];
-            gy.v[k] = gtab[8 + k];
+            gy.v[k] = gtab[10 + k];
         }
-        if (neg1) {
-            fe ny;
-            fp_sub(ny, fe_zero(), gy);
-            gy = ny;
-        }
-        pt_add_aff_lean(acc, exc, gx, gy);
+        if (neg1) f29_neg(gy, gy);
+        p29_add_aff_lean(acc, gx, gy);
     }
     fe k1 = u1, k2 = u2;
     u32 above1 = 0, above2 = 0;
@@ -475,49 +468,44 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
 #pragma unroll 1
         for (int nib = 7; nib >= 0; --nib) {
 #pragma unroll 1
-            for (int d = 0; d < 4; ++d) pt_dbl(acc, acc);
+            for (int d = 0; d < 4; ++d) p29_dbl(acc, acc);
             // Q digit (odd, in [-15, 15])
             {
                 const int d2 = 2 * (int)((u32)(f2 >> (4 * nib + 1)) & 15u) - 15;
-                jp t = tq[(d2 < 0 ? -d2 : d2) >> 1];
-                if ((d2 < 0) != neg2) {
-                    fe ny;
-                    fp_sub(ny, fe_zero(), t.y);
-                    t.y = ny;
-                }
-                pt_add_jac_lean(acc, exc, t);
+                jp29 t = tq[(d2 < 0 ? -d2 : d2) >> 1];
+                if ((d2 < 0) != neg2) f29_neg(t.y, t.y);
+                p29_add_jac_lean(acc, t);
             }
             // G digit (odd, in [-255, 255]) on every other radix-16 window
             if ((nib & 1) == 0) {
                 const int d1 = 2 * (int)((u32)(f1 >> (4 * nib + 1)) & 255u) - 255;
-                const int base = ((d1 < 0 ? -d1 : d1) >> 1) * 16;
-                fe gx, gy;
+                const int base = ((d1 < 0 ? -d1 : d1) >> 1) * 20;
+                f29 gx, gy;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
+                for (int k = 0; k < 9; ++k) {
                     gx.v[k] = gtab[base + k];
-                    gy.v[k] = gtab[base + 8 + k];
+                    gy.v[k] = gtab[base + 10 + k];
                 }
-                if ((d1 < 0) != neg1) {
-                    fe ny;
-                    fp_sub(ny, fe_zero(), gy);
-                    gy = ny;
-                }
-                pt_add_aff_lean(acc, exc, gx, gy);
+                if ((d1 < 0) != neg1) f29_neg(gy, gy);
+                p29_add_aff_lean(acc, gx, gy);
             }
         }
     }
 
-    // 5. x(R) mod n == r, projectively (R is finite on every unflagged lane)
+    // 5. The lean additions leave Z = 0 from the first exceptional case on (P + P, P + (-P),
+    // R = infinity), so Z == 0 (mod p) flags the tuple for the general path. Otherwise
+    // x(R) mod n == r is checked projectively: X == r Z^2 or, when r + n < p, X == (r + n) Z^2.
+    const bool exc = fe_is_zero_raw(f29_canon_plain(acc.z));
     bool accept;
     {
         const fe rv = load_be32(rr + 32ull * idx);  // reload: keeps r out of the loop's registers
-        fe z2, lhs, xc, rm;
-        fp_sqr(z2, acc.z);
-        fp_canon(xc, acc.x);
-        fp_mul(rm, rv, r2p);
-        fp_mul(lhs, rm, z2);
-        fp_canon(lhs, lhs);
-        accept = fe_eq(lhs, xc);
+        const f29 r2 = f29_const(C29_R2);
+        f29 z2, lhs, rm;
+        f29_sqr(z2, acc.z);
+        const fe xc = f29_canon_plain(acc.x);
+        f29_mul(rm, f29_from_u256(rv), r2);
+        f29_mul(lhs, rm, z2);
+        accept = fe_eq(f29_canon_plain(lhs), xc);
         // R.x in [n, p): compare with r + n as well when r + n < p
         fe rn;
         u64 c = 0;
@@ -528,10 +516,9 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
             c >>= 32;
         }
         if (c == 0 && fe_lt(rn, P256_P)) {
-            fp_mul(rm, rn, r2p);
-            fp_mul(lhs, rm, z2);
-            fp_canon(lhs, lhs);
-            accept = accept || fe_eq(lhs, xc);
+            f29_mul(rm, f29_from_u256(rn), r2);
+            f29_mul(lhs, rm, z2);
+            accept = accept || fe_eq(f29_canon_plain(lhs), xc);
         }
     }
     if (active) {
