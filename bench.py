@@ -296,7 +296,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u32 (256-bit integers as 8x32-bit limbs)",
+            "dtype": "int32 limbs, int64 accumulators (256-bit field elements as 9 signed 29-bit limbs)",
             "data": "synthetic (on-GPU seeded keys/signatures, ~10% corrupted; smartbft_amd/workload.py)",
             "config": {"workload": "BASELINE config 2: synthetic P-256 verifies, 32-byte SHA-256 digests, "
                                    "distinct key per tuple, 10% corrupted, device-resident",

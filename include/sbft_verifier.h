@@ -95,6 +95,15 @@ int sbft_verifier_verify_consenter_sigs(sbft_verifier* v, const sbft_signature* 
                                         const sbft_proposal* p, int32_t* status);
 /* api.Verifier.VerifySignature (dependencies.go:63-64). */
 int sbft_verifier_verify_signature(sbft_verifier* v, const sbft_signature* s, char* err, size_t err_cap);
+/* Batch form of VerifySignature for the SignedViewData signatures a NewView carries
+ * (viewchanger.go:982,1021,1075): n signatures in one launch. status[i] = 0
+ * ok, SBFT_V_EKEY unknown signer, SBFT_V_EFORMAT bad value, SBFT_V_EVERIFY invalid. Returns 0 if
+ * the call ran. */
+int sbft_verifier_verify_signatures(sbft_verifier* v, const sbft_signature* sigs, size_t n, int32_t* status);
+/* Batch form of VerifyRequest (N2): n standalone signed requests in one fused launch. status[i]
+ * = 0 ok, SBFT_V_EFORMAT malformed, SBFT_V_EVERIFY invalid signature. */
+int sbft_verifier_verify_requests(sbft_verifier* v, const uint8_t* const* reqs, const size_t* lens, size_t n,
+                                  int32_t* status);
 /* api.Verifier.AuxiliaryData (dependencies.go:69-70): returns the aux length, or -1 if msg
  * is malformed; copies min(len, aux_cap) bytes. */
 int64_t sbft_verifier_auxiliary_data(const uint8_t* msg, size_t msg_len, uint8_t* aux, size_t aux_cap);
@@ -140,6 +149,46 @@ int sbft_verify_prev_commit_signatures(sbft_verifier* v, const sbft_signature* s
 int sbft_collect_commits(sbft_verifier* v, const sbft_signature* votes, const char* const* vote_digests,
                          size_t n, const sbft_proposal* p, size_t need, size_t* valid_idx,
                          size_t* n_valid, char* log, size_t log_cap);
+
+/* ---- view change ----
+ * The decoded protos.ViewMetadata of a last decision (messages.proto; the Go side unmarshals it
+ * before the call, as ValidateLastDecision does at viewchanger.go:689-692). */
+typedef struct sbft_view_metadata {
+    uint64_t view_id;
+    uint64_t latest_sequence;
+} sbft_view_metadata;
+/* ValidateLastDecision (viewchanger.go:681-727) with ONE launch for all signatures.
+ * last_decision NULL = "the last decision is not set"; md NULL = genesis (Metadata == nil:
+ * returns 0, *last_sequence = 0). Signatures are deduplicated by signer in order, verified as
+ * VerifyConsenterSig against last_decision, and the first invalid one fails the call with the
+ * reference's error text ("last decision signature is invalid, error: ..."); fewer than quorum
+ * signatures (before or after dedupe) fail as the reference does. On success *last_sequence =
+ * md->latest_sequence. */
+int sbft_validate_last_decision(sbft_verifier* v, const sbft_proposal* last_decision,
+                                const sbft_view_metadata* md, uint64_t next_view, const sbft_signature* sigs,
+                                size_t n_sigs, int quorum, uint64_t* last_sequence, char* err, size_t err_cap);
+
+/* ---- pool re-verification (N2) ----
+ * Pool.Prune's predicate (requestpool.go:335-354) as called by MaybePruneRevokedRequests
+ * (controller.go:733-746) when the verification sequence changes: VerifyRequest over every
+ * pooled request in ONE launch. pruned_idx receives the indices (ascending) whose predicate
+ * fails, i.e. the requests the pool removes; *n_pruned their count. */
+int sbft_pool_prune(sbft_verifier* v, const uint8_t* const* reqs, const size_t* lens, size_t n, size_t* pruned_idx,
+                    size_t* n_pruned);
+
+/* ---- forwarded-request micro-batching (N3) ----
+ * Controller.HandleRequest (controller.go:233-246) calls VerifyRequest from concurrent
+ * transport goroutines, one request each. A batcher coalesces concurrent calls: a call joins
+ * the open batch, which launches when it holds max_batch requests or max_wait_us after its
+ * first request arrived. sbft_request_batcher_verify blocks and returns exactly what
+ * sbft_verifier_verify_request would for that request. Thread-safe. */
+typedef struct sbft_request_batcher sbft_request_batcher;
+sbft_request_batcher* sbft_request_batcher_new(sbft_verifier* v, size_t max_batch, uint32_t max_wait_us);
+void sbft_request_batcher_free(sbft_request_batcher* b);
+int sbft_request_batcher_verify(sbft_request_batcher* b, const uint8_t* req, size_t len, char* info,
+                                size_t info_cap, char* err, size_t err_cap);
+/* launches and requests served so far (observability; the tests check coalescing with it) */
+void sbft_request_batcher_stats(const sbft_request_batcher* b, uint64_t* launches, uint64_t* requests);
 
 #ifdef __cplusplus
 }

@@ -36,17 +36,36 @@ struct f29 {
 
 #define F29_MASK 0x1FFFFFFFu
 
-// acc + a*b (signed 32 x 32 + 64), one v_mad_i64_i32. Written as asm: the compiler lowers the C
-// expression through v_mad_u64_u32 plus sign fix-ups.
+// acc + a*b (signed 32 x 32 + 64), one v_mad_i64_i32. The empty asm makes the sum opaque so
+// the compiler keeps the accumulation a chain of mads instead of re-associating it into a
+// tree of 64-bit adds (a real asm v_mad costs an s_nop per instruction: the hazard recognizer
+// treats the asm's carry-out SGPR write conservatively).
 SBFT_DEV i64 smad(u32 a, u32 b, i64 acc) {
+#ifdef SBFT_SMAD_ASM
     i64 r;
     u64 cc;
     asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "v"(b), "v"(acc));
     return r;
+#else
+    i64 r = (i64)(i32)a * (i64)(i32)b + acc;
+    asm("" : "+v"(r));
+    return r;
+#endif
+}
+// The reduction multipliers 2^9, 2^18, 2^29 - 2^21, 2^24 - 1, held in SGPRs the compiler cannot
+// see through (otherwise m * 2^9 + acc becomes a 64-bit shift, mask and add: 3 instructions).
+struct f29_red {
+    u32 c9, c18, c7, c8;
+};
+SBFT_DEV f29_red f29_red_consts() {
+    f29_red k = {1u << 9, 1u << 18, 0x1FE00000u, 0x00FFFFFFu};
+    asm("" : "+s"(k.c9), "+s"(k.c18), "+s"(k.c7), "+s"(k.c8));
+    return k;
 }
 
 // Montgomery product a*b*2^-261 mod p (normal form out, see the contract above).
 SBFT_DEV void f29_mul(f29& r, const f29& a, const f29& b) {
+    const f29_red K = f29_red_consts();
     u32 m[9];
     i64 acc = 0;
 #pragma unroll
@@ -57,10 +76,10 @@ SBFT_DEV void f29_mul(f29& r, const f29& a, const f29& b) {
             if (j < 0 || j > 8) continue;
             acc = smad(a.v[i], b.v[j], acc);
         }
-        if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], 1u << 9, acc);
-        if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], 1u << 18, acc);
-        if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], 0x1FE00000u, acc);
-        if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], 0x00FFFFFFu, acc);
+        if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], K.c9, acc);
+        if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], K.c18, acc);
+        if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], K.c7, acc);
+        if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], K.c8, acc);
         if (k < 9) m[k] = (u32)acc & F29_MASK;
         else r.v[k - 9] = (u32)acc & F29_MASK;
         acc >>= 29;
@@ -70,6 +89,7 @@ SBFT_DEV void f29_mul(f29& r, const f29& a, const f29& b) {
 
 // a^2: off-diagonal products against the doubled operand (one mad each), then the squares.
 SBFT_DEV void f29_sqr(f29& r, const f29& a) {
+    const f29_red K = f29_red_consts();
     u32 d[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
@@ -84,15 +104,97 @@ SBFT_DEV void f29_sqr(f29& r, const f29& a) {
             acc = smad(a.v[i], d[j], acc);
         }
         if ((k & 1) == 0) acc = smad(a.v[k >> 1], a.v[k >> 1], acc);
-        if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], 1u << 9, acc);
-        if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], 1u << 18, acc);
-        if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], 0x1FE00000u, acc);
-        if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], 0x00FFFFFFu, acc);
+        if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], K.c9, acc);
+        if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], K.c18, acc);
+        if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], K.c7, acc);
+        if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], K.c8, acc);
         if (k < 9) m[k] = (u32)acc & F29_MASK;
         else r.v[k - 9] = (u32)acc & F29_MASK;
         acc >>= 29;
     }
     r.v[8] = (u32)acc;
+}
+
+// N independent products (job x squares a[x] when bit x of SQ is set) with their mads
+// interleaved job by job: back-to-back dependent 64-bit mads cost a wait state (s_nop) on
+// gfx950, independent ones issue back to back. Outputs are written after all inputs are read.
+template <int N, unsigned SQ>
+SBFT_DEV void f29_mulv(f29* const* r, const f29* const* a, const f29* const* b) {
+    const f29_red K = f29_red_consts();
+    u32 d[N][9];
+#pragma unroll
+    for (int x = 0; x < N; ++x)
+        if ((SQ >> x) & 1u)
+#pragma unroll
+            for (int i = 0; i < 9; ++i) d[x][i] = a[x]->v[i] << 1;
+    u32 m[N][9], o[N][9];
+    i64 acc[N];
+#pragma unroll
+    for (int x = 0; x < N; ++x) acc[x] = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const int j = k - i;
+#pragma unroll
+            for (int x = 0; x < N; ++x) {
+                if ((SQ >> x) & 1u) {
+                    if (j > i && j <= 8) acc[x] = smad(a[x]->v[i], d[x][j], acc[x]);
+                } else {
+                    if (j >= 0 && j <= 8) acc[x] = smad(a[x]->v[i], b[x]->v[j], acc[x]);
+                }
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < N; ++x)
+            if (((SQ >> x) & 1u) && (k & 1) == 0) acc[x] = smad(a[x]->v[k >> 1], a[x]->v[k >> 1], acc[x]);
+#pragma unroll
+        for (int x = 0; x < N; ++x) {
+            if (k >= 3 && k - 3 <= 8) acc[x] = smad(m[x][k - 3], K.c9, acc[x]);
+        }
+#pragma unroll
+        for (int x = 0; x < N; ++x) {
+            if (k >= 6 && k - 6 <= 8) acc[x] = smad(m[x][k - 6], K.c18, acc[x]);
+        }
+#pragma unroll
+        for (int x = 0; x < N; ++x) {
+            if (k >= 7 && k - 7 <= 8) acc[x] = smad(m[x][k - 7], K.c7, acc[x]);
+        }
+#pragma unroll
+        for (int x = 0; x < N; ++x) {
+            if (k >= 8 && k - 8 <= 8) acc[x] = smad(m[x][k - 8], K.c8, acc[x]);
+        }
+#pragma unroll
+        for (int x = 0; x < N; ++x) {
+            if (k < 9) m[x][k] = (u32)acc[x] & F29_MASK;
+            else o[x][k - 9] = (u32)acc[x] & F29_MASK;
+            acc[x] >>= 29;
+        }
+    }
+#pragma unroll
+    for (int x = 0; x < N; ++x) {
+        o[x][8] = (u32)acc[x];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) r[x]->v[i] = o[x][i];
+    }
+}
+SBFT_DEV void f29_mul2(f29& r0, const f29& a0, const f29& b0, f29& r1, const f29& a1, const f29& b1) {
+    f29* const r[2] = {&r0, &r1};
+    const f29* const a[2] = {&a0, &a1};
+    const f29* const b[2] = {&b0, &b1};
+    f29_mulv<2, 0u>(r, a, b);
+}
+SBFT_DEV void f29_mul3(f29& r0, const f29& a0, const f29& b0, f29& r1, const f29& a1, const f29& b1, f29& r2,
+                       const f29& a2, const f29& b2) {
+    f29* const r[3] = {&r0, &r1, &r2};
+    const f29* const a[3] = {&a0, &a1, &a2};
+    const f29* const b[3] = {&b0, &b1, &b2};
+    f29_mulv<3, 0u>(r, a, b);
+}
+SBFT_DEV void f29_sqr2(f29& r0, const f29& a0, f29& r1, const f29& a1) {
+    f29* const r[2] = {&r0, &r1};
+    const f29* const a[2] = {&a0, &a1};
+    f29_mulv<2, 3u>(r, a, a);
 }
 
 SBFT_DEV void f29_add(f29& r, const f29& a, const f29& b) {
@@ -165,7 +267,7 @@ SBFT_DEV f29 f29_const(const u32* c) {
 // 6M + 2S, every intermediate inside the signed 32-bit limbs. In: X in N, Y in N or N+-,
 // Z in N. Out: N (X3, Y3 normalised; Z3 a mul output).
 // Z = 0 maps to Z3 = 0 (the caller's exceptional-case detector relies on it).
-SBFT_DEV void p29_dbl(jp29& r, const jp29& p) {
+SBFT_DEV void p29_dbl_s(jp29& r, const jp29& p) {
     f29 d, g, b2, t0, t1, a1, a3, u, m;
     f29_sqr(d, p.z);                 // 2^29.2^2
     f29_sqr(g, p.y);
@@ -193,7 +295,7 @@ SBFT_DEV void p29_dbl(jp29& r, const jp29& p) {
 // acc += b (b Jacobian, N; b.y may be N+-) with no case analysis (12M + 4S). If H == 0
 // (acc == +-b) the result has Z3 = 0, which every later doubling and addition keeps at 0:
 // the caller checks Z once at the end and re-verifies such tuples on the general path.
-SBFT_DEV void p29_add_jac_lean(jp29& acc, const jp29& b) {
+SBFT_DEV void p29_add_jac_lean_s(jp29& acc, const jp29& b) {
     f29 z1z1, z2z2, u1, u2, s1, s2, t, h, rr, hh, hhh;
     f29_sqr(z1z1, acc.z);
     f29_mul(u2, b.x, z1z1);
@@ -221,7 +323,7 @@ SBFT_DEV void p29_add_jac_lean(jp29& acc, const jp29& b) {
 }
 
 // acc += (x2, y2) affine (N; y2 may be N+-), same structure: 8M + 3S.
-SBFT_DEV void p29_add_aff_lean(jp29& acc, const f29& x2, const f29& y2) {
+SBFT_DEV void p29_add_aff_lean_s(jp29& acc, const f29& x2, const f29& y2) {
     f29 z1z1, u2, s2, h, rr, hh, hhh, t;
     f29_sqr(z1z1, acc.z);
     f29_mul(u2, x2, z1z1);
@@ -241,6 +343,86 @@ SBFT_DEV void p29_add_aff_lean(jp29& acc, const f29& x2, const f29& y2) {
     f29_mul(t, rr, t);
     f29_mul(s2, acc.y, hhh);
     f29_sub(acc.y, t, s2);           // N+-
+}
+
+SBFT_DEV void p29_dbl_i(jp29& r, const jp29& p) {
+    f29 d, g, b2, t0, t1, a1, a3, u, m;
+    f29_sqr2(d, p.z, g, p.y);        // 2^29.2^2 each
+    f29_add(t0, g, g);               // 2g < 2^30
+    f29_sub(t1, p.x, d);             // (-2^29, 2^29.2)
+    f29_add(a1, p.x, d);             // < 2^30.1
+    f29_mul2(b2, p.x, t0,            // 2XY^2 (2^29.2 x 2^30)
+             a1, t1, a1);            // a'  (2^29.2 x 2^30.1)
+    f29_add(t1, p.y, p.y);           // 2Y < 2^30.2
+    f29_muls(a3, a1, 3);             // 3a' < 2^30.6
+    f29_mul3(r.z, t1, p.z,           // Z3 = 2YZ (2^30.2 x 2^29.2)
+             u, a1, a3,              // u = 3a'^2 (2^29 x 2^30.6)
+             g, g, t0);              // 2g^2 (2^29 x 2^30)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t1.v[i] = 3 * u.v[i] - (b2.v[i] << 2);  // (-2^31, 2^30.6)
+    f29_normalize(r.x, t1);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t0.v[i] = (b2.v[i] << 1) - r.x.v[i];  // (-2^29.2, 2^30)
+    f29_mul(m, a1, t0);              // a'(2 b2 - X3) (2^29 x 2^30)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t1.v[i] = 3 * m.v[i] - (g.v[i] << 2);  // (-2^31, 2^30.6)
+    f29_normalize(r.y, t1);
+}
+
+// acc += b (b Jacobian, N; b.y may be N+-) with no case analysis (12M + 4S). If H == 0
+// (acc == +-b) the result has Z3 = 0, which every later doubling and addition keeps at 0:
+// the caller checks Z once at the end and re-verifies such tuples on the general path.
+SBFT_DEV void p29_add_jac_lean_i(jp29& acc, const jp29& b) {
+    f29 z1z1, z2z2, u1, u2, s1, s2, t1, t2, z12, h, rr, hh, r2, hhh;
+    f29_sqr2(z1z1, acc.z, z2z2, b.z);
+    f29_mul2(u2, b.x, z1z1, t1, acc.z, z1z1);
+    f29_mul3(u1, acc.x, z2z2, t2, b.z, z2z2, z12, acc.z, b.z);
+    f29_mul2(s2, b.y, t1, s1, acc.y, t2);
+    f29_sub(h, u2, u1);              // N+-
+    f29_sub(rr, s2, s1);             // N+-
+    f29_sqr2(hh, h, r2, rr);
+    f29_mul3(hhh, hh, h, u1, u1, hh, acc.z, z12, h);  // H^3, V = U1 H^2, Z3 = Z1 Z2 H
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t1.v[i] = r2.v[i] - hhh.v[i] - (u1.v[i] << 1);  // (-3 2^29, 2^29)
+    f29_normalize(acc.x, t1);
+    f29_sub(t1, u1, acc.x);          // (-2^29.2, 2^29 + 2^26)
+    f29_mul2(t1, rr, t1, s1, s1, hhh);
+    f29_sub(acc.y, t1, s1);          // N+-
+}
+
+// acc += (x2, y2) affine (N; y2 may be N+-), same structure: 8M + 3S.
+SBFT_DEV void p29_add_aff_lean_i(jp29& acc, const f29& x2, const f29& y2) {
+    f29 z1z1, u2, s2, h, rr, hh, r2, hhh, t;
+    f29_sqr(z1z1, acc.z);
+    f29_mul2(u2, x2, z1z1, s2, acc.z, z1z1);
+    f29_mul(s2, y2, s2);
+    f29_sub(h, u2, acc.x);           // (-2^29.2, 2^29 + 2^4)
+    f29_sub(rr, s2, acc.y);          // (-2^29.2, 2^29.2)
+    f29_sqr2(hh, h, r2, rr);
+    f29_mul3(hhh, hh, h, u2, acc.x, hh, acc.z, acc.z, h);  // H^3, V = X1 H^2, Z3 = Z1 H
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] = r2.v[i] - hhh.v[i] - (u2.v[i] << 1);
+    f29_normalize(acc.x, t);
+    f29_sub(t, u2, acc.x);
+    f29_mul2(t, rr, t, s2, acc.y, hhh);
+    f29_sub(acc.y, t, s2);           // N+-
+}
+
+#ifndef SBFT_F29_IL
+#define SBFT_F29_IL 6
+#endif
+// SBFT_F29_IL bit 0/1/2: interleaved form of the doubling / Jacobian addition / mixed addition
+SBFT_DEV void p29_dbl(jp29& r, const jp29& p) {
+    if (SBFT_F29_IL & 1) p29_dbl_i(r, p);
+    else p29_dbl_s(r, p);
+}
+SBFT_DEV void p29_add_jac_lean(jp29& acc, const jp29& b) {
+    if (SBFT_F29_IL & 2) p29_add_jac_lean_i(acc, b);
+    else p29_add_jac_lean_s(acc, b);
+}
+SBFT_DEV void p29_add_aff_lean(jp29& acc, const f29& x2, const f29& y2) {
+    if (SBFT_F29_IL & 4) p29_add_aff_lean_i(acc, x2, y2);
+    else p29_add_aff_lean_s(acc, x2, y2);
 }
 
 // ---------------------------------------------------------------- conversions

@@ -9,9 +9,12 @@
 
 #include <array>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
@@ -412,6 +415,87 @@ struct sbft_verifier {
                                           s.data(), qx.data(), qy.data(), n, ok, nullptr);
     }
 
+    // Verify n standalone signed requests with one fused launch (VerifyRequest's batch form).
+    // status[i]: 0 ok, SBFT_V_EFORMAT, SBFT_V_EVERIFY; parsed[i] holds the request's ids.
+    int requests_batch(const uint8_t* const* reqs, const size_t* lens, size_t n, int32_t* status,
+                       std::vector<Req>& parsed) {
+        parsed.assign(n, Req());
+        std::vector<const uint8_t*> msgs, sv, kv;
+        std::vector<size_t> mlens, which;
+        for (size_t i = 0; i < n; ++i) {
+            status[i] = 0;
+            if (!reqs[i] || !parse_request(reqs[i], lens[i], 0, parsed[i]) || parsed[i].pub[0] != 0x04) {
+                status[i] = SBFT_V_EFORMAT;
+                continue;
+            }
+            msgs.push_back(reqs[i]);
+            mlens.push_back(parsed[i].body_len);
+            sv.push_back(parsed[i].sig);
+            kv.push_back(parsed[i].pub + 1);
+            which.push_back(i);
+        }
+        std::vector<uint8_t> ok(which.size());
+        const int rc = gpu_verify_messages(msgs, mlens, sv, kv, ok.data());
+        if (rc) return rc;
+        for (size_t k = 0; k < which.size(); ++k)
+            if (!ok[k]) status[which[k]] = SBFT_V_EVERIFY;
+        return 0;
+    }
+
+    // VerifySignature's batch form: n (id, r||s, msg) under registered keys; keys with comb
+    // tables take the keyed launch, the rest the generic fused launch. reasons[i] = error text.
+    int signatures_batch(const sbft_signature* sigs, size_t n, int32_t* status, std::vector<std::string>* reasons) {
+        std::vector<const uint8_t*> msgs, sv, kv, kmsgs, ksv;
+        std::vector<size_t> lens, which, klens, kwhich;
+        std::vector<uint32_t> kids;
+        std::vector<std::array<uint8_t, 64>> keybuf(n);
+        if (reasons) reasons->assign(n, std::string());
+        static const uint8_t empty = 0;
+        for (size_t i = 0; i < n; ++i) {
+            status[i] = 0;
+            uint32_t kid = 0;
+            if (!key_of(sigs[i].id, keybuf[i], &kid)) {
+                status[i] = SBFT_V_EKEY;
+                if (reasons) (*reasons)[i] = "unknown signer " + std::to_string(sigs[i].id);
+                continue;
+            }
+            if (sigs[i].value_len != 64 || !sigs[i].value) {
+                status[i] = SBFT_V_EFORMAT;
+                if (reasons) (*reasons)[i] = "signature value must be 64 bytes r||s";
+                continue;
+            }
+            const uint8_t* m = sigs[i].msg ? sigs[i].msg : &empty;
+            if (kid) {
+                kmsgs.push_back(m);
+                klens.push_back(sigs[i].msg_len);
+                ksv.push_back(sigs[i].value);
+                kids.push_back(kid);
+                kwhich.push_back(i);
+            } else {
+                msgs.push_back(m);
+                lens.push_back(sigs[i].msg_len);
+                sv.push_back(sigs[i].value);
+                kv.push_back(keybuf[i].data());
+                which.push_back(i);
+            }
+        }
+        std::vector<uint8_t> ok(which.size()), kok(kwhich.size());
+        int rc = gpu_verify_keyed(kmsgs, klens, ksv, kids, kok.data());
+        if (rc) return rc;
+        rc = gpu_verify_messages(msgs, lens, sv, kv, ok.data());
+        if (rc) return rc;
+        auto mark = [&](const std::vector<size_t>& w, const std::vector<uint8_t>& o) {
+            for (size_t k = 0; k < w.size(); ++k)
+                if (!o[k]) {
+                    status[w[k]] = SBFT_V_EVERIFY;
+                    if (reasons) (*reasons)[w[k]] = "invalid signature from " + std::to_string(sigs[w[k]].id);
+                }
+        };
+        mark(kwhich, kok);
+        mark(which, ok);
+        return 0;
+    }
+
     // Check + verify consenter signatures over one proposal. status[i]: 0 ok, <0 error;
     // reasons[i] gets the error text.
     int consenter_batch(const sbft_signature* sigs, size_t n, const sbft_proposal* p, int32_t* status,
@@ -663,30 +747,27 @@ int sbft_verifier_verify_consenter_sigs(sbft_verifier* v, const sbft_signature* 
 
 int sbft_verifier_verify_signature(sbft_verifier* v, const sbft_signature* s, char* err, size_t err_cap) {
     if (!v || !s) return SBFT_GV_EINVAL;
-    std::array<uint8_t, 64> key;
-    uint32_t kid = 0;
-    if (!v->key_of(s->id, key, &kid)) {
-        put_err(err, err_cap, "unknown signer %llu", (unsigned long long)s->id);
-        return SBFT_V_EKEY;
-    }
-    if (s->value_len != 64 || !s->value) {
-        put_err(err, err_cap, "signature value must be 64 bytes r||s");
-        return SBFT_V_EFORMAT;
-    }
-    std::vector<const uint8_t*> msgs{s->msg ? s->msg : (const uint8_t*)""}, sigs{s->value}, keys{key.data()};
-    std::vector<size_t> lens{s->msg_len};
-    uint8_t ok = 0;
-    const int rc = kid ? v->gpu_verify_keyed(msgs, lens, sigs, {kid}, &ok)
-                       : v->gpu_verify_messages(msgs, lens, sigs, keys, &ok);
+    int32_t st = 0;
+    std::vector<std::string> why;
+    const int rc = v->signatures_batch(s, 1, &st, &why);
     if (rc) {
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
         return rc;
     }
-    if (!ok) {
-        put_err(err, err_cap, "invalid signature from %llu", (unsigned long long)s->id);
-        return SBFT_V_EVERIFY;
-    }
-    return 0;
+    if (st) put_err(err, err_cap, "%s", why[0].c_str());
+    return st;
+}
+
+int sbft_verifier_verify_signatures(sbft_verifier* v, const sbft_signature* sigs, size_t n, int32_t* status) {
+    if (!v || (n && (!sigs || !status))) return SBFT_GV_EINVAL;
+    return v->signatures_batch(sigs, n, status, nullptr);
+}
+
+int sbft_verifier_verify_requests(sbft_verifier* v, const uint8_t* const* reqs, const size_t* lens, size_t n,
+                                  int32_t* status) {
+    if (!v || (n && (!reqs || !lens || !status))) return SBFT_GV_EINVAL;
+    std::vector<Req> parsed;
+    return v->requests_batch(reqs, lens, n, status, parsed);
 }
 
 int64_t sbft_verifier_auxiliary_data(const uint8_t* msg, size_t msg_len, uint8_t* aux, size_t aux_cap) {
@@ -766,6 +847,190 @@ int sbft_collect_commits(sbft_verifier* v, const sbft_signature* votes, const ch
         std::memcpy(log, lg.data(), m);
         log[m] = 0;
     }
+    return 0;
+}
+
+// ---------------------------------------------------------------------- view change (N1)
+int sbft_validate_last_decision(sbft_verifier* v, const sbft_proposal* last_decision,
+                                const sbft_view_metadata* md, uint64_t next_view, const sbft_signature* sigs,
+                                size_t n_sigs, int quorum, uint64_t* last_sequence, char* err, size_t err_cap) {
+    if (!v || (n_sigs && !sigs)) return SBFT_GV_EINVAL;
+    if (last_sequence) *last_sequence = 0;
+    if (!last_decision) {
+        put_err(err, err_cap, "the last decision is not set");
+        return SBFT_V_EVERIFY;
+    }
+    if (!md) return 0;  // genesis proposal: no signatures to validate
+    if (md->view_id >= next_view) {
+        put_err(err, err_cap, "last decision view %llu is greater or equal to requested next view %llu",
+                (unsigned long long)md->view_id, (unsigned long long)next_view);
+        return SBFT_V_EVERIFY;
+    }
+    if ((long long)n_sigs < (long long)quorum) {
+        put_err(err, err_cap, "there are only %zu last decision signatures", n_sigs);
+        return SBFT_V_EVERIFY;
+    }
+    // dedupe by signer in arrival order (viewchanger.go:700-706), then one launch for all
+    std::vector<sbft_signature> batch;
+    std::unordered_map<uint64_t, bool> seen;
+    for (size_t i = 0; i < n_sigs; ++i) {
+        if (seen.count(sigs[i].id)) continue;
+        seen[sigs[i].id] = true;
+        batch.push_back(sigs[i]);
+    }
+    std::vector<int32_t> st(batch.size());
+    std::vector<std::string> why;
+    const int rc = v->consenter_batch(batch.data(), batch.size(), last_decision, st.data(), &why);
+    if (rc) {
+        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+        return rc;
+    }
+    for (size_t k = 0; k < batch.size(); ++k)
+        if (st[k]) {  // the first invalid one in order, as the serial loop reports it
+            put_err(err, err_cap, "last decision signature is invalid, error: %s", why[k].c_str());
+            return SBFT_V_EVERIFY;
+        }
+    if ((long long)batch.size() < (long long)quorum) {
+        put_err(err, err_cap, "there are only %zu valid last decision signatures", batch.size());
+        return SBFT_V_EVERIFY;
+    }
+    if (last_sequence) *last_sequence = md->latest_sequence;
+    return 0;
+}
+
+// ---------------------------------------------------------------------- pool prune (N2)
+int sbft_pool_prune(sbft_verifier* v, const uint8_t* const* reqs, const size_t* lens, size_t n, size_t* pruned_idx,
+                    size_t* n_pruned) {
+    if (!v || !n_pruned || (n && (!reqs || !lens || !pruned_idx))) return SBFT_GV_EINVAL;
+    *n_pruned = 0;
+    std::vector<int32_t> st(n);
+    std::vector<Req> parsed;
+    const int rc = v->requests_batch(reqs, lens, n, st.data(), parsed);
+    if (rc) return rc;
+    for (size_t i = 0; i < n; ++i)
+        if (st[i]) pruned_idx[(*n_pruned)++] = i;
+    return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------- request batcher (N3)
+// Concurrent VerifyRequest callers (Controller.HandleRequest from transport goroutines,
+// controller.go:233-246) are coalesced into one launch. No background thread: the first
+// caller of an open batch leads it - it waits until the batch is full or its deadline
+// passes, closes it, runs one requests_batch launch and wakes the followers. Batches that
+// close while another is in flight launch concurrently (the engine is thread-safe).
+struct sbft_request_batcher {
+    sbft_verifier* v;
+    size_t max_batch;
+    std::chrono::microseconds max_wait;
+    struct Entry {
+        const uint8_t* req;
+        size_t len;
+        int32_t status = 0;
+        Req parsed;
+    };
+    struct Batch {
+        std::vector<Entry*> entries;
+        bool closed = false, done = false;
+        int rc = 0;
+        std::condition_variable cv;
+    };
+    std::mutex mu;
+    std::shared_ptr<Batch> open;
+    std::atomic<uint64_t> launches{0}, requests{0};
+};
+
+extern "C" {
+
+sbft_request_batcher* sbft_request_batcher_new(sbft_verifier* v, size_t max_batch, uint32_t max_wait_us) {
+    if (!v || max_batch == 0) return nullptr;
+    auto* b = new sbft_request_batcher();
+    b->v = v;
+    b->max_batch = max_batch;
+    b->max_wait = std::chrono::microseconds(max_wait_us);
+    return b;
+}
+
+void sbft_request_batcher_free(sbft_request_batcher* b) { delete b; }
+
+void sbft_request_batcher_stats(const sbft_request_batcher* b, uint64_t* launches, uint64_t* requests) {
+    if (!b) return;
+    if (launches) *launches = b->launches.load();
+    if (requests) *requests = b->requests.load();
+}
+
+int sbft_request_batcher_verify(sbft_request_batcher* b, const uint8_t* req, size_t len, char* info, size_t info_cap,
+                                char* err, size_t err_cap) {
+    if (!b || !req) return SBFT_GV_EINVAL;
+    using Batch = sbft_request_batcher::Batch;
+    sbft_request_batcher::Entry me;
+    me.req = req;
+    me.len = len;
+    std::shared_ptr<Batch> batch;
+    bool leader = false;
+    {
+        std::unique_lock<std::mutex> g(b->mu);
+        if (!b->open) {
+            b->open = std::make_shared<Batch>();
+            leader = true;
+        }
+        batch = b->open;
+        batch->entries.push_back(&me);
+        if (batch->entries.size() >= b->max_batch) {
+            batch->closed = true;
+            b->open.reset();
+            batch->cv.notify_all();  // wakes the leader early
+        }
+        if (leader) {
+            const auto deadline = std::chrono::steady_clock::now() + b->max_wait;
+            batch->cv.wait_until(g, deadline, [&] { return batch->closed; });
+            if (!batch->closed) {
+                batch->closed = true;
+                b->open.reset();
+            }
+        } else {
+            batch->cv.wait(g, [&] { return batch->done; });
+        }
+    }
+    if (leader) {
+        // the batch is closed: nobody else touches its entries until done is published
+        const size_t n = batch->entries.size();
+        std::vector<const uint8_t*> reqs(n);
+        std::vector<size_t> lens(n);
+        for (size_t i = 0; i < n; ++i) {
+            reqs[i] = batch->entries[i]->req;
+            lens[i] = batch->entries[i]->len;
+        }
+        std::vector<int32_t> st(n);
+        std::vector<Req> parsed;
+        const int rc = b->v->requests_batch(reqs.data(), lens.data(), n, st.data(), parsed);
+        b->launches++;
+        b->requests += n;
+        std::lock_guard<std::mutex> g(b->mu);
+        for (size_t i = 0; i < n; ++i) {
+            batch->entries[i]->status = st[i];
+            batch->entries[i]->parsed = std::move(parsed[i]);
+        }
+        batch->rc = rc;
+        batch->done = true;
+        batch->cv.notify_all();
+    }
+    if (batch->rc) {
+        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(batch->rc));
+        return batch->rc;
+    }
+    if (me.status == SBFT_V_EFORMAT) {
+        put_err(err, err_cap, "malformed request");
+        return SBFT_V_EFORMAT;
+    }
+    if (me.status) {
+        put_err(err, err_cap, "request %s:%s has an invalid signature", me.parsed.client_id.c_str(),
+                me.parsed.req_id.c_str());
+        return me.status;
+    }
+    char* w = info;
+    if (info && !write_info(w, info + info_cap, me.parsed.client_id, me.parsed.req_id)) return SBFT_V_ESPACE;
     return 0;
 }
 

@@ -32,6 +32,17 @@ class _Signature(ctypes.Structure):
                 ("msg", _u8p), ("msg_len", ctypes.c_size_t)]
 
 
+class _ViewMetadata(ctypes.Structure):
+    _fields_ = [("view_id", ctypes.c_uint64), ("latest_sequence", ctypes.c_uint64)]
+
+
+@dataclass
+class ViewMetadata:
+    """The decoded protos.ViewMetadata fields ValidateLastDecision reads (viewchanger.go:689-693)."""
+    ViewId: int
+    LatestSequence: int
+
+
 @dataclass
 class Proposal:
     """types.Proposal (pkg/types/types.go:18-23)."""
@@ -77,6 +88,12 @@ def _prop(p: Proposal, keep: list) -> _Proposal:
 
 def _sig(s: Signature, keep: list) -> _Signature:
     return _Signature(s.ID, _buf(s.Value, keep), len(s.Value), _buf(s.Msg, keep), len(s.Msg))
+
+
+def _blobs(items: list[bytes], keep: list):
+    arr = (_u8p * max(1, len(items)))(*[_buf(b, keep) for b in items])
+    lens = (ctypes.c_size_t * max(1, len(items)))(*[len(b) for b in items])
+    return arr, lens
 
 
 def _infos(buf, count: int) -> list[RequestInfo]:
@@ -134,6 +151,22 @@ def _lib():
                                                      ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_size_t]
     L.sbft_collect_commits.argtypes = [_vp, S, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, P,
                                        ctypes.c_size_t, sz, sz, ctypes.c_char_p, ctypes.c_size_t]
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    u8pp = ctypes.POINTER(_u8p)
+    L.sbft_verifier_verify_signatures.argtypes = [_vp, S, ctypes.c_size_t, i32p]
+    L.sbft_verifier_verify_requests.argtypes = [_vp, u8pp, sz, ctypes.c_size_t, i32p]
+    L.sbft_validate_last_decision.argtypes = [_vp, P, ctypes.POINTER(_ViewMetadata), ctypes.c_uint64, S,
+                                              ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                              ctypes.c_char_p, ctypes.c_size_t]
+    L.sbft_pool_prune.argtypes = [_vp, u8pp, sz, ctypes.c_size_t, sz, sz]
+    L.sbft_request_batcher_new.restype = _vp
+    L.sbft_request_batcher_new.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint32]
+    L.sbft_request_batcher_free.argtypes = [_vp]
+    L.sbft_request_batcher_free.restype = None
+    L.sbft_request_batcher_verify.argtypes = [_vp, _u8p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                              ctypes.c_char_p, ctypes.c_size_t]
+    L.sbft_request_batcher_stats.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    L.sbft_request_batcher_stats.restype = None
     _L = L
     return L
 
@@ -273,6 +306,55 @@ class Verifier:
             raise VerifyError(rc, err.value.decode())
         return bool(skipped.value)
 
+    def VerifySignatures(self, sigs: list[Signature]) -> list[int]:
+        """Batch VerifySignature (NewView's SignedViewData, viewchanger.go:982,1021,1075)."""
+        keep = []
+        arr = (_Signature * max(1, len(sigs)))(*[_sig(s, keep) for s in sigs])
+        st = (ctypes.c_int32 * max(1, len(sigs)))()
+        rc = self.L.sbft_verifier_verify_signatures(self.h, arr, len(sigs), st)
+        if rc:
+            raise VerifyError(rc, "engine failure")
+        return list(st[:len(sigs)])
+
+    def VerifyRequests(self, reqs: list[bytes]) -> list[int]:
+        """Batch VerifyRequest: status per request (0 ok, EFORMAT, EVERIFY)."""
+        keep = []
+        arr, lens = _blobs(reqs, keep)
+        st = (ctypes.c_int32 * max(1, len(reqs)))()
+        rc = self.L.sbft_verifier_verify_requests(self.h, arr, lens, len(reqs), st)
+        if rc:
+            raise VerifyError(rc, "engine failure")
+        return list(st[:len(reqs)])
+
+    def validate_last_decision(self, last_decision: Proposal | None, md: ViewMetadata | None, next_view: int,
+                               sigs: list[Signature], quorum: int) -> int:
+        """ValidateLastDecision (viewchanger.go:681-727): returns the last sequence, raises
+        VerifyError with the reference's error text."""
+        keep = []
+        arr = (_Signature * max(1, len(sigs)))(*[_sig(s, keep) for s in sigs])
+        cmd = _ViewMetadata(md.ViewId, md.LatestSequence) if md is not None else None
+        seq = ctypes.c_uint64()
+        err = ctypes.create_string_buffer(512)
+        rc = self.L.sbft_validate_last_decision(
+            self.h, ctypes.byref(_prop(last_decision, keep)) if last_decision is not None else None,
+            ctypes.byref(cmd) if cmd is not None else None, next_view, arr, len(sigs), quorum,
+            ctypes.byref(seq), err, 512)
+        if rc:
+            raise VerifyError(rc, err.value.decode())
+        return seq.value
+
+    def pool_prune(self, reqs: list[bytes]) -> list[int]:
+        """Pool.Prune(VerifyRequest) (requestpool.go:335-354, controller.go:742-745): indices
+        of the requests the pool removes."""
+        keep = []
+        arr, lens = _blobs(reqs, keep)
+        idx = (ctypes.c_size_t * max(1, len(reqs)))()
+        n = ctypes.c_size_t()
+        rc = self.L.sbft_pool_prune(self.h, arr, lens, len(reqs), idx, ctypes.byref(n))
+        if rc:
+            raise VerifyError(rc, "engine failure")
+        return list(idx[:n.value])
+
     def collect_commits(self, votes: list[tuple[Signature, str]], p: Proposal, need: int):
         keep = []
         arr = (_Signature * max(1, len(votes)))(*[_sig(s, keep) for s, _ in votes])
@@ -285,6 +367,42 @@ class Verifier:
         if rc:
             raise VerifyError(rc, "engine failure")
         return list(idx[:nv.value]), log.value.decode()
+
+
+class RequestBatcher:
+    """Forwarded-request micro-batching (controller.go:233-246): concurrent VerifyRequest
+    calls share one launch (include/sbft_verifier.h, sbft_request_batcher_*)."""
+
+    def __init__(self, verifier: Verifier, max_batch: int = 256, max_wait_us: int = 200):
+        self.L = verifier.L
+        self.verifier = verifier  # keeps the verifier alive
+        self.h = self.L.sbft_request_batcher_new(verifier.h, max_batch, max_wait_us)
+        assert self.h
+
+    def close(self):
+        if self.h:
+            self.L.sbft_request_batcher_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def VerifyRequest(self, req: bytes) -> RequestInfo:
+        keep = []
+        info = ctypes.create_string_buffer(len(req) + 8)
+        err = ctypes.create_string_buffer(512)
+        rc = self.L.sbft_request_batcher_verify(self.h, _buf(req, keep), len(req), info, len(req) + 8, err, 512)
+        if rc:
+            raise VerifyError(rc, err.value.decode())
+        return _infos(info, 1)[0]
+
+    def stats(self) -> tuple[int, int]:
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self.L.sbft_request_batcher_stats(self.h, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
 
 
 class Signer:

@@ -170,3 +170,106 @@ def test_collect_commits_quorum_n100(gpu):
     assert 3 not in idx and 7 not in idx and 10 not in idx
     assert f"Couldn't verify {votes[3][0].ID}'s signature: invalid signature" in log
     assert "Got wrong digest at processCommits" in log
+
+
+# ---- N1: view change --------------------------------------------------------------------
+def test_validate_last_decision(net):
+    """ValidateLastDecision (viewchanger.go:681-727), one launch; the cases of
+    TestValidateLastDecision (viewchanger_test.go:1415-1522): dedupe by signer, any invalid
+    signature fails, fewer valid than quorum fails."""
+    v, nodes, clients = net
+    prev, _ = _proposal(clients, 4)
+    md = plugin.ViewMetadata(ViewId=1, LatestSequence=7)
+    sigs = [n.SignProposal(prev, b"") for n in nodes[:3]]
+    assert v.validate_last_decision(prev, md, 2, sigs, 3) == 7
+    # a duplicate of a valid signer does not count twice
+    with pytest.raises(plugin.VerifyError, match="^there are only 2 valid last decision signatures$"):
+        v.validate_last_decision(prev, md, 2, [sigs[0], sigs[1], sigs[0]], 3)
+    bad = list(sigs)
+    bad[1] = plugin.Signature(sigs[1].ID, sigs[0].Value, sigs[1].Msg)
+    with pytest.raises(plugin.VerifyError,
+                       match="^last decision signature is invalid, error: invalid signature$"):
+        v.validate_last_decision(prev, md, 2, bad, 3)
+    other, _ = _proposal(clients, 5)
+    with pytest.raises(plugin.VerifyError, match="does not bind"):
+        v.validate_last_decision(other, md, 2, sigs, 3)
+
+
+def test_verify_signatures_batch(net):
+    """NewView's SignedViewData signatures (viewchanger.go:982,1021,1075) in one launch; each
+    status equals what the single VerifySignature call returns."""
+    v, nodes, clients = net
+    sigs = [plugin.Signature(n.id, n.Sign(b"view-data-%d" % n.id), b"view-data-%d" % n.id) for n in nodes]
+    sigs.append(plugin.Signature(nodes[0].id, sigs[1].Value, sigs[0].Msg))   # wrong value
+    sigs.append(plugin.Signature(99, sigs[0].Value, sigs[0].Msg))            # unknown signer
+    sigs.append(plugin.Signature(nodes[0].id, sigs[0].Value[:63], sigs[0].Msg))  # short value
+    st = v.VerifySignatures(sigs)
+    assert st == [0, 0, 0, 0, plugin.EVERIFY, plugin.EKEY, plugin.EFORMAT]
+    for s, want in zip(sigs, st):
+        if want == 0:
+            v.VerifySignature(s)
+        else:
+            with pytest.raises(plugin.VerifyError) as ei:
+                v.VerifySignature(s)
+            assert ei.value.code == want
+
+
+# ---- N2: pool re-verification -------------------------------------------------------------
+def test_pool_prune_and_verify_requests(net):
+    """MaybePruneRevokedRequests -> Pool.Prune(VerifyRequest) (controller.go:733-746,
+    requestpool.go:335-354): one launch over the pool; pruned = the requests whose
+    VerifyRequest fails, in pool order."""
+    v, nodes, clients = net
+    pool = [clients[i % 8].make_request(f"c{i % 8}", f"r{i}", b"x" * (i % 97)) for i in range(400)]
+    bad = {3, 77, 200, 399}
+    for i in bad:
+        r = pool[i]
+        pool[i] = r[:-1] + bytes([r[-1] ^ 4])
+    pool[150] = pool[150][:20]  # malformed
+    st = v.VerifyRequests(pool)
+    assert [i for i, s in enumerate(st) if s] == sorted(bad | {150})
+    assert st[150] == plugin.EFORMAT and st[3] == plugin.EVERIFY
+    assert v.pool_prune(pool) == sorted(bad | {150})
+    for i in (0, 3, 150):  # same verdict as the single call
+        if st[i]:
+            with pytest.raises(plugin.VerifyError):
+                v.VerifyRequest(pool[i])
+        else:
+            v.VerifyRequest(pool[i])
+
+
+# ---- N3: forwarded-request micro-batching ------------------------------------------------
+def test_request_batcher_coalesces_concurrent_callers(net):
+    """HandleRequest's VerifyRequest from concurrent transport goroutines (controller.go:233-246):
+    64 threads, one request each, coalesce into few launches; every caller gets its own verdict."""
+    import threading
+    v, nodes, clients = net
+    reqs = [clients[i % 8].make_request(f"c{i % 8}", f"fw{i}", b"p%d" % i) for i in range(64)]
+    reqs[9] = reqs[9][:-1] + bytes([reqs[9][-1] ^ 1])
+    b = plugin.RequestBatcher(v, max_batch=64, max_wait_us=20000)
+    out = [None] * len(reqs)
+    start = threading.Barrier(len(reqs))
+
+    def call(i):
+        start.wait()
+        try:
+            out[i] = b.VerifyRequest(reqs[i])
+        except plugin.VerifyError as e:
+            out[i] = e
+
+    th = [threading.Thread(target=call, args=(i,)) for i in range(len(reqs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    assert isinstance(out[9], plugin.VerifyError) and out[9].code == plugin.EVERIFY
+    assert "has an invalid signature" in str(out[9])
+    for i, o in enumerate(out):
+        if i != 9:
+            assert (o.ClientID, o.ID) == (f"c{i % 8}", f"fw{i}")
+    launches, served = b.stats()
+    assert served == 64 and launches < 16, (launches, served)
+    # a lone caller is served after its deadline, with one launch
+    assert b.VerifyRequest(reqs[0]).ID == "fw0"
+    assert b.stats() == (launches + 1, 65)
+    b.close()

@@ -83,3 +83,34 @@ def test_auxiliary_data():
     assert plugin.AuxiliaryData(msg) == aux
     assert plugin.AuxiliaryData(msg[:-1]) is None
     assert plugin.AuxiliaryData(b"") is None
+
+
+def test_validate_last_decision_prechecks():
+    """ValidateLastDecision's checks that precede any signature work (viewchanger.go:682-699),
+    with the reference's error texts; a parse-only verifier never reaches the engine here."""
+    v = plugin.Verifier(None)
+    sig = plugin.Signature(1, b"\0" * 64, b"m")
+    with pytest.raises(plugin.VerifyError, match="^the last decision is not set$"):
+        v.validate_last_decision(None, None, 5, [sig], 3)
+    p = plugin.Proposal(b"payload", b"h", b"md", 1)
+    assert v.validate_last_decision(p, None, 5, [], 3) == 0  # genesis: nothing to validate
+    with pytest.raises(plugin.VerifyError,
+                       match="^last decision view 5 is greater or equal to requested next view 5$"):
+        v.validate_last_decision(p, plugin.ViewMetadata(5, 9), 5, [sig] * 3, 3)
+    with pytest.raises(plugin.VerifyError, match="^there are only 2 last decision signatures$"):
+        v.validate_last_decision(p, plugin.ViewMetadata(4, 9), 5, [sig] * 2, 3)
+
+
+def test_batch_entry_points_need_engine():
+    """Batch forms on a parse-only verifier: malformed inputs are classified on the host, and
+    anything needing a signature check fails loudly (no CPU fallback)."""
+    v = plugin.Verifier(None)
+    assert v.VerifyRequests([b"", b"SBR1junk"]) == [plugin.EFORMAT, plugin.EFORMAT]
+    assert v.pool_prune([b"junk"]) == [0]
+    assert v.VerifySignatures([plugin.Signature(9, b"\0" * 64, b"x")]) == [plugin.EKEY]
+    # a syntactically valid request built by hand (no engine to sign one)
+    req = (b"SBR1" + (1).to_bytes(2, "little") + b"a" + (1).to_bytes(2, "little") + b"b" +
+           (0).to_bytes(4, "little") + b"\x04" + b"\1" * 64 + b"\2" * 64)
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyRequests([req])
+    assert ei.value.code == -2  # SBFT_GV_ENODEV

@@ -44,8 +44,8 @@ __global__ void kcheck(const u32* in, u32* out, int n) {
     // worst-case-ish bounds: (a - b) * 3(a + b) after one carry pass
     f29_sub(d, m, s);
     f29_add(e, m, s);
+    f29_normalize(e, e);
     f29_muls(e, e, 3);
-    f29_carry(e, e);
     f29_mul(d, d, e);
     for (int i = 0; i < 9; ++i) { out[27 * t + i] = m.v[i]; out[27 * t + 9 + i] = s.v[i]; out[27 * t + 18 + i] = d.v[i]; }
 }
