@@ -52,6 +52,27 @@ SBFT_DEV i64 smad(u32 a, u32 b, i64 acc) {
     return r;
 #endif
 }
+// acc >> 29 (arithmetic). SBFT_SHR_ASM pins it to one v_ashrrev_i64 so the compiler cannot
+// fold the shift into the next mad's addend (which costs register-pair moves).
+SBFT_DEV i64 sar29(i64 acc) {
+#ifdef SBFT_SHR_ASM
+    i64 r;
+    asm("v_ashrrev_i64 %0, 29, %1" : "=v"(r) : "v"(acc));
+    return r;
+#else
+    return acc >> 29;
+#endif
+}
+// low 29 bits of acc as a limb whose range the compiler cannot see: a limb it proves
+// non-negative turns a later sext(a) * sext(b) into a u64 mad plus a sign-correction mad and
+// register-pair moves. The asm sits on the freshly masked value (no copy needed).
+SBFT_DEV u32 lo29(i64 acc) {
+    u32 t = (u32)acc & F29_MASK;
+#ifndef SBFT_NO_OPAQUE_LIMBS
+    asm("" : "+v"(t));
+#endif
+    return t;
+}
 // The reduction multipliers 2^9, 2^18, 2^29 - 2^21, 2^24 - 1, held in SGPRs the compiler cannot
 // see through (otherwise m * 2^9 + acc becomes a 64-bit shift, mask and add: 3 instructions).
 struct f29_red {
@@ -80,9 +101,9 @@ SBFT_DEV void f29_mul(f29& r, const f29& a, const f29& b) {
         if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], K.c18, acc);
         if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], K.c7, acc);
         if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], K.c8, acc);
-        if (k < 9) m[k] = (u32)acc & F29_MASK;
-        else r.v[k - 9] = (u32)acc & F29_MASK;
-        acc >>= 29;
+        if (k < 9) m[k] = lo29(acc);
+        else r.v[k - 9] = lo29(acc);
+        acc = sar29(acc);
     }
     r.v[8] = (u32)acc;
 }
@@ -108,9 +129,9 @@ SBFT_DEV void f29_sqr(f29& r, const f29& a) {
         if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], K.c18, acc);
         if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], K.c7, acc);
         if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], K.c8, acc);
-        if (k < 9) m[k] = (u32)acc & F29_MASK;
-        else r.v[k - 9] = (u32)acc & F29_MASK;
-        acc >>= 29;
+        if (k < 9) m[k] = lo29(acc);
+        else r.v[k - 9] = lo29(acc);
+        acc = sar29(acc);
     }
     r.v[8] = (u32)acc;
 }
@@ -166,9 +187,9 @@ SBFT_DEV void f29_mulv(f29* const* r, const f29* const* a, const f29* const* b) 
         }
 #pragma unroll
         for (int x = 0; x < N; ++x) {
-            if (k < 9) m[x][k] = (u32)acc[x] & F29_MASK;
-            else o[x][k - 9] = (u32)acc[x] & F29_MASK;
-            acc[x] >>= 29;
+            if (k < 9) m[x][k] = lo29(acc[x]);
+            else o[x][k - 9] = lo29(acc[x]);
+            acc[x] = sar29(acc[x]);
         }
     }
 #pragma unroll

@@ -6,7 +6,7 @@ import sys
 
 def main(path, kernel, top=8):
     s = open(path).read()
-    i = s.index(kernel + ":")
+    i = s.index("\n" + kernel + ":")
     j = s.index("s_endpgm", i)
     body = s[i:j]
     parts = re.split(r"\n(\.LBB\d+_\d+):", body)
