@@ -1,4 +1,5 @@
-// p256_inv.hpp — variable-time modular inversion mod the P-256 group order n by batched
+// p256_inv.hpp — variable-time modular inversion mod the P-256 group order n (or the field
+// prime p: the verify kernel's affine Q table) by batched
 // divsteps (Bernstein–Yang "safegcd", 30 divsteps per batch on 32-bit words).
 //
 // Used where one inversion sits on a latency path: the keyed single-signature verify
@@ -59,6 +60,16 @@ struct s30 {
 // n in radix 2^30 and n^-1 mod 2^30
 #define SBFT_N30_INIT {0x3c632551, 0x0ee72b0b, 0x3179e84f, 0x39beab69, 0x3fffffbc, 0x3fffffff, 0x00000fff, 0x3fffc000, 0x0000ffff}
 #define SBFT_NINV30 0x11ff43b1u  // n^-1 mod 2^30 (so that d + md*n = 0 mod 2^30 for md = -d * NINV30)
+// the field prime p in radix 2^30; p = -1 mod 2^96, so p^-1 = -1 mod 2^30
+#define SBFT_P30_INIT {0x3fffffff, 0x3fffffff, 0x3fffffff, 0x0000003f, 0x00000000, 0x00000000, 0x00001000, 0x3fffc000, 0x0000ffff}
+#define SBFT_PINV30 0x3fffffffu
+
+// The modulus of an inversion: P = false for the group order n, true for the field prime p.
+template <bool P>
+SBFT_HD void mod30(int32_t m[9]) {
+    const int32_t N30[9] = SBFT_N30_INIT, P30[9] = SBFT_P30_INIT;
+    for (int i = 0; i < 9; ++i) m[i] = P ? P30[i] : N30[i];
+}
 
 SBFT_HD void pack30(s30& r, const uint32_t a[8]) {
     // 8 x 32-bit little-endian limbs -> 9 x 30-bit limbs (value < 2^256)
@@ -124,14 +135,18 @@ SBFT_HD void update_fg(s30& f, s30& g, int32_t u, int32_t v, int32_t q, int32_t 
     g.v[8] = (int32_t)cg;
 }
 
-// (d, e) <- (T (d, e) + (md, me) n) / 2^30 with md, me chosen to clear the low 30 bits.
-// |d|, |e| grow by at most n per batch (|u| + |v| <= 2^30), so 25 batches stay below 2^262.
+// (d, e) <- (T (d, e) + (md, me) m) / 2^30 with md, me chosen to clear the low 30 bits
+// (m = n, or p when P). |d|, |e| grow by at most m per batch (|u| + |v| <= 2^30), so 25
+// batches stay below 2^262.
+template <bool P>
 SBFT_HD void update_de(s30& d, s30& e, int32_t u, int32_t v, int32_t q, int32_t r) {
-    const int32_t N30[9] = SBFT_N30_INIT;
+    int32_t N30[9];
+    mod30<P>(N30);
+    const uint32_t minv = P ? SBFT_PINV30 : SBFT_NINV30;
     int64_t cd = mac(mac(0, u, d.v[0]), v, e.v[0]);
     int64_t ce = mac(mac(0, q, d.v[0]), r, e.v[0]);
-    const int32_t md = (int32_t)((0u - (uint32_t)cd * SBFT_NINV30) & SBFT_M30);
-    const int32_t me = (int32_t)((0u - (uint32_t)ce * SBFT_NINV30) & SBFT_M30);
+    const int32_t md = (int32_t)((0u - (uint32_t)cd * minv) & SBFT_M30);
+    const int32_t me = (int32_t)((0u - (uint32_t)ce * minv) & SBFT_M30);
     cd = mac(cd, md, N30[0]);
     ce = mac(ce, me, N30[0]);
     cd >>= 30;
@@ -154,9 +169,11 @@ SBFT_HD bool is_zero30(const s30& a) {
     return o == 0;
 }
 
-// a += k * n for a small signed k, renormalising limbs 0..7 to [0, 2^30)
+// a += k * m for a small signed k (m = n, or p when P), renormalising limbs 0..7 to [0, 2^30)
+template <bool P>
 SBFT_HD void add_kn(s30& a, int32_t k) {
-    const int32_t N30[9] = SBFT_N30_INIT;
+    int32_t N30[9];
+    mod30<P>(N30);
     int64_t c = 0;
     for (int i = 0; i < 8; ++i) {
         c += (int64_t)a.v[i] + (int64_t)k * N30[i];
@@ -166,13 +183,15 @@ SBFT_HD void add_kn(s30& a, int32_t k) {
     a.v[8] = (int32_t)(c + a.v[8] + (int64_t)k * N30[8]);
 }
 
-// a (normalised, |a| < 2^262) -> [0, n), then 8 x 32-bit limbs
+// a (normalised, |a| < 2^262) -> [0, m), then 8 x 32-bit limbs
+template <bool P>
 SBFT_HD void reduce_unpack(uint32_t out[8], s30 a) {
-    // a = t * 2^240 + low with t = a.v[8]; n = 2^256 - small, so k = -floor(a / 2^256) gets
-    // within a few n of [0, n)
-    add_kn(a, -(a.v[8] >> 16));
-    for (int it = 0; it < 4 && a.v[8] < 0; ++it) add_kn(a, 1);
-    const int32_t N30[9] = SBFT_N30_INIT;
+    // a = t * 2^240 + low with t = a.v[8]; m = 2^256 - c with c < 2^225 (n: c < 2^128), so
+    // k = -floor(a / 2^256) gets within a few m of [0, m)
+    add_kn<P>(a, -(a.v[8] >> 16));
+    for (int it = 0; it < 4 && a.v[8] < 0; ++it) add_kn<P>(a, 1);
+    int32_t N30[9];
+    mod30<P>(N30);
     for (int it = 0; it < 4; ++it) {
         // a >= n ?
         bool ge = true;
@@ -183,7 +202,7 @@ SBFT_HD void reduce_unpack(uint32_t out[8], s30 a) {
             }
         }
         if (!ge) break;
-        add_kn(a, -1);
+        add_kn<P>(a, -1);
     }
     for (int w = 0; w < 8; ++w) {
         const int bit = 32 * w, i = bit / 30, sh = bit % 30;
@@ -194,10 +213,12 @@ SBFT_HD void reduce_unpack(uint32_t out[8], s30 a) {
     }
 }
 
-// out = x^-1 mod n for 0 < x < n (8 x 32-bit little-endian limbs). x = 0 gives 0.
-// tab: SBFT_DIVSTEP5_TABLE (p256_inv_table.inc).
-SBFT_HD void inv_mod_n(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) {
-    s30 f = {SBFT_N30_INIT}, g, d, e;
+// out = x^-1 mod m for 0 < x < m (8 x 32-bit little-endian limbs; m = n, or p when P).
+// x = 0 gives 0. tab: SBFT_DIVSTEP5_TABLE (p256_inv_table.inc).
+template <bool P>
+SBFT_HD void inv_mod(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) {
+    s30 f, g, d, e;
+    mod30<P>(f.v);
     pack30(g, x);
     for (int i = 0; i < 9; ++i) {
         d.v[i] = 0;
@@ -209,16 +230,18 @@ SBFT_UNROLL1
     for (int batch = 0; batch < 26 && !is_zero30(g); ++batch) {
         int32_t u, v, q, r;
         delta = divsteps30(delta, (uint32_t)f.v[0], (uint32_t)g.v[0], tab, u, v, q, r);
-        update_de(d, e, u, v, q, r);
+        update_de<P>(d, e, u, v, q, r);
         update_fg(f, g, u, v, q, r);
     }
     // f = +-1: x^-1 = f * d
     if (f.v[8] < 0) {
         for (int i = 0; i < 9; ++i) d.v[i] = -d.v[i];
-        add_kn(d, 0);  // renormalise limbs
+        add_kn<P>(d, 0);  // renormalise limbs
     }
-    reduce_unpack(out, d);
+    reduce_unpack<P>(out, d);
 }
+SBFT_HD void inv_mod_n(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) { inv_mod<false>(out, x, tab); }
+SBFT_HD void inv_mod_p(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) { inv_mod<true>(out, x, tab); }
 
 #if defined(__HIPCC__)
 __device__ __constant__ static const uint32_t C_DIVSTEP5[SBFT_DIVSTEP5_WORDS] = SBFT_DIVSTEP5_TABLE;

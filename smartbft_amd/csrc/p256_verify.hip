@@ -7,8 +7,9 @@
 //   3. u1 = e*w, u2 = r*w
 //   4. R = u1*G + u2*Q: one shared doubling chain (Straus/Shamir) with regular signed-odd
 //      digits (never zero, so every addition is live and select-free): radix 16 for u2 over
-//      [1,3,..,15]Q built per lane (Jacobian, scratch), radix 256 for u1 over
-//      [1,3,..,255]G, an 8 KiB affine table staged in LDS (33 mixed additions)
+//      [1,3,..,15]Q built per lane and made affine with one safegcd inversion mod p
+//      (scratch; 64 mixed additions), radix 256 for u1 over [1,3,..,255]G, an affine table
+//      staged in LDS (33 mixed additions)
 //   5. R = infinity -> reject; accept iff X == r*Z^2 or (r+n < p and X == (r+n)*Z^2)
 // Exceptional additions (P + P, P + (-P), infinity) are branched per lane under a
 // wave-uniform guard, so adversarial inputs take the slow path only when present.
@@ -17,6 +18,7 @@
 #include <cstdio>
 
 #include "p256_f29.hpp"
+#include "p256_inv.hpp"
 #include "p256_point.hpp"
 #include "sbft_kernels.h"
 
@@ -336,8 +338,9 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
                                                           uint8_t* __restrict__ ok, uint32_t n,
                                                           uint32_t* __restrict__ work, sinv_ws ws) {
     __shared__ u32 gtab[P256_GODD8_F29_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     for (int i = threadIdx.x; i < P256_GODD8_F29_WORDS; i += blockDim.x) gtab[i] = C29_GODD8[i];
-    __syncthreads();
+    inv::stage_divstep_table(dtab);  // ends with a barrier
     const int tid = threadIdx.x;
 
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -374,7 +377,11 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
 
     // Q in the radix-2^29 Montgomery domain of the ladder (p256_f29.hpp). Invalid lanes run a
     // harmless stand-in (Q = 2G, u1 = u2 = 1); their verdict is masked by `valid` at the end.
-    jp29 tq[8];  // odd multiples [1,3,...,15]Q, Jacobian (scratch)
+    // The odd multiples [1,3,...,15]Q are built in Jacobian form (one doubling, seven lean
+    // additions), then made affine with ONE inversion per lane (Montgomery's trick over the
+    // seven Z's, safegcd mod p): every Q digit of the ladder is then a mixed addition
+    // (8M + 3S) instead of a Jacobian one (12M + 4S).
+    f29 tx[8], ty[8];  // affine odd multiples (scratch)
     {
         jp29 q;
         const f29 r2 = f29_const(C29_R2);
@@ -385,15 +392,42 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
             q.x = f29_const(C29_G2X);
             q.y = f29_const(C29_G2Y);
         }
-        tq[0] = q;
+        tx[0] = q.x;
+        ty[0] = q.y;
+        jp29 tj[8];
+        tj[0] = q;
         jp29 q2;
         p29_dbl(q2, q);
-        // (2k+1)Q == +-2Q is impossible for a point of prime order n: no exceptional case here
+        // (2k+1)Q == +-2Q is impossible for a point of prime order n: no exceptional case here,
+        // and no Z is 0
 #pragma unroll 1
         for (int k = 1; k < 8; ++k) {
-            jp29 t = tq[k - 1];
+            jp29 t = tj[k - 1];
             p29_add_jac_lean(t, q2);
-            tq[k] = t;
+            tj[k] = t;
+        }
+        f29 c[7];  // c[k] = Z_1 ... Z_{k+1}
+        c[0] = tj[1].z;
+#pragma unroll 1
+        for (int k = 1; k < 7; ++k) f29_mul(c[k], c[k - 1], tj[k + 1].z);
+        f29 inv;  // (Z_1 ... Z_7)^-1, Montgomery form
+        {
+            const fe cp = f29_canon_plain(c[6]);
+            fe ci;
+            inv::inv_mod_p(ci.v, cp.v, dtab);
+            f29_mul(inv, f29_from_u256(ci), r2);
+        }
+#pragma unroll 1
+        for (int k = 7; k >= 1; --k) {
+            f29 zi = inv, zi2, zi3;
+            if (k > 1) {
+                f29_mul(zi, inv, c[k - 2]);     // Z_k^-1
+                f29_mul(inv, inv, tj[k].z);     // (Z_1 ... Z_{k-1})^-1
+            }
+            f29_sqr(zi2, zi);
+            f29_mul(zi3, zi2, zi);
+            f29_mul(tx[k], tj[k].x, zi2);
+            f29_mul(ty[k], tj[k].y, zi3);      // Y may be N+- : 2^29 x 2^29
         }
     }
     // 3. w = s^-1 from the launch-wide Montgomery trick (see p256_sinv_* kernels)
@@ -439,7 +473,10 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     // u = sum_{i<64} d_i 16^i + 16^64 with d_i = 2*((u >> (4i+1)) & 15) - 15 (odd, nonzero);
     // likewise radix 256 for u1 over the [1,3,...,255]G table. The top digits are 1, so the
     // accumulator starts at Q + G, never at infinity.
-    jp29 acc = tq[0];  // reload from scratch: keeps q out of registers during the setup
+    jp29 acc;  // reloaded from scratch: keeps q out of registers during the setup
+    acc.x = tx[0];
+    acc.y = ty[0];
+    acc.z = f29_const(C29_ONE);
     if (neg2) f29_neg(acc.y, acc.y);
     {
         f29 gx, gy;
@@ -472,9 +509,11 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
             // Q digit (odd, in [-15, 15])
             {
                 const int d2 = 2 * (int)((u32)(f2 >> (4 * nib + 1)) & 15u) - 15;
-                jp29 t = tq[(d2 < 0 ? -d2 : d2) >> 1];
-                if ((d2 < 0) != neg2) f29_neg(t.y, t.y);
-                p29_add_jac_lean(acc, t);
+                const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
+                const f29 x2 = tx[m2];
+                f29 y2 = ty[m2];
+                if ((d2 < 0) != neg2) f29_neg(y2, y2);
+                p29_add_aff_lean(acc, x2, y2);
             }
             // G digit (odd, in [-255, 255]) on every other radix-16 window
             if ((nib & 1) == 0) {

@@ -1,5 +1,5 @@
 // CPU build of smartbft_amd/csrc/p256_inv.hpp (the device inversion) for tests/test_native.py:
-// reads hex x per line on stdin, prints hex x^-1 mod n.
+// reads hex x per line on stdin, prints hex x^-1 mod n (argument "p": mod the field prime).
 #include <cstdio>
 #include <cstring>
 
@@ -7,7 +7,8 @@
 
 static const uint32_t TAB[SBFT_DIVSTEP5_WORDS] = SBFT_DIVSTEP5_TABLE;
 
-int main() {
+int main(int argc, char** argv) {
+    const bool modp = argc > 1 && std::strcmp(argv[1], "p") == 0;
     char line[256];
     while (fgets(line, sizeof line, stdin)) {
         uint32_t x[8] = {0}, out[8];
@@ -19,7 +20,10 @@ int main() {
             sscanf(line + 8 * (7 - w), "%8x", &v);
             x[w] = v;
         }
-        sbft::inv::inv_mod_n(out, x, TAB);
+        if (modp)
+            sbft::inv::inv_mod_p(out, x, TAB);
+        else
+            sbft::inv::inv_mod_n(out, x, TAB);
         for (int w = 7; w >= 0; --w) printf("%08x", out[w]);
         printf("\n");
     }

@@ -1,6 +1,6 @@
 """CPU tests of header-only device algorithms compiled for the host with g++ (same source the
-HIP kernels include): the safegcd inversion mod n (smartbft_amd/csrc/p256_inv.hpp) against
-Python's pow(x, -1, n)."""
+HIP kernels include): the safegcd inversion mod n and mod p (smartbft_amd/csrc/p256_inv.hpp) against
+Python's pow(x, -1, m)."""
 import os
 import random
 import subprocess
@@ -10,6 +10,7 @@ import pytest
 from conftest import ROOT
 
 N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+P = 2**256 - 2**224 + 2**192 + 2**96 - 1
 
 
 @pytest.fixture(scope="module")
@@ -20,15 +21,18 @@ def inv_exe(tmp_path_factory):
     return exe
 
 
-def test_safegcd_inverse_matches_pow(inv_exe):
+@pytest.mark.parametrize("mod", ["n", "p"])
+def test_safegcd_inverse_matches_pow(inv_exe, mod):
+    M = N if mod == "n" else P
     rng = random.Random(1)
-    xs = [1, 2, 3, N - 1, N - 2, N // 2, N // 3, 1 << 255, (1 << 256) % N, (1 << 128) - 1, 0xFFFFFFFF]
+    xs = [1, 2, 3, M - 1, M - 2, M // 2, M // 3, 1 << 255, (1 << 256) % M, (1 << 128) - 1, 0xFFFFFFFF]
     xs += [1 << k for k in range(0, 256, 7)]
-    xs += [rng.randrange(1, N) for _ in range(20000)]
+    xs += [(1 << 256) - 1 - (1 << k) for k in range(0, 255, 13) if (1 << 256) - 1 - (1 << k) < M]
+    xs += [rng.randrange(1, M) for _ in range(20000)]
     # adversarial-ish: long runs of equal low bits (many divsteps with g even)
-    xs += [((1 << 200) * rng.randrange(1, 1 << 55)) % N or 1 for _ in range(200)]
-    out = subprocess.run([inv_exe], input="".join("%064x\n" % x for x in xs), capture_output=True,
+    xs += [((1 << 200) * rng.randrange(1, 1 << 55)) % M or 1 for _ in range(200)]
+    out = subprocess.run([inv_exe, mod], input="".join("%064x\n" % x for x in xs), capture_output=True,
                          text=True, check=True).stdout.split()
     assert len(out) == len(xs)
-    bad = [hex(x) for x, o in zip(xs, out) if int(o, 16) != pow(x, -1, N)]
+    bad = [hex(x) for x, o in zip(xs, out) if int(o, 16) != pow(x, -1, M)]
     assert not bad, bad[:4]
