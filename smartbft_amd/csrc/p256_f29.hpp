@@ -256,6 +256,13 @@ SBFT_DEV void f29_normalize(f29& r, const f29& a) {
     t.v[6] = (u32)((i32)t.v[6] + h * -(1 << 18));
     t.v[3] = (u32)((i32)t.v[3] + h * -(1 << 9));
     t.v[0] += (u32)h;
+#if !defined(SBFT_NO_OPAQUE_LIMBS) && !defined(SBFT_NO_OPAQUE_NORM)
+    // range-opaque like lo29: with the limbs' ranges visible (a masked word plus a small signed
+    // carry), ROCm 7.2's lowering of a later sext * sext product miscompiled two inlined
+    // back-to-back doublings (tests/test_gpu_field.py::test_f29_point_ops, unrolled loop)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) asm("" : "+v"(t.v[i]));
+#endif
     r = t;
 }
 

@@ -327,8 +327,12 @@ __global__ __launch_bounds__(256) void p256_sinv_totals_kernel(uint32_t nb, sinv
 }
 
 // ------------------------------------------------------------ the kernel
+#ifndef SBFT_DBL_UNROLL
+#define SBFT_DBL_UNROLL 1
+#endif
+constexpr int kDblUnroll = SBFT_DBL_UNROLL;  // doublings per iteration of the 4-doubling loop
 #ifndef SBFT_VERIFY_WAVES
-#define SBFT_VERIFY_WAVES 3
+#define SBFT_VERIFY_WAVES 4
 #endif
 __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(const uint8_t* __restrict__ digest,
                                                           const uint8_t* __restrict__ rr,
@@ -504,7 +508,7 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
         above2 = cur2;
 #pragma unroll 1
         for (int nib = 7; nib >= 0; --nib) {
-#pragma unroll 1
+#pragma unroll kDblUnroll
             for (int d = 0; d < 4; ++d) p29_dbl(acc, acc);
             // Q digit (odd, in [-15, 15])
             {

@@ -76,3 +76,58 @@ def test_canonical_forms(gpu):
     assert _run(gpu, 8, pairs) == [a % N for a, _ in pairs]
     small = [(a % N, b % N) for a, b in pairs]
     assert _run(gpu, 9, small) == [(a + b) % N for a, b in small]
+
+
+# ---- radix-2^29 ladder layer (p256_f29.hpp): ops 11..19 ------------------------------------
+B = 0x5AC635D8AA3A93E7B3EBBD55769886BC651D06B0CC53B0F63BCE3C3E27D2604B
+GX = 0x6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296
+GY = 0x4FE342E2FE1A7F9B8EE7EB4A7C0F9E162BCE33576B315ECECBB6406837BF51F5
+
+
+def _add(p1, p2):
+    if p1 is None:
+        return p2
+    (x1, y1), (x2, y2) = p1, p2
+    if x1 == x2:
+        if (y1 + y2) % P == 0:
+            return None
+        lam = (3 * x1 * x1 - 3) * pow(2 * y1, -1, P) % P
+    else:
+        lam = (y2 - y1) * pow(x2 - x1, -1, P) % P
+    x3 = (lam * lam - x1 - x2) % P
+    return x3, (lam * (x1 - x3) - y1) % P
+
+
+def _mul(k, pt):
+    acc = None
+    for bit in bin(k)[2:]:
+        acc = _add(acc, acc) if acc else None
+        if bit == "1":
+            acc = _add(acc, pt)
+    return acc
+
+
+def test_f29_mul_sqr_inv(gpu):
+    """f29_mul / f29_sqr (Montgomery, R = 2^261) and the safegcd inversion mod p."""
+    pairs = [(a % P, b % P) for a, b in _inputs(n_rand=3000, seed=11)]
+    _check(pairs, _run(gpu, 11, pairs), lambda a, b: a * b, P, "f29_mul")
+    _check(pairs, _run(gpu, 12, pairs), lambda a, b: a * a, P, "f29_sqr")
+    xs = [(x, 0) for x, _ in pairs if x % P]
+    got = _run(gpu, 13, xs)
+    bad = [hex(x) for (x, _), g in zip(xs, got) if g != pow(x, -1, P)]
+    assert not bad, bad[:3]
+
+
+def test_f29_point_ops(gpu):
+    """The ladder's lean doubling / mixed / Jacobian additions on random curve points, with the
+    doubling loop both rolled and unrolled (same source the verify kernel inlines)."""
+    rng = random.Random(5)
+    pts = [(GX, GY)] + [_mul(rng.randrange(1, N), (GX, GY)) for _ in range(60)]
+    pts += [_mul(k, (GX, GY)) for k in (2, 3, N - 1, N - 2, (N + 1) // 2)]
+    x32 = [_mul(32, p) for p in pts]
+    assert _run(gpu, 14, pts) == [q[0] for q in x32], "x(32P), rolled doubling loop"
+    assert _run(gpu, 15, pts) == [q[0] for q in x32], "x(32P), unrolled doubling loop"
+    assert _run(gpu, 16, pts) == [q[1] for q in x32], "y(32P)"
+    assert _run(gpu, 17, pts) == [_mul(3, p)[0] for p in pts], "x(2P + P), mixed addition"
+    assert _run(gpu, 18, pts) == [_mul(6, p)[1] for p in pts], "y(4P + 2P), Jacobian addition"
+    assert _run(gpu, 19, pts) == [_mul(3, p)[1] for p in pts], "y(2P + P), negated twice"
