@@ -281,6 +281,8 @@ __global__ __launch_bounds__(256) void p256_sinv_totals_kernel(uint32_t nb, sinv
     __shared__ u32 buf[8][256];
     __shared__ u32 pre_c[8][256];
     __shared__ u32 ginv[8];
+    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    inv::stage_divstep_table(dtab);  // ends with a barrier
     const int tid = threadIdx.x;
     const uint32_t chunk = (nb + 255) / 256;
     const uint32_t b0 = tid * chunk, b1 = min(nb, b0 + chunk);
@@ -294,10 +296,17 @@ __global__ __launch_bounds__(256) void p256_sinv_totals_kernel(uint32_t nb, sinv
     block_scan_mul_n(cp, pre_c, tid, false);  // inclusive prefix of chunk products
     block_scan_mul_n(cs, buf, tid, true);     // inclusive suffix
     if (tid < 64) {
-        fe g, gi;
+        // G^-1 in Montgomery form: the safegcd inverse of G's Montgomery representative M
+        // is M^-1 = g^-1 R^-1, and two multiplications by R^2 (mod n) give g^-1 R. One
+        // wavefront, ~0.03 ms (a Fermat chain here was ~0.3 ms of dependent multiplications).
+        fe g, gi, m, mi;
 #pragma unroll
         for (int k = 0; k < 8; ++k) g.v[k] = pre_c[k][255];
-        fn_inv(gi, g);
+        fn_canon(m, g);
+        inv::inv_mod_n(mi.v, m.v, dtab);
+        const fe r2n = fe_const(C_R2N);
+        fn_mul(gi, mi, r2n);
+        fn_mul(gi, gi, r2n);
         if (tid == 0)
 #pragma unroll
             for (int k = 0; k < 8; ++k) ginv[k] = gi.v[k];
