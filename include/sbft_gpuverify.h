@@ -134,6 +134,13 @@ int sbft_gv_sha256_verify_p256_keyed(sbft_gv_ctx* ctx, const uint8_t* blob, size
                                      const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint32_t* key_id,
                                      size_t n, uint8_t* ok_out);
 
+/* Kernel timing (measurement): while enabled, every device-resident verify records HIP
+ * events on the caller's stream around its main p256_verify_kernel launch (not the s^-1
+ * batching or fixup kernels). sbft_gv_kernel_time waits for the recorded events and returns
+ * (then forgets) the number of timed launches and their summed duration in milliseconds. */
+int sbft_gv_kernel_timing(sbft_gv_ctx* ctx, int enable);
+int sbft_gv_kernel_time(sbft_gv_ctx* ctx, uint64_t* launches, double* ms);
+
 /* Element-wise self-test of the device primitives (diagnostics; op codes in
  * smartbft_amd/csrc/p256_selftest.hip). a, b, out: n x 32 bytes big-endian. */
 int sbft_gv_selftest_field(sbft_gv_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, size_t n,

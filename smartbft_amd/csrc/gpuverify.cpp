@@ -98,6 +98,11 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 }  // namespace
 
 struct sbft_gv_ctx {
+    // kernel timing (sbft_gv_kernel_timing): event pairs around each device-resident verify's
+    // main kernel, read and released by sbft_gv_kernel_time
+    std::atomic<bool> timing{false};
+    std::mutex ev_mu;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     std::vector<Slot*> slots;
     uint32_t min_split = 65536;
     std::atomic<uint32_t> rr{0};
@@ -160,6 +165,9 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
 
 void sbft_gv_destroy(sbft_gv_ctx* ctx) {
     if (!ctx) return;
+    uint64_t nl;
+    double ms;
+    (void)sbft_gv_kernel_time(ctx, &nl, &ms);  // releases pending timing events
     for (Slot* s : ctx->slots) {
         (void)hipSetDevice(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
@@ -180,6 +188,37 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
 }
 
 size_t sbft_gv_verify_workspace_bytes(size_t n) { return sbft_verify_work_bytes(n); }
+
+int sbft_gv_kernel_timing(sbft_gv_ctx* ctx, int enable) {
+    if (!ctx) return SBFT_GV_EINVAL;
+    ctx->timing = enable != 0;
+    return SBFT_GV_OK;
+}
+
+int sbft_gv_kernel_time(sbft_gv_ctx* ctx, uint64_t* launches, double* ms) {
+    if (!ctx || !launches || !ms) return SBFT_GV_EINVAL;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+    {
+        std::lock_guard<std::mutex> g(ctx->ev_mu);
+        evs.swap(ctx->events);
+    }
+    *launches = 0;
+    *ms = 0.0;
+    int rc = SBFT_GV_OK;
+    for (auto& e : evs) {
+        float t = 0.f;
+        if (rc == SBFT_GV_OK &&
+            (hipEventSynchronize(e.second) != hipSuccess || hipEventElapsedTime(&t, e.first, e.second) != hipSuccess))
+            rc = SBFT_GV_EDEVICE;
+        if (rc == SBFT_GV_OK) {
+            *ms += t;
+            ++*launches;
+        }
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    return rc;
+}
 
 int sbft_gv_device_count(const sbft_gv_ctx* ctx) { return ctx ? (int)ctx->slots.size() : 0; }
 
@@ -220,9 +259,19 @@ int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, 
     if (hipSetDevice(device) != hipSuccess) return SBFT_GV_EDEVICE;
     uint32_t* work = sl->stream_workspace((hipStream_t)stream, sbft_verify_work_bytes(n));
     if (!work) return SBFT_GV_ENOMEM;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (ctx->timing.load()) {
+        if (hipEventCreate(&ev0) != hipSuccess) return SBFT_GV_EDEVICE;
+        if (hipEventCreate(&ev1) != hipSuccess) {
+            (void)hipEventDestroy(ev0);
+            return SBFT_GV_EDEVICE;
+        }
+        std::lock_guard<std::mutex> g(ctx->ev_mu);
+        ctx->events.emplace_back(ev0, ev1);
+    }
     return sbft_launch_p256_verify((const uint8_t*)d_digest, (const uint8_t*)d_r, (const uint8_t*)d_s,
                                    (const uint8_t*)d_qx, (const uint8_t*)d_qy, (uint8_t*)d_ok,
-                                   (uint32_t)n, work, (hipStream_t)stream)
+                                   (uint32_t)n, work, (hipStream_t)stream, ev0, ev1)
                ? SBFT_GV_ELAUNCH
                : SBFT_GV_OK;
 }

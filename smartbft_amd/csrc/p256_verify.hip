@@ -591,7 +591,8 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
 // device, so the whole sequence stays asynchronous.
 extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                        const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
-                                       uint32_t n, uint32_t* d_work, hipStream_t stream) {
+                                       uint32_t n, uint32_t* d_work, hipStream_t stream, hipEvent_t ev0,
+                                       hipEvent_t ev1) {
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned blocks = (n + threads - 1) / threads;
@@ -620,8 +621,10 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
     SBFT_STEP("prep");
     hipLaunchKernelGGL(sbft::p256_sinv_totals_kernel, dim3(1), dim3(threads), 0, stream, (uint32_t)blocks, ws);
     SBFT_STEP("totals");
+    if (ev0 && hipEventRecord(ev0, stream) != hipSuccess) return -1;
     hipLaunchKernelGGL(sbft::p256_verify_kernel, dim3(blocks), dim3(threads), 0, stream, d_digest, d_r,
                        d_s, d_qx, d_qy, d_ok, n, d_work, ws);
+    if (ev1 && hipEventRecord(ev1, stream) != hipSuccess) return -1;
     SBFT_STEP("verify");
     const unsigned fix_blocks = blocks < 64 ? blocks : 64;
     hipLaunchKernelGGL(sbft::p256_verify_fixup_kernel, dim3(fix_blocks), dim3(threads), 0, stream,

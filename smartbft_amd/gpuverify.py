@@ -21,6 +21,7 @@ EXPORTS = [
     "sbft_gv_normalize_hash", "sbft_gv_normalize_scalar", "sbft_gv_sign_p256", "sbft_gv_sign_p256_dev",
     "sbft_gv_selftest_field", "sbft_gv_verify_workspace_bytes",
     "sbft_gv_register_key", "sbft_gv_verify_p256_keyed", "sbft_gv_sha256_verify_p256_keyed",
+    "sbft_gv_kernel_timing", "sbft_gv_kernel_time",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -70,6 +71,8 @@ def load_library():
     L.sbft_gv_verify_workspace_bytes.argtypes = [ctypes.c_size_t]
     L.sbft_gv_verify_workspace_bytes.restype = ctypes.c_size_t
     L.sbft_gv_selftest_field.argtypes = [_vp, ctypes.c_int, _u8p, _u8p, ctypes.c_size_t, _u8p]
+    L.sbft_gv_kernel_timing.argtypes = [_vp, ctypes.c_int]
+    L.sbft_gv_kernel_time.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]
     L.sbft_gv_normalize_hash.argtypes = [_u8p, ctypes.c_size_t, _u8p]
     L.sbft_gv_normalize_hash.restype = None
     L.sbft_gv_normalize_scalar.argtypes = [_u8p, ctypes.c_size_t, _u8p]
@@ -248,6 +251,16 @@ class GpuVerifier:
         self._check(self.L.sbft_gv_verify_p256_dev(
             self.ctx, dev, d_digest.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), d_qx.data_ptr(),
             d_qy.data_ptr(), n, d_ok.data_ptr(), self._stream(stream)), "sbft_gv_verify_p256_dev")
+
+    def kernel_timing(self, enable: bool):
+        """Record HIP events around each device-resident verify's main kernel."""
+        self._check(self.L.sbft_gv_kernel_timing(self.ctx, int(enable)), "sbft_gv_kernel_timing")
+
+    def kernel_time(self) -> tuple[int, float]:
+        """(timed launches, summed milliseconds) since the last read."""
+        n, ms = ctypes.c_uint64(), ctypes.c_double()
+        self._check(self.L.sbft_gv_kernel_time(self.ctx, ctypes.byref(n), ctypes.byref(ms)), "sbft_gv_kernel_time")
+        return n.value, ms.value
 
     def sha256_dev(self, d_blob, d_off, d_len, d_dig, stream=None, d_order=None):
         n = d_off.numel()
