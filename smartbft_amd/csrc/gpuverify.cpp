@@ -66,6 +66,32 @@ struct Slot {
     // pinned host staging for the small-batch (latency) path: one H2D and one D2H per call
     uint8_t* pin = nullptr;
     size_t pin_cap = 0;
+    // fixed-base comb table for u1*G of the generic verify (p256_verify.hip), built on first use
+    std::mutex gcomb_mu;
+    void* gcomb = nullptr;
+    bool gcomb_ready = false;
+
+    // The comb table, building it (synchronously, on this slot's stream) the first time.
+    // Returns nullptr on failure; a table size of 0 (kernel built without the comb) returns a
+    // dummy non-null pointer that is never read.
+    const void* gcomb_table() {
+        std::lock_guard<std::mutex> g(gcomb_mu);
+        if (gcomb_ready) return gcomb;
+        const size_t bytes = sbft_gcomb_table_bytes();
+        if (bytes == 0) {
+            gcomb_ready = true;
+            gcomb = (void*)this;
+            return gcomb;
+        }
+        if (hipSetDevice(device) != hipSuccess) return nullptr;
+        if (!gcomb && hipMalloc(&gcomb, bytes) != hipSuccess) {
+            gcomb = nullptr;
+            return nullptr;
+        }
+        if (sbft_launch_gcomb_build(gcomb, stream) || hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+        gcomb_ready = true;
+        return gcomb;
+    }
 
     int reserve_pinned(size_t bytes) {
         if (bytes <= pin_cap) return SBFT_GV_OK;
@@ -177,6 +203,7 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
         if (s->d_keytab) (void)hipFree(s->d_keytab);
         for (void* t : s->retired) (void)hipFree(t);
         if (s->pin) (void)hipHostFree(s->pin);
+        if (s->gcomb && sbft_gcomb_table_bytes()) (void)hipFree(s->gcomb);
         for (auto& kv : s->ws) {
             (void)hipStreamSynchronize(kv.first);
             if (kv.second.ptr) (void)hipFree(kv.second.ptr);
@@ -257,6 +284,8 @@ int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, 
     if (!sl) return SBFT_GV_ENODEV;
     if (n == 0) return SBFT_GV_OK;
     if (hipSetDevice(device) != hipSuccess) return SBFT_GV_EDEVICE;
+    const void* gcomb = sl->gcomb_table();
+    if (!gcomb) return SBFT_GV_ENOMEM;
     uint32_t* work = sl->stream_workspace((hipStream_t)stream, sbft_verify_work_bytes(n));
     if (!work) return SBFT_GV_ENOMEM;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -271,7 +300,7 @@ int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, 
     }
     return sbft_launch_p256_verify((const uint8_t*)d_digest, (const uint8_t*)d_r, (const uint8_t*)d_s,
                                    (const uint8_t*)d_qx, (const uint8_t*)d_qy, (uint8_t*)d_ok,
-                                   (uint32_t)n, work, (hipStream_t)stream, ev0, ev1)
+                                   (uint32_t)n, work, gcomb, (hipStream_t)stream, ev0, ev1)
                ? SBFT_GV_ELAUNCH
                : SBFT_GV_OK;
 }
@@ -359,6 +388,8 @@ int enqueue_verify(const Chunk& c, const uint8_t* digest, const uint8_t* r, cons
     const size_t fo = align_up(c.count, 256);
     int rc = sl->reserve(5 * f + fo + sbft_verify_work_bytes(c.count));
     if (rc) return rc;
+    const void* gcomb = sl->gcomb_table();
+    if (!gcomb) return SBFT_GV_ENOMEM;
     uint8_t* base = sl->dbuf;
     uint32_t* work = (uint32_t*)(base + 5 * f + fo);
     const uint8_t* src[5] = {digest, r, s, qx, qy};
@@ -366,7 +397,7 @@ int enqueue_verify(const Chunk& c, const uint8_t* digest, const uint8_t* r, cons
         HIPCHK(hipMemcpyAsync(base + k * f, src[k] + 32 * c.begin, 32 * c.count, hipMemcpyHostToDevice,
                               sl->stream));
     if (sbft_launch_p256_verify(base, base + f, base + 2 * f, base + 3 * f, base + 4 * f, base + 5 * f,
-                                (uint32_t)c.count, work, sl->stream))
+                                (uint32_t)c.count, work, gcomb, sl->stream))
         return SBFT_GV_ELAUNCH;
     HIPCHK(hipMemcpyAsync(ok_out + c.begin, base + 5 * f, c.count, hipMemcpyDeviceToHost, sl->stream));
     return SBFT_GV_OK;
@@ -415,8 +446,10 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
                                   sl->stream));
         uint8_t* d_ok = v + 4 * fd;
         uint32_t* work = (uint32_t*)(d_ok + align_up(c.count, 256));
+        const void* gcomb = sl->gcomb_table();
+        if (!gcomb) return SBFT_GV_ENOMEM;
         if (sbft_launch_p256_verify(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_ok, (uint32_t)c.count,
-                                    work, sl->stream))
+                                    work, gcomb, sl->stream))
             return SBFT_GV_ELAUNCH;
         HIPCHK(hipMemcpyAsync(ok_out + c.begin, d_ok, c.count, hipMemcpyDeviceToHost, sl->stream));
     }

@@ -335,13 +335,89 @@ __global__ __launch_bounds__(256) void p256_sinv_totals_kernel(uint32_t nb, sinv
     }
 }
 
+// ------------------------------------------------------------ fixed-base comb for u1*G
+// SBFT_G_COMB = 1: u1*G is summed from a 16-window comb table in HBM after the Q ladder
+// (17 mixed additions, no doublings) instead of 33 radix-256 additions inside it.
+#ifndef SBFT_G_COMB
+#define SBFT_G_COMB 1
+#endif
+#define SBFT_GCOMB_WINDOWS 16
+#define SBFT_GCOMB_ENTRIES 32768  // odd digits 1, 3, ..., 65535
+// entry = 20 words (80 B, five 16-B loads): x limbs 0..8, pad, y limbs 0..8, pad (f29 Montgomery)
+#define SBFT_GCOMB_BYTES ((size_t)(SBFT_GCOMB_WINDOWS * SBFT_GCOMB_ENTRIES + 1) * 80)
+
+// affine (x, y) of P as canonical plain integers (8 x 32 domain; one Fermat inversion)
+SBFT_DEV void comb_affine(fe& x, fe& y, const jp& p) {
+    fe zi, zi2, zi3, t;
+    fp_inv(zi, p.z);
+    fp_sqr(zi2, zi);
+    fp_mul(zi3, zi2, zi);
+    const fe one_plain = {{1, 0, 0, 0, 0, 0, 0, 0}};
+    fp_mul(t, p.x, zi2);
+    fp_mul(t, t, one_plain);
+    fp_canon(x, t);
+    fp_mul(t, p.y, zi3);
+    fp_mul(t, t, one_plain);
+    fp_canon(y, t);
+}
+
+// table[w][j] = (2j+1) 2^(16 w) G for w < 16, j < 32768; table[16][0] = 2^256 G. One point
+// per thread through the (case-split) fixed-base multiplication of the signer; built once per
+// device (~42 MB of the 288 GB).
+__global__ __launch_bounds__(256) void p256_gcomb_build_kernel(uint4* __restrict__ table) {
+    __shared__ u32 gtab4[2 * 8 * P256_GTAB4_ENTRIES];
+    for (int i = threadIdx.x; i < 2 * 8 * P256_GTAB4_ENTRIES; i += blockDim.x) gtab4[i] = C_GTAB[i];
+    __syncthreads();
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t total = SBFT_GCOMB_WINDOWS * SBFT_GCOMB_ENTRIES + 1;
+    if (gid >= total) return;
+    fe d = fe_zero();
+    if (gid < SBFT_GCOMB_WINDOWS * SBFT_GCOMB_ENTRIES) {
+        const uint32_t w = gid / SBFT_GCOMB_ENTRIES, j = gid % SBFT_GCOMB_ENTRIES;
+        const uint32_t odd = 2 * j + 1, bit = 16 * w;
+        d.v[bit >> 5] = odd << (bit & 31);  // 16 w is 0 or 16 mod 32: no spill into the next limb
+        if (!fe_lt(d, P256_N)) {           // < 2^256 < 2n: one subtraction
+            u64 b = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const u64 t = (u64)d.v[k] - P256_N[k] - b;
+                d.v[k] = lo32(t);
+                b = t >> 63;
+            }
+        }
+    } else {  // 2^256 mod n = 2^256 - n
+        u64 b = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const u64 t = (u64)0 - P256_N[k] - b;
+            d.v[k] = lo32(t);
+            b = t >> 63;
+        }
+    }
+    jp P;
+    bool inf;
+    pt_mul_base(P, inf, d, gtab4);
+    fe x, y;
+    comb_affine(x, y, P);
+    const f29 r2 = f29_const(C29_R2);
+    f29 mx, my;
+    f29_mul(mx, f29_from_u256(x), r2);
+    f29_mul(my, f29_from_u256(y), r2);
+    uint4* e = table + (size_t)gid * 5;
+    e[0] = make_uint4(mx.v[0], mx.v[1], mx.v[2], mx.v[3]);
+    e[1] = make_uint4(mx.v[4], mx.v[5], mx.v[6], mx.v[7]);
+    e[2] = make_uint4(mx.v[8], 0u, my.v[0], my.v[1]);
+    e[3] = make_uint4(my.v[2], my.v[3], my.v[4], my.v[5]);
+    e[4] = make_uint4(my.v[6], my.v[7], my.v[8], 0u);
+}
+
 // ------------------------------------------------------------ the kernel
 #ifndef SBFT_DBL_UNROLL
 #define SBFT_DBL_UNROLL 1
 #endif
 constexpr int kDblUnroll = SBFT_DBL_UNROLL;  // doublings per iteration of the 4-doubling loop
 #ifndef SBFT_VERIFY_WAVES
-#define SBFT_VERIFY_WAVES 4
+#define SBFT_VERIFY_WAVES 2
 #endif
 __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(const uint8_t* __restrict__ digest,
                                                           const uint8_t* __restrict__ rr,
@@ -349,10 +425,13 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
                                                           const uint8_t* __restrict__ qxx,
                                                           const uint8_t* __restrict__ qyy,
                                                           uint8_t* __restrict__ ok, uint32_t n,
-                                                          uint32_t* __restrict__ work, sinv_ws ws) {
+                                                          uint32_t* __restrict__ work, sinv_ws ws,
+                                                          const uint4* __restrict__ gcomb) {
+#if !SBFT_G_COMB
     __shared__ u32 gtab[P256_GODD8_F29_WORDS];
-    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     for (int i = threadIdx.x; i < P256_GODD8_F29_WORDS; i += blockDim.x) gtab[i] = C29_GODD8[i];
+#endif
+    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     inv::stage_divstep_table(dtab);  // ends with a barrier
     const int tid = threadIdx.x;
 
@@ -483,14 +562,15 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
         fe_sel(u1, neg1, t1);
         fe_sel(u2, neg2, t2);
     }
-    // u = sum_{i<64} d_i 16^i + 16^64 with d_i = 2*((u >> (4i+1)) & 15) - 15 (odd, nonzero);
-    // likewise radix 256 for u1 over the [1,3,...,255]G table. The top digits are 1, so the
-    // accumulator starts at Q + G, never at infinity.
+    // u = sum_{i<64} d_i 16^i + 16^64 with d_i = 2*((u >> (4i+1)) & 15) - 15 (odd, nonzero).
+    // The top digit is 1, so the accumulator starts at +-Q, never at infinity.
     jp29 acc;  // reloaded from scratch: keeps q out of registers during the setup
     acc.x = tx[0];
     acc.y = ty[0];
     acc.z = f29_const(C29_ONE);
     if (neg2) f29_neg(acc.y, acc.y);
+#if !SBFT_G_COMB
+    // radix 256 for u1 over the LDS table [1,3,...,255]G, on every other radix-16 window
     {
         f29 gx, gy;
 #pragma unroll
@@ -501,20 +581,25 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
         if (neg1) f29_neg(gy, gy);
         p29_add_aff_lean(acc, gx, gy);
     }
-    fe k1 = u1, k2 = u2;
-    u32 above1 = 0, above2 = 0;
+    fe k1 = u1;
+    u32 above1 = 0;
+#endif
+    fe k2 = u2;
+    u32 above2 = 0;
 #pragma unroll 1
     for (int limb = 7; limb >= 0; --limb) {
-        const u32 cur1 = k1.v[7], cur2 = k2.v[7];
+        const u32 cur2 = k2.v[7];
 #pragma unroll
-        for (int k = 7; k > 0; --k) {
-            k1.v[k] = k1.v[k - 1];
-            k2.v[k] = k2.v[k - 1];
-        }
-        const u64 f1 = ((u64)above1 << 32) | cur1;
+        for (int k = 7; k > 0; --k) k2.v[k] = k2.v[k - 1];
         const u64 f2 = ((u64)above2 << 32) | cur2;
-        above1 = cur1;
         above2 = cur2;
+#if !SBFT_G_COMB
+        const u32 cur1 = k1.v[7];
+#pragma unroll
+        for (int k = 7; k > 0; --k) k1.v[k] = k1.v[k - 1];
+        const u64 f1 = ((u64)above1 << 32) | cur1;
+        above1 = cur1;
+#endif
 #pragma unroll 1
         for (int nib = 7; nib >= 0; --nib) {
 #pragma unroll kDblUnroll
@@ -528,6 +613,7 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
                 if ((d2 < 0) != neg2) f29_neg(y2, y2);
                 p29_add_aff_lean(acc, x2, y2);
             }
+#if !SBFT_G_COMB
             // G digit (odd, in [-255, 255]) on every other radix-16 window
             if ((nib & 1) == 0) {
                 const int d1 = 2 * (int)((u32)(f1 >> (4 * nib + 1)) & 255u) - 255;
@@ -541,8 +627,61 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
                 if ((d1 < 0) != neg1) f29_neg(gy, gy);
                 p29_add_aff_lean(acc, gx, gy);
             }
+#endif
         }
     }
+#if SBFT_G_COMB
+    // u1*G by the fixed-base comb in HBM (no doublings): u1 = sum_{i<16} d_i 2^(16 i) + 2^256
+    // with d_i = 2*((u1 >> (16 i + 1)) & 0xFFFF) - 0xFFFF (odd, nonzero), i.e. 16 mixed
+    // additions of table[i][(|d_i| - 1) / 2] = |d_i| 2^(16 i) G plus one of table[16][0] = 2^256 G.
+    // The next entry's five 16-B loads are issued before the current addition.
+    {
+        fe k1 = u1;
+        uint4 cur[5], nxt[5];
+        int dneg_cur = 0, dneg_nxt = 0;
+        // digit i of u1 -> (entry pointer, negative?)
+        auto digit = [&](int i, const uint4*& ptr, int& neg) {
+            if (i < 16) {
+                const u32 bits = (k1.v[0] >> 1) & 0xFFFFu;  // bits 16i+1 .. 16i+16 (k1 shifted)
+                const int d = 2 * (int)bits - 0xFFFF;
+                const u32 j = (u32)((d < 0 ? -d : d) >> 1);
+                ptr = gcomb + ((size_t)i * SBFT_GCOMB_ENTRIES + j) * 5;
+                neg = d < 0;
+                // k1 >>= 16 for the next window
+#pragma unroll
+                for (int k = 0; k < 7; ++k) k1.v[k] = __builtin_amdgcn_alignbit(k1.v[k + 1], k1.v[k], 16);
+                k1.v[7] >>= 16;
+            } else {
+                ptr = gcomb + (size_t)16 * SBFT_GCOMB_ENTRIES * 5;
+                neg = 0;
+            }
+        };
+        const uint4* ptr;
+        digit(0, ptr, dneg_nxt);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
+#pragma unroll 1
+        for (int i = 0; i < 17; ++i) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) cur[k] = nxt[k];
+            dneg_cur = dneg_nxt;
+            if (i < 16) {
+                digit(i + 1, ptr, dneg_nxt);
+#pragma unroll
+                for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
+            }
+            f29 gx, gy;
+            const u32* w = reinterpret_cast<const u32*>(cur);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                gx.v[k] = w[k];
+                gy.v[k] = w[10 + k];
+            }
+            if ((dneg_cur != 0) != neg1) f29_neg(gy, gy);
+            p29_add_aff_lean(acc, gx, gy);
+        }
+    }
+#endif
 
     // 5. The lean additions leave Z = 0 from the first exceptional case on (P + P, P + (-P),
     // R = infinity), so Z == 0 (mod p) flags the tuple for the general path. Otherwise
@@ -591,8 +730,8 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
 // device, so the whole sequence stays asynchronous.
 extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                        const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
-                                       uint32_t n, uint32_t* d_work, hipStream_t stream, hipEvent_t ev0,
-                                       hipEvent_t ev1) {
+                                       uint32_t n, uint32_t* d_work, const void* d_gcomb, hipStream_t stream,
+                                       hipEvent_t ev0, hipEvent_t ev1) {
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned blocks = (n + threads - 1) / threads;
@@ -623,7 +762,7 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
     SBFT_STEP("totals");
     if (ev0 && hipEventRecord(ev0, stream) != hipSuccess) return -1;
     hipLaunchKernelGGL(sbft::p256_verify_kernel, dim3(blocks), dim3(threads), 0, stream, d_digest, d_r,
-                       d_s, d_qx, d_qy, d_ok, n, d_work, ws);
+                       d_s, d_qx, d_qy, d_ok, n, d_work, ws, (const uint4*)d_gcomb);
     if (ev1 && hipEventRecord(ev1, stream) != hipSuccess) return -1;
     SBFT_STEP("verify");
     const unsigned fix_blocks = blocks < 64 ? blocks : 64;
@@ -631,4 +770,19 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
                        d_digest, d_r, d_s, d_qx, d_qy, d_ok, (const uint32_t*)d_work);
     SBFT_STEP("fixup");
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" size_t sbft_gcomb_table_bytes(void) { return SBFT_G_COMB ? SBFT_GCOMB_BYTES : 0; }
+
+extern "C" int sbft_launch_gcomb_build(void* d_table, hipStream_t stream) {
+#if SBFT_G_COMB
+    const unsigned total = SBFT_GCOMB_WINDOWS * SBFT_GCOMB_ENTRIES + 1;
+    hipLaunchKernelGGL(sbft::p256_gcomb_build_kernel, dim3((total + 255) / 256), dim3(256), 0, stream,
+                       (uint4*)d_table);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+#else
+    (void)d_table;
+    (void)stream;
+    return 0;
+#endif
 }

@@ -6,7 +6,9 @@ import sys
 
 def main(path, kernel, top=8):
     s = open(path).read()
-    i = s.index("\n" + kernel + ":")
+    import re as _re
+    m = _re.search(r"\n(" + _re.escape(kernel) + r"\w*):", s)  # kernel = a mangled-name prefix
+    i = m.start()
     j = s.index("s_endpgm", i)
     body = s[i:j]
     parts = re.split(r"\n(\.LBB\d+_\d+):", body)

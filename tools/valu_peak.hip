@@ -70,6 +70,59 @@ __global__ __launch_bounds__(256) void k_add3(uint32_t* out, uint32_t seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// 64-bit arithmetic shift (the radix-2^29 carry step): 8 independent chains
+template <int ITERS>
+__global__ __launch_bounds__(256) void k_ashr64(uint64_t* out, uint32_t seed) {
+    int64_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = ((int64_t)(seed ^ threadIdx.x) << 40) * (j + 1);
+    for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("v_ashrrev_i64 %0, 1, %0" : "+v"(x[j]));
+    }
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s ^= x[j];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// signed 32x32+64 mad (the radix-2^29 product), compiler-scheduled: 8 independent chains
+template <int ITERS>
+__global__ __launch_bounds__(256) void k_madi(uint64_t* out, uint32_t seed) {
+    int32_t a = (int32_t)(seed ^ threadIdx.x), b = (int32_t)(seed * 7u + blockIdx.x);
+    int64_t acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = (int64_t)(a + j) << 3;
+    for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            acc[j] = (int64_t)a * (int64_t)(b + j) + acc[j];
+            asm("" : "+v"(acc[j]));
+        }
+    }
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s ^= acc[j];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)s;
+}
+
+// 32-bit and (the radix-2^29 mask)
+template <int ITERS>
+__global__ __launch_bounds__(256) void k_and(uint32_t* out, uint32_t seed) {
+    uint32_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = seed + threadIdx.x * (j + 1);
+    uint32_t y = seed ^ blockIdx.x;
+    for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("v_and_b32 %0, %0, %1" : "+v"(x[j]) : "v"(y));
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s ^= x[j];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 int main() {
     const int ITERS = 4096;
     const int blocks = 256 * 8 * 4;  // plenty of waves per SIMD
@@ -102,6 +155,9 @@ int main() {
     timeit([&] { k_mad<ITERS><<<blocks, threads>>>((uint64_t*)d, 1234u); }, 8, "v_mad_u64_u32");
     timeit([&] { k_addc<ITERS><<<blocks, threads>>>((uint32_t*)d, 1234u); }, 8, "v_add(c)_co_u32");
     timeit([&] { k_add3<ITERS><<<blocks, threads>>>((uint32_t*)d, 1234u); }, 8, "v_add3_u32");
+    timeit([&] { k_ashr64<ITERS><<<blocks, threads>>>((uint64_t*)d, 1234u); }, 8, "v_ashrrev_i64");
+    timeit([&] { k_madi<ITERS><<<blocks, threads>>>((uint64_t*)d, 1234u); }, 8, "v_mad_i64_i32");
+    timeit([&] { k_and<ITERS><<<blocks, threads>>>((uint32_t*)d, 1234u); }, 8, "v_and_b32");
     CHK(hipFree(d));
     return 0;
 }
