@@ -453,6 +453,70 @@ SBFT_DEV void p29_add_aff_lean(jp29& acc, const f29& x2, const f29& y2) {
     else p29_add_aff_lean_s(acc, x2, y2);
 }
 
+// ---------------------------------------------------------------- co-Z table building
+// Odd multiples [1, 3, ..., 2^w - 1]Q with Meloni's co-Z additions (2007): every point of the
+// chain shares the Z of the running 2Q, so an addition costs 4M + 2S and only the Z ratios
+// h_k need keeping to make the table affine afterwards (one inversion per lane).
+// N' = f29_normalize output (limbs in (-2^26, 2^29 + 2^26)).
+
+// DBLU, a = -3, from affine P = (x, y) (N): D = 2P = (dx, dy) and P' = (px, py), both with
+// Z = 2y (returned in z; limbs < 2^30). 2M + 4S. Outputs N'.
+//   B = x^2, E = y^2, L = E^2, S = 4xE, M = 3(B - 1), X2 = M^2 - 2S, Y2 = M(S - X2) - 8L,
+//   P' = (S, 8L)
+SBFT_DEV void p29_dblu(const f29& x, const f29& y, f29& dx, f29& dy, f29& px, f29& py, f29& z) {
+    f29 b, e, l, t, m, m2;
+    f29_sqr(b, x);
+    f29_sqr(e, y);
+    f29_sqr(l, e);
+    f29_mul(t, x, e);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] <<= 2;              // 4xE < 2^31
+    f29_normalize(px, t);                                   // S (N')
+    const f29 one = f29_const(C29_ONE);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) m.v[i] = 3 * (b.v[i] - one.v[i]);  // |.| < 2^30.6
+    f29_normalize(m, m);                                    // M (N')
+    f29_sqr(m2, m);                                         // 2^29.2^2
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] = m2.v[i] - (px.v[i] << 1);  // (-2^30.2, 2^29 + 2^27)
+    f29_normalize(dx, t);                                   // X2 (N')
+#pragma unroll
+    for (int i = 0; i < 9; ++i) l.v[i] <<= 2;              // 4L < 2^31
+    f29_normalize(l, l);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) l.v[i] <<= 1;              // 8L, |.| < 2^30.2
+    f29_normalize(py, l);                                   // 8L (N')
+    f29_sub(t, px, dx);                                     // S - X2, |.| < 2^29.3
+    f29_mul(m2, m, t);                                      // 2^29.2 x 2^29.3
+    f29_sub(t, m2, py);                                     // (-2^29.2, 2^29)
+    f29_normalize(dy, t);                                   // Y2 (N')
+    f29_add(z, y, y);                                       // Z = 2y
+}
+
+// ZADDU: (dx, dy) = D and (tx, ty) = T share Z. T <- T + D and D <- D rescaled to the new
+// Z = Z h, with h = X_D - X_T returned (4M + 2S). In: N or N'. Out: T in N', D in N, h with
+// |limb| < 2^29.3. D == +-T (h = 0) cannot occur for the odd multiples of a point of prime
+// order n: (2k+1)Q = +-2Q would need 2k+1 = +-2 mod n.
+SBFT_DEV void p29_zaddu(f29& tx, f29& ty, f29& dx, f29& dy, f29& h) {
+    f29 c, w1, w2, r, dd, a1, t;
+    f29_sub(h, dx, tx);                                     // |.| < 2^29.3
+    f29_sqr(c, h);
+    f29_mul2(w1, dx, c, w2, tx, c);
+    f29_sub(r, dy, ty);                                     // |.| < 2^29.3
+    f29_sqr(dd, r);
+    f29_sub(t, w1, w2);                                     // |.| < 2^29
+    f29_mul(a1, dy, t);                                     // A1 = Y1 (W1 - W2)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] = dd.v[i] - w1.v[i] - w2.v[i];  // (-2^30, 2^29)
+    f29_normalize(tx, t);                                   // X3 (N')
+    f29_sub(t, w1, tx);                                     // |.| < 2^29.2
+    f29_mul(c, r, t);                                       // 2^29.3 x 2^29.2
+    f29_sub(t, c, a1);                                      // (-2^29, 2^29)
+    f29_normalize(ty, t);                                   // Y3 (N')
+    dx = w1;
+    dy = a1;
+}
+
 // ---------------------------------------------------------------- conversions
 // 8 x 32-bit limbs (a value < 2^256) -> 9 x 29-bit limbs (plain integer, not Montgomery).
 SBFT_DEV f29 f29_from_u256(const fe& a) {

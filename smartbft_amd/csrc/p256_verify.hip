@@ -415,7 +415,13 @@ __global__ __launch_bounds__(256) void p256_gcomb_build_kernel(uint4* __restrict
 #ifndef SBFT_DBL_UNROLL
 #define SBFT_DBL_UNROLL 1
 #endif
-constexpr int kDblUnroll = SBFT_DBL_UNROLL;  // doublings per iteration of the 4-doubling loop
+constexpr int kDblUnroll = SBFT_DBL_UNROLL;  // doublings per iteration of the w-doubling loop
+#ifndef SBFT_QWIN
+#define SBFT_QWIN 4
+#endif
+constexpr int kQWin = SBFT_QWIN;                    // u2 in radix 2^w
+constexpr int kQTab = 1 << (kQWin - 1);             // [1, 3, ..., 2^w - 1]Q
+constexpr int kQDigits = (255 + kQWin - 1) / kQWin; // windows over u2 >> 1 (< 2^255)
 #ifndef SBFT_VERIFY_WAVES
 #define SBFT_VERIFY_WAVES 2
 #endif
@@ -469,57 +475,49 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
 
     // Q in the radix-2^29 Montgomery domain of the ladder (p256_f29.hpp). Invalid lanes run a
     // harmless stand-in (Q = 2G, u1 = u2 = 1); their verdict is masked by `valid` at the end.
-    // The odd multiples [1,3,...,15]Q are built in Jacobian form (one doubling, seven lean
-    // additions), then made affine with ONE inversion per lane (Montgomery's trick over the
-    // seven Z's, safegcd mod p): every Q digit of the ladder is then a mixed addition
-    // (8M + 3S) instead of a Jacobian one (12M + 4S).
-    f29 tx[8], ty[8];  // affine odd multiples (scratch)
+    // The odd multiples [1,3,...,2^w - 1]Q are built with co-Z additions (DBLU, then ZADDU of
+    // the running 2Q: 4M + 2S each), then made affine with ONE inversion per lane (safegcd
+    // mod p of the final Z; the earlier Z's follow from the recorded ratios h_k). Every Q digit
+    // of the ladder is then a mixed addition (8M + 3S).
+    f29 tx[kQTab], ty[kQTab];  // affine odd multiples (scratch)
     {
-        jp29 q;
         const f29 r2 = f29_const(C29_R2);
-        f29_mul(q.x, f29_from_u256(qx), r2);
-        f29_mul(q.y, f29_from_u256(qy), r2);
-        q.z = f29_const(C29_ONE);
+        f29 qxm, qym;
+        f29_mul(qxm, f29_from_u256(qx), r2);
+        f29_mul(qym, f29_from_u256(qy), r2);
         if (!valid) {
-            q.x = f29_const(C29_G2X);
-            q.y = f29_const(C29_G2Y);
+            qxm = f29_const(C29_G2X);
+            qym = f29_const(C29_G2Y);
         }
-        tx[0] = q.x;
-        ty[0] = q.y;
-        jp29 tj[8];
-        tj[0] = q;
-        jp29 q2;
-        p29_dbl(q2, q);
-        // (2k+1)Q == +-2Q is impossible for a point of prime order n: no exceptional case here,
-        // and no Z is 0
+        tx[0] = qxm;
+        ty[0] = qym;
+        f29 dx, dy, cx, cy, z;  // D = 2Q and the current odd multiple, co-Z (Z = z)
+        p29_dblu(qxm, qym, dx, dy, cx, cy, z);
+        f29 hs[kQTab - 1];      // Z ratios: Z(T_k) = Z(T_{k-1}) h_k
 #pragma unroll 1
-        for (int k = 1; k < 8; ++k) {
-            jp29 t = tj[k - 1];
-            p29_add_jac_lean(t, q2);
-            tj[k] = t;
+        for (int k = 1; k < kQTab; ++k) {
+            f29 h;
+            p29_zaddu(cx, cy, dx, dy, h);  // T_k = T_{k-1} + 2Q
+            tx[k] = cx;
+            ty[k] = cy;
+            hs[k - 1] = h;
+            f29_mul(z, z, h);              // 2^30 (first) x 2^29.3
         }
-        f29 c[7];  // c[k] = Z_1 ... Z_{k+1}
-        c[0] = tj[1].z;
-#pragma unroll 1
-        for (int k = 1; k < 7; ++k) f29_mul(c[k], c[k - 1], tj[k + 1].z);
-        f29 inv;  // (Z_1 ... Z_7)^-1, Montgomery form
+        f29 inv;  // 1 / Z(T_last), Montgomery form
         {
-            const fe cp = f29_canon_plain(c[6]);
-            fe ci;
-            inv::inv_mod_p(ci.v, cp.v, dtab);
-            f29_mul(inv, f29_from_u256(ci), r2);
+            const fe zp = f29_canon_plain(z);
+            fe zi;
+            inv::inv_mod_p(zi.v, zp.v, dtab);
+            f29_mul(inv, f29_from_u256(zi), r2);
         }
 #pragma unroll 1
-        for (int k = 7; k >= 1; --k) {
-            f29 zi = inv, zi2, zi3;
-            if (k > 1) {
-                f29_mul(zi, inv, c[k - 2]);     // Z_k^-1
-                f29_mul(inv, inv, tj[k].z);     // (Z_1 ... Z_{k-1})^-1
-            }
-            f29_sqr(zi2, zi);
-            f29_mul(zi3, zi2, zi);
-            f29_mul(tx[k], tj[k].x, zi2);
-            f29_mul(ty[k], tj[k].y, zi3);      // Y may be N+- : 2^29 x 2^29
+        for (int k = kQTab - 1; k >= 1; --k) {
+            f29 zi2, zi3;
+            f29_sqr(zi2, inv);
+            f29_mul(zi3, zi2, inv);
+            f29_mul(tx[k], tx[k], zi2);
+            f29_mul(ty[k], ty[k], zi3);
+            f29_mul(inv, inv, hs[k - 1]);  // 1 / Z(T_{k-1})
         }
     }
     // 3. w = s^-1 from the launch-wide Montgomery trick (see p256_sinv_* kernels)
@@ -562,73 +560,29 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
         fe_sel(u1, neg1, t1);
         fe_sel(u2, neg2, t2);
     }
-    // u = sum_{i<64} d_i 16^i + 16^64 with d_i = 2*((u >> (4i+1)) & 15) - 15 (odd, nonzero).
-    // The top digit is 1, so the accumulator starts at +-Q, never at infinity.
     jp29 acc;  // reloaded from scratch: keeps q out of registers during the setup
     acc.x = tx[0];
     acc.y = ty[0];
     acc.z = f29_const(C29_ONE);
     if (neg2) f29_neg(acc.y, acc.y);
-#if !SBFT_G_COMB
-    // radix 256 for u1 over the LDS table [1,3,...,255]G, on every other radix-16 window
-    {
-        f29 gx, gy;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            gx.v[k] = gtab[k];
-            gy.v[k] = gtab[10 + k];
-        }
-        if (neg1) f29_neg(gy, gy);
-        p29_add_aff_lean(acc, gx, gy);
-    }
-    fe k1 = u1;
-    u32 above1 = 0;
-#endif
+    // u2 = sum_{i<K} d_i 2^(w i) + 2^(w K), d_i = 2*((u2 >> (w i + 1)) & (2^w - 1)) - (2^w - 1)
+    // (odd, nonzero), K = ceil(255 / w): the accumulator starts at +-Q (the 2^(wK) term).
     fe k2 = u2;
-    u32 above2 = 0;
 #pragma unroll 1
-    for (int limb = 7; limb >= 0; --limb) {
-        const u32 cur2 = k2.v[7];
-#pragma unroll
-        for (int k = 7; k > 0; --k) k2.v[k] = k2.v[k - 1];
-        const u64 f2 = ((u64)above2 << 32) | cur2;
-        above2 = cur2;
-#if !SBFT_G_COMB
-        const u32 cur1 = k1.v[7];
-#pragma unroll
-        for (int k = 7; k > 0; --k) k1.v[k] = k1.v[k - 1];
-        const u64 f1 = ((u64)above1 << 32) | cur1;
-        above1 = cur1;
-#endif
-#pragma unroll 1
-        for (int nib = 7; nib >= 0; --nib) {
+    for (int i = kQDigits - 1; i >= 0; --i) {
 #pragma unroll kDblUnroll
-            for (int d = 0; d < 4; ++d) p29_dbl(acc, acc);
-            // Q digit (odd, in [-15, 15])
-            {
-                const int d2 = 2 * (int)((u32)(f2 >> (4 * nib + 1)) & 15u) - 15;
-                const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
-                const f29 x2 = tx[m2];
-                f29 y2 = ty[m2];
-                if ((d2 < 0) != neg2) f29_neg(y2, y2);
-                p29_add_aff_lean(acc, x2, y2);
-            }
+        for (int d = 0; d < kQWin; ++d) p29_dbl(acc, acc);
+        const int b = kQWin * i + 1, lw = b >> 5;
+        const u32 lo = k2.v[lw], hi = lw < 7 ? k2.v[lw + 1] : 0u;
+        const int d2 = 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & (2 * kQTab - 1)) - (2 * kQTab - 1);
+        const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
+        const f29 x2 = tx[m2];
+        f29 y2 = ty[m2];
+        if ((d2 < 0) != neg2) f29_neg(y2, y2);
+        p29_add_aff_lean(acc, x2, y2);
 #if !SBFT_G_COMB
-            // G digit (odd, in [-255, 255]) on every other radix-16 window
-            if ((nib & 1) == 0) {
-                const int d1 = 2 * (int)((u32)(f1 >> (4 * nib + 1)) & 255u) - 255;
-                const int base = ((d1 < 0 ? -d1 : d1) >> 1) * 20;
-                f29 gx, gy;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    gx.v[k] = gtab[base + k];
-                    gy.v[k] = gtab[base + 10 + k];
-                }
-                if ((d1 < 0) != neg1) f29_neg(gy, gy);
-                p29_add_aff_lean(acc, gx, gy);
-            }
+#error "the radix-256 in-ladder G windows need kQWin = 4; build with SBFT_G_COMB=1"
 #endif
-        }
     }
 #if SBFT_G_COMB
     // u1*G by the fixed-base comb in HBM (no doublings): u1 = sum_{i<16} d_i 2^(16 i) + 2^256
