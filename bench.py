@@ -28,10 +28,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # Roofline accounting: algorithmic work per verify = 4,096 F_p-multiplication
-# equivalents x 64 32x32->64 products; peak = measured v_mad_u64_u32 rate on
-# MI355X (tools/valu_peak.hip: 33.9 T lane-ops/s; profiles/r01_valu_peak.txt).
+# equivalents x 64 32x32->64 products; peak = measured rate of the product
+# instruction the kernel issues, v_mad_i64_i32, on MI355X (tools/valu_peak.hip: 38.0 T
+# lane-ops/s; profiles/r01g_valu_peak.txt).
 PRODUCTS_PER_VERIFY = 262_144
-MAD_PEAK_T = 33.9
+MAD_PEAK_T = 38.0
 
 
 def parse():
@@ -310,7 +311,7 @@ def main():
                                    "distinct key per tuple, 10% corrupted, device-resident",
                        "tuples_per_gpu": n, "parallelism": f"batch split x{world} (no collective)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_t, 3), "peak": MAD_PEAK_T,
-                         "unit": "T 32x32->64 products/s (v_mad_u64_u32)",
+                         "unit": "T 32x32->64 products/s (v_mad_i64_i32 issue rate)",
                          "frac": round(achieved_t / MAD_PEAK_T, 4), "traffic": traffic,
                          "kernel": "p256_verify_kernel", "avg_kernel_ms": round(avg_kern_s * 1e3, 4),
                          "kernel_timing": "HIP events around p256_verify_kernel on its launch stream",

@@ -72,17 +72,11 @@ struct Slot {
     bool gcomb_ready = false;
 
     // The comb table, building it (synchronously, on this slot's stream) the first time.
-    // Returns nullptr on failure; a table size of 0 (kernel built without the comb) returns a
-    // dummy non-null pointer that is never read.
+    // Returns nullptr on failure.
     const void* gcomb_table() {
         std::lock_guard<std::mutex> g(gcomb_mu);
         if (gcomb_ready) return gcomb;
         const size_t bytes = sbft_gcomb_table_bytes();
-        if (bytes == 0) {
-            gcomb_ready = true;
-            gcomb = (void*)this;
-            return gcomb;
-        }
         if (hipSetDevice(device) != hipSuccess) return nullptr;
         if (!gcomb && hipMalloc(&gcomb, bytes) != hipSuccess) {
             gcomb = nullptr;
@@ -203,7 +197,7 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
         if (s->d_keytab) (void)hipFree(s->d_keytab);
         for (void* t : s->retired) (void)hipFree(t);
         if (s->pin) (void)hipHostFree(s->pin);
-        if (s->gcomb && sbft_gcomb_table_bytes()) (void)hipFree(s->gcomb);
+        if (s->gcomb) (void)hipFree(s->gcomb);
         for (auto& kv : s->ws) {
             (void)hipStreamSynchronize(kv.first);
             if (kv.second.ptr) (void)hipFree(kv.second.ptr);

@@ -276,7 +276,6 @@ __device__ __constant__ static const u32 C29_ONE[9] = P256_F29_ONE;
 __device__ __constant__ static const u32 C29_2P[9] = P256_F29_2P;
 __device__ __constant__ static const u32 C29_G2X[9] = P256_F29_G2X;
 __device__ __constant__ static const u32 C29_G2Y[9] = P256_F29_G2Y;
-__device__ __constant__ static const u32 C29_GODD8[P256_GODD8_F29_WORDS] = P256_GODD8_F29_DATA;
 
 SBFT_DEV f29 f29_const(const u32* c) {
     f29 r;
