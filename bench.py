@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-latency", action="store_true", help="skip configs 3/4 latency")
     ap.add_argument("--latency-calls", type=int, default=200)
     ap.add_argument("--no-sha", action="store_true", help="skip the config-5 hashing measurement")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer rate")
     ap.add_argument("--sha-messages", type=int, default=2_097_152,
                     help="config 5: 16M requests over 8 GPUs = 2M per GPU (~68 GB of payload in HBM)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_verify_latest.json"))
@@ -94,6 +95,24 @@ def cpu_baseline(wl, sample: int, threads: int):
     if go_proxy:
         go_proxy["cpu"] = cpu_model
     return port, go_proxy, ok_cpu
+
+
+def host_path(gv, wl, dev, reps: int = 3):
+    """PCIe-inclusive rate of the host-buffer C ABI (sbft_gv_verify_p256: the call a cgo
+    plugin makes with Go-heap tuples): H2D of 160 B/tuple + verify pipeline + D2H of verdicts,
+    on the same 1M tuples. Reported beside `value`, never as it."""
+    f = [np.ascontiguousarray(a) for a in wl.host_fields(0, wl.n)]
+    ok = gv.verify(*f)  # warm-up (workspace growth)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ok = gv.verify(*f)
+        ts.append(time.perf_counter() - t0)
+    want = (~wl.corrupted).to(torch.uint8).cpu().numpy()
+    best = min(ts)
+    return {"value": round(wl.n / best, 1), "unit": "verifies/s", "ms": round(best * 1e3, 3),
+            "mismatches": int((ok != want).sum()),
+            "path": "sbft_gv_verify_p256, pageable host buffers, H2D + kernels + D2H"}
 
 
 def _pcts(ts):
@@ -331,6 +350,8 @@ def main():
             rec["speedup_vs_cpu_baseline"] = round(value / port["value"], 1)
             if go_proxy:
                 rec["speedup_vs_go_proxy"] = round(value / go_proxy["value"], 1)
+        if world == 1 and not args.no_host_path:
+            rec["host_buffer_path"] = host_path(gv, wl, dev)
         if world == 1 and not args.no_sha:
             rec["sha256_config5"] = sha_config5(gv, dev, args.sha_messages)
         if world == 1 and not args.no_latency:
