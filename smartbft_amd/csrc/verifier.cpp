@@ -7,12 +7,16 @@
 // the structure-of-arrays batches; there is no CPU verification path.
 #include "../../include/sbft_verifier.h"
 
+#include <cpuid.h>
+#include <immintrin.h>
+
 #include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -36,6 +40,57 @@ const uint32_t K256[64] = {
 
 inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
+// SHA-256 compression with the x86 SHA extensions (Proposal.Digest hashes whole proposals on
+// the host: 3.2 MB at 10k requests; Go's crypto/sha256 uses the same instructions). Two rounds
+// per sha256rnds2; state kept as ABEF / CDGH; message schedule by sha256msg1/msg2:
+//   X_g = msg2(msg1(X_{g-4}, X_{g-3}) + alignr(X_{g-1}, X_{g-2}, 4), X_{g-1}), X_g = W[4g..4g+3].
+__attribute__((target("sha,sse4.1"))) void sha256_blocks_ni(uint32_t h[8], const uint8_t* p, size_t nblk) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    __m128i t = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&h[0]), 0xB1);  // C D A B
+    __m128i s1 = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&h[4]), 0x1B); // E F G H
+    __m128i s0 = _mm_alignr_epi8(t, s1, 8);                                         // A B E F
+    s1 = _mm_blend_epi16(s1, t, 0xF0);                                              // C D G H
+    for (; nblk; --nblk, p += 64) {
+        const __m128i save0 = s0, save1 = s1;
+        __m128i x[4];
+        for (int g = 0; g < 16; ++g) {
+            __m128i m;
+            if (g < 4) {
+                m = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(p + 16 * g)), bswap);
+            } else {
+                m = _mm_sha256msg1_epu32(x[g & 3], x[(g + 1) & 3]);                    // X_{g-4}, X_{g-3}
+                m = _mm_add_epi32(m, _mm_alignr_epi8(x[(g + 3) & 3], x[(g + 2) & 3], 4)); // X_{g-1}, X_{g-2}
+                m = _mm_sha256msg2_epu32(m, x[(g + 3) & 3]);
+            }
+            x[g & 3] = m;
+            __m128i k = _mm_add_epi32(m, _mm_loadu_si128((const __m128i*)&K256[4 * g]));
+            s1 = _mm_sha256rnds2_epu32(s1, s0, k);
+            k = _mm_shuffle_epi32(k, 0x0E);
+            s0 = _mm_sha256rnds2_epu32(s0, s1, k);
+        }
+        s0 = _mm_add_epi32(s0, save0);
+        s1 = _mm_add_epi32(s1, save1);
+    }
+    t = _mm_shuffle_epi32(s0, 0x1B);    // F E B A
+    s1 = _mm_shuffle_epi32(s1, 0xB1);   // D C H G
+    s0 = _mm_blend_epi16(t, s1, 0xF0);  // D C B A
+    s1 = _mm_alignr_epi8(s1, t, 8);     // H G F E
+    _mm_storeu_si128((__m128i*)&h[0], s0);
+    _mm_storeu_si128((__m128i*)&h[4], s1);
+}
+
+bool cpu_has_sha() {
+    static const bool has = [] {
+        if (std::getenv("SBFT_NO_SHANI")) return false;  // tests exercise the portable path too
+        unsigned a, b, c, d;
+        if (!__get_cpuid_count(7, 0, &a, &b, &c, &d)) return false;
+        const bool sha = (b >> 29) & 1;
+        if (!__get_cpuid(1, &a, &b, &c, &d)) return false;
+        return sha && ((c >> 19) & 1);  // SSE4.1
+    }();
+    return has;
+}
+
 struct Sha256 {
     uint32_t h[8];
     uint8_t buf[64];
@@ -46,7 +101,15 @@ struct Sha256 {
                                        0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
         std::memcpy(h, iv, sizeof h);
     }
-    void block(const uint8_t* p) {
+    void block(const uint8_t* p) { blocks(p, 1); }
+    void blocks(const uint8_t* p, size_t nblk) {
+        if (cpu_has_sha()) {
+            sha256_blocks_ni(h, p, nblk);
+            return;
+        }
+        for (; nblk; --nblk, p += 64) block_portable(p);
+    }
+    void block_portable(const uint8_t* p) {
         uint32_t w[64];
         for (int i = 0; i < 16; ++i)
             w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
@@ -65,9 +128,10 @@ struct Sha256 {
         total += n;
         while (n) {
             if (fill == 0 && n >= 64) {
-                block(p);
-                p += 64;
-                n -= 64;
+                const size_t nb = n / 64;
+                blocks(p, nb);
+                p += 64 * nb;
+                n -= 64 * nb;
                 continue;
             }
             const size_t take = std::min(n, 64 - fill);
@@ -184,11 +248,6 @@ void der_len(std::vector<uint8_t>& o, size_t n) {
     o.push_back((uint8_t)(0x80 | k));
     while (k) o.push_back(tmp[--k]);
 }
-void der_octets(std::vector<uint8_t>& o, const uint8_t* p, size_t n) {
-    o.push_back(0x04);
-    der_len(o, n);
-    if (n) o.insert(o.end(), p, p + n);
-}
 void der_int64(std::vector<uint8_t>& o, int64_t v) {
     // minimal two's complement, as Go encoding/asn1 marshals int64
     uint8_t b[8];
@@ -226,7 +285,11 @@ struct Reader {
 };
 
 struct Req {
-    std::string client_id, req_id;
+    // views into the request bytes (borrowed for the call; no per-request allocation)
+    struct Str {
+        const char* p = "";
+        int n = 0;
+    } client_id, req_id;
     size_t body_off = 0, body_len = 0;  // relative to the buffer handed to parse_request
     const uint8_t* pub = nullptr;       // 65 bytes SEC1
     const uint8_t* sig = nullptr;       // 64 bytes r||s
@@ -241,9 +304,9 @@ bool parse_request(const uint8_t* d, size_t len, size_t base, Req& out) {
     uint32_t a, b, c;
     if (!r.take(4, q) || std::memcmp(q, REQ_MAGIC, 4)) return false;
     if (!r.u16(a) || !r.take(a, q)) return false;
-    out.client_id.assign((const char*)q, a);
+    out.client_id = {(const char*)q, (int)a};
     if (!r.u16(b) || !r.take(b, q)) return false;
-    out.req_id.assign((const char*)q, b);
+    out.req_id = {(const char*)q, (int)b};
     if (!r.u32(c) || !r.take(c, q)) return false;
     if (!r.take(65, out.pub)) return false;
     out.body_off = base;
@@ -296,13 +359,13 @@ void put_err(char* err, size_t cap, const char* fmt, ...) {
     va_end(ap);
 }
 
-bool write_info(char*& w, char* end, const std::string& cid, const std::string& id) {
-    if ((size_t)(end - w) < cid.size() + id.size() + 2) return false;
-    std::memcpy(w, cid.data(), cid.size());
-    w += cid.size();
+bool write_info(char*& w, char* end, const Req::Str& cid, const Req::Str& id) {
+    if ((size_t)(end - w) < (size_t)cid.n + (size_t)id.n + 2) return false;
+    std::memcpy(w, cid.p, cid.n);
+    w += cid.n;
     *w++ = 0;
-    std::memcpy(w, id.data(), id.size());
-    w += id.size();
+    std::memcpy(w, id.p, id.n);
+    w += id.n;
     *w++ = 0;
     return true;
 }
@@ -568,19 +631,31 @@ extern "C" {
 void sbft_sha256_host(const uint8_t* msg, size_t len, uint8_t out[32]) { sha256(msg, len, out); }
 
 void sbft_proposal_digest(const sbft_proposal* p, char out65[65]) {
-    std::vector<uint8_t> body;
-    body.reserve(p->payload_len + p->header_len + p->metadata_len + 32);
-    der_octets(body, p->payload, p->payload_len);
-    der_octets(body, p->header, p->header_len);
-    der_octets(body, p->metadata, p->metadata_len);
-    der_int64(body, p->verification_sequence);
-    std::vector<uint8_t> der;
-    der.reserve(body.size() + 8);
-    der.push_back(0x30);
-    der_len(der, body.size());
-    der.insert(der.end(), body.begin(), body.end());
+    // SHA-256 over the DER encoding, streamed: SEQUENCE { OCTET STRING payload, header,
+    // metadata; INTEGER verification_sequence }. Only the tag/length prefixes are built here;
+    // the (MB-sized) payload is hashed where it lies.
+    std::vector<uint8_t> pre[3], seq, tail;
+    const uint8_t* data[3] = {p->payload, p->header, p->metadata};
+    const size_t lens[3] = {p->payload_len, p->header_len, p->metadata_len};
+    size_t body = 0;
+    for (int i = 0; i < 3; ++i) {
+        pre[i].push_back(0x04);
+        der_len(pre[i], lens[i]);
+        body += pre[i].size() + lens[i];
+    }
+    der_int64(tail, p->verification_sequence);
+    body += tail.size();
+    seq.push_back(0x30);
+    der_len(seq, body);
+    Sha256 h;
+    h.update(seq.data(), seq.size());
+    for (int i = 0; i < 3; ++i) {
+        h.update(pre[i].data(), pre[i].size());
+        if (lens[i]) h.update(data[i], lens[i]);
+    }
+    h.update(tail.data(), tail.size());
     uint8_t d[32];
-    sha256(der.data(), der.size(), d);
+    h.final(d);
     static const char* hx = "0123456789abcdef";
     for (int i = 0; i < 32; ++i) {
         out65[2 * i] = hx[d[i] >> 4];
@@ -651,8 +726,8 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     for (size_t i = 0; i < n; ++i) {
         if (reqs[i].pub[0] != 0x04) {
             if (bad_index) *bad_index = (int64_t)i;
-            put_err(err, err_cap, "request %zu (%s:%s): public key is not SEC1 uncompressed", i,
-                    reqs[i].client_id.c_str(), reqs[i].req_id.c_str());
+            put_err(err, err_cap, "request %zu (%.*s:%.*s): public key is not SEC1 uncompressed", i,
+                    reqs[i].client_id.n, reqs[i].client_id.p, reqs[i].req_id.n, reqs[i].req_id.p);
             return SBFT_V_EFORMAT;
         }
         off[i] = reqs[i].body_off;
@@ -678,8 +753,8 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     for (size_t i = 0; i < n; ++i)
         if (!ok[i]) {
             if (bad_index) *bad_index = (int64_t)i;
-            put_err(err, err_cap, "request %zu (%s:%s) has an invalid signature", i, reqs[i].client_id.c_str(),
-                    reqs[i].req_id.c_str());
+            put_err(err, err_cap, "request %zu (%.*s:%.*s) has an invalid signature", i, reqs[i].client_id.n,
+                    reqs[i].client_id.p, reqs[i].req_id.n, reqs[i].req_id.p);
             return SBFT_V_EVERIFY;
         }
     char* w = infos;
@@ -707,7 +782,8 @@ int sbft_verifier_verify_request(sbft_verifier* v, const uint8_t* req, size_t le
         return rc;
     }
     if (!ok) {
-        put_err(err, err_cap, "request %s:%s has an invalid signature", q.client_id.c_str(), q.req_id.c_str());
+        put_err(err, err_cap, "request %.*s:%.*s has an invalid signature", q.client_id.n, q.client_id.p,
+                q.req_id.n, q.req_id.p);
         return SBFT_V_EVERIFY;
     }
     char* w = info;
@@ -1025,8 +1101,8 @@ int sbft_request_batcher_verify(sbft_request_batcher* b, const uint8_t* req, siz
         return SBFT_V_EFORMAT;
     }
     if (me.status) {
-        put_err(err, err_cap, "request %s:%s has an invalid signature", me.parsed.client_id.c_str(),
-                me.parsed.req_id.c_str());
+        put_err(err, err_cap, "request %.*s:%.*s has an invalid signature", me.parsed.client_id.n,
+                me.parsed.client_id.p, me.parsed.req_id.n, me.parsed.req_id.p);
         return me.status;
     }
     char* w = info;

@@ -5,6 +5,7 @@ import hashlib
 
 import pytest
 
+from conftest import ROOT
 from smartbft_amd import plugin
 
 
@@ -51,9 +52,32 @@ def test_proposal_digest_matches_go_asn1(size, vseq):
 
 
 def test_host_sha256():
-    for n in (0, 1, 55, 56, 63, 64, 65, 1000):
-        m = bytes(range(256)) * 4
-        assert plugin.sha256_host(m[:n]) == hashlib.sha256(m[:n]).digest()
+    """Host SHA-256 (SHA-NI when the CPU has it) against hashlib: every length 0..300, then
+    random lengths up to 200 KB."""
+    import random
+    rng = random.Random(3)
+    m = rng.randbytes(200_000)
+    for n in list(range(301)) + [rng.randrange(301, 200_000) for _ in range(60)]:
+        assert plugin.sha256_host(m[:n]) == hashlib.sha256(m[:n]).digest(), n
+
+
+def test_host_sha256_portable_path():
+    """The portable compression (CPUs without the SHA extensions), forced by SBFT_NO_SHANI, in
+    a fresh process: same digests, and Proposal.Digest unchanged."""
+    import os
+    import subprocess
+    import sys
+    code = ("import hashlib, random, sys; sys.path.insert(0, %r); from smartbft_amd import plugin; "
+            "rng = random.Random(4); m = rng.randbytes(50_000); "
+            "assert all(plugin.sha256_host(m[:n]) == hashlib.sha256(m[:n]).digest() "
+            "for n in list(range(200)) + [777, 4096, 50_000]); "
+            "print(plugin.Proposal(m, b'h', b'md', 7).Digest())") % ROOT
+    env = dict(os.environ, SBFT_NO_SHANI="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    import random as _r
+    m = _r.Random(4).randbytes(50_000)
+    assert out.stdout.strip() == plugin.Proposal(m, b"h", b"md", 7).Digest()
 
 
 def _fake_request(cid, rid, payload):
