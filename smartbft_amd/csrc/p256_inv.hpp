@@ -92,9 +92,9 @@ SBFT_HD int32_t divsteps30(int32_t delta, uint32_t f, uint32_t g, const uint32_t
     for (int j = 0; j < 6; ++j) {
         const int32_t dc = delta < -4 ? -4 : (delta > 5 ? 5 : delta);
         const uint32_t idx = ((uint32_t)(dc + 4) << 9) | (((f >> 1) & 15u) << 5) | (g & 31u);
-        const uint32_t w0 = tab[2 * idx], w1 = tab[2 * idx + 1];
-        const int32_t a = (int32_t)(w0 << 24) >> 24, b = (int32_t)(w0 << 16) >> 24;
-        const int32_t c = (int32_t)(w0 << 8) >> 24, d = (int32_t)w0 >> 24;
+        const uint32_t w = tab[idx];  // packed entry, tools/gen_inv_table.py
+        const int32_t a = (int32_t)(w & 63u) - 8, b = (int32_t)((w >> 6) & 63u) - 6;
+        const int32_t c = (int32_t)((w >> 12) & 63u) - 16, d = (int32_t)((w >> 18) & 63u) - 15;
         // low words advance by 5 divsteps (the low 5 bits of a f + b g and c f + d g are zero)
         const uint32_t nf = ((uint32_t)a * f + (uint32_t)b * g) >> 5;
         const uint32_t ng = ((uint32_t)c * f + (uint32_t)d * g) >> 5;
@@ -107,8 +107,8 @@ SBFT_HD int32_t divsteps30(int32_t delta, uint32_t f, uint32_t g, const uint32_t
         vv = nv;
         qq = nq;
         rr = nr;
-        const int32_t cst = (int32_t)(w1 << 16) >> 24;
-        delta = ((w1 & 1u) ? -delta : delta) + cst;
+        const int32_t cst = (int32_t)((w >> 24) & 15u) - 3;
+        delta = ((w >> 28) & 1u ? -delta : delta) + cst;
     }
     u = uu;
     v = vv;
