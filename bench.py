@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 # lane-ops/s; profiles/r01g_valu_peak.txt).
 PRODUCTS_PER_VERIFY = 262_144
 MAD_PEAK_T = 38.0
+VALU_ISSUE_PEAK_T = 39.3  # 1,024 SIMDs x 64 lanes / 4 cycles x 2.4 GHz (64-bit ops and mads)
 
 
 def parse():
@@ -230,9 +231,21 @@ def sha_config5(gv, dev, n_msgs: int, uniform_len: int = 0):
 
     sec = timed(None)  # index order: the load-balanced kernel needs no length sort
     gbs = (total + 32 * n_msgs) / sec / 1e9
-    del blob
+    # end to end from host memory (the host-buffer C ABI: pageable H2D + kernel + D2H) on a
+    # bounded sample of the same messages: 65,536 messages, ~2.1 GB
+    k = min(n_msgs, 65536)
+    hb = blob[:int(off[k - 1]) + int(ln[k - 1])].cpu().numpy()
+    gv.sha256(hb, off[:k], ln[:k])  # warm-up (staging growth)
+    t0 = time.perf_counter()
+    hd = gv.sha256(hb, off[:k], ln[:k])
+    e2e = time.perf_counter() - t0
+    assert hd[k - 1].tobytes() == dig[k - 1].cpu().numpy().tobytes()
+    e2e_gbs = (hb.size + 32 * k) / e2e / 1e9
+    del blob, hb
     return {"value": round(gbs, 1), "unit": "GB/s (payload + digest bytes, kernel time)",
             "messages": n_msgs, "payload_bytes": total, "avg_kernel_ms": round(sec * 1e3, 3),
+            "end_to_end": {"value": round(e2e_gbs, 1), "unit": "GB/s", "messages": k,
+                           "path": "sbft_gv_sha256 from pageable host memory (H2D + kernel + D2H)"},
             "roofline": {"bound": "valu", "hbm_peak_GBs": 8000, "frac_of_hbm": round(gbs / 8000, 4),
                          "valu_ceiling_GBs": 1840,
                          "frac_of_valu_ceiling": round(gbs / 1840, 4),
@@ -306,11 +319,13 @@ def main():
         value = total / elapsed
         achieved_t = n * PRODUCTS_PER_VERIFY / avg_kern_s / 1e12
         traffic = None
+        instr_per_verify = None
         if os.path.exists(args.traffic_file):
             try:
                 tj = json.load(open(args.traffic_file))
                 if tj.get("n") == n:
                     traffic = tj.get("hbm_bytes_per_launch")
+                    instr_per_verify = tj.get("valu_instructions_per_verify")
             except (OSError, ValueError):
                 traffic = None
         rec = {
@@ -337,6 +352,14 @@ def main():
                          "step_gpu_ms": round(avg_step_gpu_ms, 4),
                          "step_kernels": "sinv_prep + sinv_totals + verify + fixup",
                          "products_per_verify": PRODUCTS_PER_VERIFY},
+            # issued-instruction view of the same kernel: VALU instructions per verify from the
+            # committed PMC pass (SQ_INSTS_VALU x 64 / n, profiles/pmc_verify_latest.json) at this
+            # run's rate, against the chip's issue capacity (1,024 SIMDs x 64 lanes / 4 cycles at
+            # the 2.4 GHz peak clock; the kernel runs at ~2.05 GHz, GRBM_GUI_ACTIVE)
+            "valu_issue": None if not instr_per_verify else {
+                "instr_per_verify": round(instr_per_verify), "achieved_T": round(instr_per_verify * n / avg_kern_s / 1e12, 2),
+                "peak_T": VALU_ISSUE_PEAK_T, "frac": round(instr_per_verify * n / avg_kern_s / 1e12 / VALU_ISSUE_PEAK_T, 3),
+                "frac_at_2_05GHz": round(instr_per_verify * n / avg_kern_s / 1e12 / (VALU_ISSUE_PEAK_T * 2.05 / 2.4), 3)},
             "parity": {"full_size_mismatches": mismatches,
                        "expected_accepts": int(expect.sum()) * world},
         }
