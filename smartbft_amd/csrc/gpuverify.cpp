@@ -114,6 +114,12 @@ struct Slot {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// signing batches up to this size take the wavefront-per-signature kernel (defined with the
+// registered-key code below, which owns G's comb table)
+constexpr size_t kSignWaveMax = 4096;
+int sign_wave(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_t* digest, size_t n, uint8_t* qx,
+              uint8_t* qy, uint8_t* r, uint8_t* s, uint8_t* status);
+
 
 }  // namespace
 
@@ -526,6 +532,9 @@ int sbft_gv_sign_p256(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, cons
     if (!ctx) return SBFT_GV_EINVAL;
     if (n == 0) return SBFT_GV_OK;
     if (!d || !k || !digest || !qx || !qy || !r || !s || !status || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    // latency path (api.Signer: one signature per call): a wavefront per signature over G's comb
+    // table instead of one lane running two scalar multiplications alone
+    if (n <= kSignWaveMax) return sign_wave(ctx, d, k, digest, n, qx, qy, r, s, status);
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
         return enqueue_sign(c, d, k, digest, qx, qy, r, s, status);
     });
@@ -696,6 +705,48 @@ int run_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* blob, size
     if (rc == SBFT_GV_OK)
         for (auto& c : chunks) std::memcpy(ok_out + c.begin, c.slot->pin + c.out_off, c.count);
     return rc;
+}
+
+// Small signing batches on one device: one H2D of d | k | digest through pinned staging, the
+// wave kernel over G's comb table (slot 0, built on first use), one D2H of qx | qy | r | s | status.
+int sign_wave(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_t* digest, size_t n, uint8_t* qx,
+              uint8_t* qy, uint8_t* r, uint8_t* s, uint8_t* status) {
+    std::vector<std::array<uint8_t, 64>> keys;
+    {
+        std::lock_guard<std::mutex> g(ctx->keys_mu);
+        keys.assign(ctx->keys.begin(), ctx->keys.begin() + ctx->nkeys.load());
+    }
+    std::vector<Chunk> chunks = plan(ctx, n);  // n < min_split: one device
+    Slot* sl = chunks[0].slot;
+    std::lock_guard<std::mutex> lk(sl->mu);
+    int rc = build_tables(sl, keys, 1, nullptr);  // G's table
+    if (rc) return rc;
+    const size_t f = align_up(32 * n, 256), fs = align_up(n, 256);
+    const size_t in_bytes = 3 * f, out_bytes = 4 * f + fs;
+    HIPCHK(hipSetDevice(sl->device));
+    rc = sl->reserve(in_bytes + out_bytes);
+    if (rc) return rc;
+    rc = sl->reserve_pinned(in_bytes + out_bytes);
+    if (rc) return rc;
+    uint8_t* h = sl->pin;
+    std::memcpy(h, d, 32 * n);
+    std::memcpy(h + f, k, 32 * n);
+    std::memcpy(h + 2 * f, digest, 32 * n);
+    uint8_t* b = sl->dbuf;
+    HIPCHK(hipMemcpyAsync(b, h, in_bytes, hipMemcpyHostToDevice, sl->stream));
+    uint8_t* o = b + in_bytes;
+    if (sbft_launch_p256_sign_wave(b, b + f, b + 2 * f, (const void* const*)sl->d_keytab, o, o + f, o + 2 * f,
+                                   o + 3 * f, o + 4 * f, (uint32_t)n, sl->stream))
+        return SBFT_GV_ELAUNCH;
+    HIPCHK(hipMemcpyAsync(h + in_bytes, o, out_bytes, hipMemcpyDeviceToHost, sl->stream));
+    HIPCHK(hipStreamSynchronize(sl->stream));
+    const uint8_t* ho = h + in_bytes;
+    std::memcpy(qx, ho, 32 * n);
+    std::memcpy(qy, ho + f, 32 * n);
+    std::memcpy(r, ho + 2 * f, 32 * n);
+    std::memcpy(s, ho + 3 * f, 32 * n);
+    std::memcpy(status, ho + 4 * f, n);
+    return SBFT_GV_OK;
 }
 
 }  // namespace

@@ -47,6 +47,11 @@ extern "C" {
 size_t sbft_comb_table_bytes(void);
 // table[w][j] = j 2^(8w) Q for the key (qx, qy) (32-byte big-endian, device memory);
 // d_status[0] = 1 iff the key is valid.
+// Latency-path signing, one wavefront per signature over G's comb table (keytab[0]); same
+// outputs as sbft_launch_p256_sign.
+int sbft_launch_p256_sign_wave(const uint8_t* d_d, const uint8_t* d_k, const uint8_t* d_e,
+                               const void* const* d_keytab, uint8_t* d_qx, uint8_t* d_qy, uint8_t* d_r,
+                               uint8_t* d_s, uint8_t* d_status, uint32_t n, hipStream_t stream);
 int sbft_launch_comb_build(const uint8_t* d_qx, const uint8_t* d_qy, void* d_table, uint32_t* d_status,
                            hipStream_t stream);
 // Verify n tuples against registered keys: d_key[t] in [1, nkeys) indexes d_keytab (slot 0 = G).

@@ -204,6 +204,18 @@ def test_signer_matches_oracle(gpu):
     bad = arr([0, oracle.N, oracle.N + 5])
     *_, st2 = gpu.sign(bad, arr([1, 1, 1]), arr([b"\0" * 32] * 3))
     assert not st2.any()
+    # batches above the latency-path size (4,096) take the one-lane-per-signature kernel: same
+    # outputs, byte for byte, on the same inputs
+    m = 5000
+    d2 = d + [int.from_bytes(rng.bytes(32), "big") % oracle.N or 1 for _ in range(m - n)]
+    k2 = k + [int.from_bytes(rng.bytes(32), "big") % oracle.N or 1 for _ in range(m - n)]
+    e2 = e + [rng.bytes(32) for _ in range(m - n)]
+    big = gpu.sign(arr(d2), arr(k2), arr(e2))
+    for got, want in zip(big, (qx, qy, r, s, st)):
+        assert np.array_equal(got[:n], want)
+    assert big[4].all()
+    for i in rng.choice(np.arange(n, m), 100, replace=False):
+        assert (big[2][i].tobytes(), big[3][i].tobytes()) == oracle.sign(d2[i], k2[i], e2[i]), i
 
 
 def test_bench_workload_properties(gpu):
