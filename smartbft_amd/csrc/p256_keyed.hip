@@ -289,19 +289,41 @@ SBFT_DEV bool x_matches_r(const jp& R, const fe& r) {
 // One wavefront per tuple. Digests come either precomputed (digest != null) or as messages
 // blob[off[t] .. +len[t]) hashed here (digest == null). key[t] indexes keytab (slot 0 is G's
 // table, so registered keys are 1 .. nkeys-1).
-__global__ __launch_bounds__(64) void p256_verify_keyed_wave_kernel(
+// Two wavefronts per signature: wave 1 inverts s (safegcd, wave-uniform: the compiler runs it
+// on the scalar unit, ~37k cycles) while wave 0 hashes the message; they meet at one barrier
+// and wave 0 carries on alone. The two dependent chains overlapped instead of following each
+// other.
+__global__ __launch_bounds__(128) void p256_verify_keyed_wave_kernel(
     const uint8_t* __restrict__ digest, const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint8_t* __restrict__ rr, const uint8_t* __restrict__ ss,
     const uint32_t* __restrict__ key, const uint4* const* __restrict__ keytab, uint32_t nkeys,
     uint8_t* __restrict__ ok, uint32_t n) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    __shared__ u32 w_lds[8];
     inv::stage_divstep_table(dtab);
     const uint32_t t = blockIdx.x;
-    const u32 lane = threadIdx.x;
-    if (t >= n) return;  // uniform per wave
+    const u32 lane = threadIdx.x & 63u;
+    const u32 wave = threadIdx.x >> 6;
+    if (t >= n) return;  // uniform per workgroup
 
+    const fe r = load_be32(rr + 32ull * t);
+    const fe s = load_be32(ss + 32ull * t);
+    const uint32_t kid = key[t];
+    const bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
+                       kid >= 1 && kid < nkeys;
     fe e_raw;
-    if (digest) {
+    if (wave == 1) {
+        // w = s^-1 (plain)
+        fe sv = s, w;
+        if (!valid) {
+            sv = fe_zero();
+            sv.v[0] = 1;
+        }
+        inv::inv_mod_n(w.v, sv.v, dtab);
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w_lds[k] = w.v[k];
+    } else if (digest) {
         e_raw = load_be32(digest + 32ull * t);
     } else {
         uint32_t h[8];
@@ -309,23 +331,11 @@ __global__ __launch_bounds__(64) void p256_verify_keyed_wave_kernel(
 #pragma unroll
         for (int k = 0; k < 8; ++k) e_raw.v[k] = h[7 - k];
     }
-    const fe r = load_be32(rr + 32ull * t);
-    const fe s = load_be32(ss + 32ull * t);
-    const uint32_t kid = key[t];
-    const bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
-                       kid >= 1 && kid < nkeys;
-
-    // w = s^-1 (plain), then u1 = e w, u2 = r w (plain, canonical)
+    __syncthreads();
+    if (wave == 1) return;
     fe w;
-    {
-        fe sv = s;
-        if (!valid) {
-            sv = fe_zero();
-            sv.v[0] = 1;
-        }
-        // wave-uniform: the compiler runs it on the scalar unit (~37k cycles, tools/phase_timer.hip)
-        inv::inv_mod_n(w.v, sv.v, dtab);
-    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w.v[k] = w_lds[k];
     fe e, wm, u1, u2;
     fn_canon(e, e_raw);
     fn_mul(wm, w, fe_const(C_R2N));  // w R
@@ -478,7 +488,7 @@ extern "C" int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint
                                              uint8_t* d_ok, uint32_t n, hipStream_t stream) {
     if (n == 0) return 0;
     if (!d_digest && (!d_blob || !d_off || !d_len)) return -1;
-    hipLaunchKernelGGL(sbft::p256_verify_keyed_wave_kernel, dim3(n), dim3(64), 0, stream, d_digest, d_blob, d_off,
+    hipLaunchKernelGGL(sbft::p256_verify_keyed_wave_kernel, dim3(n), dim3(128), 0, stream, d_digest, d_blob, d_off,
                        d_len, d_r, d_s, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
