@@ -435,12 +435,51 @@ SBFT_DEV void p29_add_aff_lean_i(jp29& acc, const f29& x2, const f29& y2) {
     f29_sub(acc.y, t, s2);           // N+-
 }
 
+// dbl-2001-b shape (3M + 5S in the literature) under the signed-limb bounds: 4M + 4S and two
+// more normalisations than p29_dbl_s, i.e. 72 fewer 64-bit mads per doubling.
+//   d = Z^2, g = Y^2, b2 = X (2g) = 2 X Y^2, a' = (X - d)(X + d), al = norm(3 a') (alpha),
+//   X3 = norm(al^2 - 4 b2), Z3 = 2 Y Z, L4 = norm(4 g^2),
+//   Y3 = norm(al (2 b2 - X3) - 2 L4)      [= alpha (4 beta - X3) - 8 gamma^2]
+// In: X in N or N', Y in N' or N+-, Z in N. Out: X3, Y3 in N', Z3 in N. Z = 0 maps to Z3 = 0.
+SBFT_DEV void p29_dbl_b(jp29& r, const jp29& p) {
+    f29 d, g, t0, t1, a1, al, b2, m, l;
+    f29_sqr(d, p.z);                 // 2^29.2^2
+    f29_sqr(g, p.y);
+    f29_add(t0, g, g);               // 2g < 2^30
+    f29_mul(b2, p.x, t0);            // 2^29.2 x 2^30
+    f29_sub(t1, p.x, d);             // |.| < 2^29.2
+    f29_add(a1, p.x, d);             // < 2^30.1
+    f29_mul(a1, t1, a1);             // a' (2^29.2 x 2^30.1)
+    f29_muls(al, a1, 3);             // 3a' < 2^30.6, |3a'| < 2^259.6
+    f29_normalize(al, al);           // alpha (N')
+    f29_add(t1, p.y, p.y);           // 2Y < 2^30.2
+    f29_mul(r.z, t1, p.z);           // Z3 = 2YZ (2^30.2 x 2^29.2)
+    f29_sqr(m, al);                  // alpha^2 (2^29.2^2)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t1.v[i] = m.v[i] - (b2.v[i] << 2);  // (-2^31, 2^29)
+    f29_normalize(r.x, t1);          // X3 (N')
+    f29_sqr(l, g);                   // gamma^2 (N)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) l.v[i] <<= 2;                      // 4L < 2^31
+    f29_normalize(l, l);             // 4L (N')
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t0.v[i] = (b2.v[i] << 1) - r.x.v[i];  // (-2^29.2, 2^30 + 2^26)
+    f29_mul(m, al, t0);              // alpha (2 b2 - X3) (2^29.2 x 2^30.1)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t1.v[i] = m.v[i] - (l.v[i] << 1);   // (-2^30.2, 2^29 + 2^27)
+    f29_normalize(r.y, t1);          // Y3 (N')
+}
+
 #ifndef SBFT_F29_IL
 #define SBFT_F29_IL 6
 #endif
 // SBFT_F29_IL bit 0/1/2: interleaved form of the doubling / Jacobian addition / mixed addition
+#ifndef SBFT_DBL_FORM
+#define SBFT_DBL_FORM 1  // 0: 6M + 2S (p29_dbl_s / _i), 1: 4M + 4S (p29_dbl_b)
+#endif
 SBFT_DEV void p29_dbl(jp29& r, const jp29& p) {
-    if (SBFT_F29_IL & 1) p29_dbl_i(r, p);
+    if (SBFT_DBL_FORM == 1) p29_dbl_b(r, p);
+    else if (SBFT_F29_IL & 1) p29_dbl_i(r, p);
     else p29_dbl_s(r, p);
 }
 SBFT_DEV void p29_add_jac_lean(jp29& acc, const jp29& b) {

@@ -421,7 +421,7 @@ constexpr int kQWin = SBFT_QWIN;                    // u2 in radix 2^w
 constexpr int kQTab = 1 << (kQWin - 1);             // [1, 3, ..., 2^w - 1]Q
 constexpr int kQDigits = (255 + kQWin - 1) / kQWin; // windows over u2 >> 1 (< 2^255)
 #ifndef SBFT_VERIFY_WAVES
-#define SBFT_VERIFY_WAVES 2
+#define SBFT_VERIFY_WAVES 4
 #endif
 __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(const uint8_t* __restrict__ digest,
                                                           const uint8_t* __restrict__ rr,
