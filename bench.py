@@ -158,6 +158,26 @@ def latency_configs(gv, calls: int):
                                   "verifies_per_s": round(10_000 / (p50 / 1e3)),
                                   "python_wrapper_p50_ms": _pcts(tp)[0],
                                   "path": "sbft_verifier_verify_proposal (C ABI), host buffers, PCIe incl."}
+    # the same proposals with the 10k client keys registered (sbft_verifier_add_clients): every
+    # request takes the keyed comb-table launch (no doublings, one wavefront per signature)
+    vr = plugin.Verifier(gv, 1)
+    t0 = time.perf_counter()
+    vr.add_clients([q[-129:-64] for q in reqs])
+    reg_s = time.perf_counter() - t0
+    assert vr.VerifyProposal(prop) == v.VerifyProposal(prop)
+    ts = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        rc = vr.L.sbft_verifier_verify_proposal(vr.h, ctypes.byref(cprop), infos, cap, ctypes.byref(count),
+                                                ctypes.byref(bad), err, 512)
+        ts.append(time.perf_counter() - t0)
+        assert rc == 0 and count.value == 10_000, (rc, err.value)
+    p50, p99 = _pcts(ts)
+    out["verify_proposal_10k_registered_clients"] = {
+        "p50_ms": p50, "p99_ms": p99, "calls": calls, "requests": 10_000,
+        "registration_s": round(reg_s, 2), "client_tables_GB": round(10_000 * 512 * 1024 / 1e9, 2),
+        "path": "sbft_verifier_verify_proposal with the clients' keys registered (keyed launch), host buffers"}
+    vr.close()
     # n = 100 replicas: q = 67 signatures per decision
     import hashlib
     q, f = plugin.compute_quorum(100)

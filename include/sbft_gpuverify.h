@@ -122,6 +122,11 @@ int sbft_gv_sign_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_d, const v
  * fail verification: use the unkeyed calls, which reject it). Registering the same key
  * twice returns the same id. Ids start at 1. */
 int sbft_gv_register_key(sbft_gv_ctx* ctx, const uint8_t qx[32], const uint8_t qy[32], uint32_t* key_id);
+/* Batch form: n keys (qx, qy: n x 32 bytes big-endian), their comb tables built in one launch
+ * per device (a client-key registry: 10,000 keys = 5 GB of tables). key_ids[i] receives the
+ * key's id, or 0 if it is not a point on the curve. Keys registered before keep their id.
+ * Returns a negative SBFT_GV_E* only on an engine failure (nothing is registered then). */
+int sbft_gv_register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy, size_t n, uint32_t* key_ids);
 
 /* Verify n tuples (digest, r, s) against registered keys key_id[k]. Same verdict semantics
  * as sbft_gv_verify_p256 (an unknown key id verifies false). Small batches run one

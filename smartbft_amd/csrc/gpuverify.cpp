@@ -14,6 +14,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <unordered_map>
 #include <new>
 #include <vector>
 
@@ -59,7 +60,8 @@ struct Slot {
     // registered-key comb tables (p256_keyed.hip): comb[id] is key id's table on this device,
     // comb[0] the generator's; d_keytab mirrors comb for the kernels. Tables never move; a
     // grown pointer array retires the old one only at destroy (kernels may still read it).
-    std::vector<void*> comb;
+    std::vector<void*> comb;        // per key id (nullptr for an invalid key)
+    std::vector<void*> comb_alloc;  // the allocations holding them (one per build batch)
     void** d_keytab = nullptr;
     size_t keytab_cap = 0;
     std::vector<void*> retired;
@@ -135,6 +137,16 @@ struct sbft_gv_ctx {
     // registered public keys (x || y big-endian); index = key id, entry 0 = the generator
     std::mutex keys_mu;
     std::vector<std::array<uint8_t, 64>> keys;
+    std::vector<uint8_t> key_valid;  // 1 if keys[i] is a point on the curve
+    struct KeyHash {
+        size_t operator()(const std::array<uint8_t, 64>& k) const {
+            uint64_t a, b;
+            std::memcpy(&a, k.data() + 24, 8);  // low words of x and y: uniformly distributed
+            std::memcpy(&b, k.data() + 56, 8);
+            return (size_t)(a * 0x9E3779B97F4A7C15ull ^ b);
+        }
+    };
+    std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_index;
     std::atomic<uint32_t> nkeys{1};
 };
 
@@ -185,6 +197,7 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     std::array<uint8_t, 64> g;
     std::memcpy(g.data(), GXY, 64);
     ctx->keys.push_back(g);
+    ctx->key_valid.push_back(1);
     *out = ctx;
     return SBFT_GV_OK;
 }
@@ -198,8 +211,7 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
         (void)hipSetDevice(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         if (s->dbuf) (void)hipFree(s->dbuf);
-        for (void* t : s->comb)
-            if (t) (void)hipFree(t);
+        for (void* t : s->comb_alloc) (void)hipFree(t);
         if (s->d_keytab) (void)hipFree(s->d_keytab);
         for (void* t : s->retired) (void)hipFree(t);
         if (s->pin) (void)hipHostFree(s->pin);
@@ -579,36 +591,45 @@ int sbft_gv_sha256_verify_p256(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blo
 // ---------------------------------------------------------------- registered keys
 namespace {
 
-// Build the comb tables of keys [sl->comb.size(), upto) on sl's device and refresh its device
-// pointer array. Caller holds sl->mu. valid_out (optional) receives the last key's status.
-int build_tables(Slot* sl, const std::vector<std::array<uint8_t, 64>>& keys, size_t upto, bool* valid_out) {
+// Build the comb tables of keys [sl->comb.size(), upto) on sl's device in one launch (one
+// allocation for the batch) and refresh its device pointer array. Caller holds sl->mu.
+// status_out (optional) receives one validity byte per built key.
+int build_tables(Slot* sl, const std::vector<std::array<uint8_t, 64>>& keys, size_t upto,
+                 std::vector<uint8_t>* status_out) {
     HIPCHK(hipSetDevice(sl->device));
-    const size_t tb = sbft_comb_table_bytes();
-    if (sl->comb.size() >= upto) return SBFT_GV_OK;
-    uint8_t* tmp = nullptr;  // qx | qy | status
-    HIPCHK(hipMalloc(&tmp, 256));
-    int rc = SBFT_GV_OK;
-    while (sl->comb.size() < upto && rc == SBFT_GV_OK) {
-        const size_t id = sl->comb.size();
-        void* t = nullptr;
-        if (hipMalloc(&t, tb) != hipSuccess) {
-            rc = SBFT_GV_ENOMEM;
-            break;
-        }
-        uint32_t st = 0;
-        if (hipMemcpyAsync(tmp, keys[id].data(), 64, hipMemcpyHostToDevice, sl->stream) != hipSuccess ||
-            sbft_launch_comb_build(tmp, tmp + 32, t, (uint32_t*)(tmp + 64), sl->stream) ||
-            hipMemcpyAsync(&st, tmp + 64, 4, hipMemcpyDeviceToHost, sl->stream) != hipSuccess ||
-            hipStreamSynchronize(sl->stream) != hipSuccess) {
-            (void)hipFree(t);
-            rc = SBFT_GV_EDEVICE;
-            break;
-        }
-        sl->comb.push_back(t);
-        if (valid_out) *valid_out = st == 1;
+    const size_t have = sl->comb.size();
+    if (status_out) status_out->clear();
+    if (have >= upto) return SBFT_GV_OK;
+    const size_t nk = upto - have, tb = sbft_comb_table_bytes();
+    void* block = nullptr;
+    if (hipMalloc(&block, nk * tb) != hipSuccess) return SBFT_GV_ENOMEM;
+    uint8_t* tmp = nullptr;  // qx[nk] | qy[nk] | status[nk]
+    if (hipMalloc(&tmp, nk * 68) != hipSuccess) {
+        (void)hipFree(block);
+        return SBFT_GV_ENOMEM;
     }
+    std::vector<uint8_t> h(nk * 64);
+    for (size_t i = 0; i < nk; ++i) {
+        std::memcpy(&h[32 * i], keys[have + i].data(), 32);
+        std::memcpy(&h[32 * (nk + i)], keys[have + i].data() + 32, 32);
+    }
+    std::vector<uint32_t> st(nk);
+    int rc = SBFT_GV_OK;
+    if (hipMemcpyAsync(tmp, h.data(), nk * 64, hipMemcpyHostToDevice, sl->stream) != hipSuccess ||
+        sbft_launch_comb_build(tmp, tmp + 32 * nk, block, (uint32_t*)(tmp + 64 * nk), (uint32_t)nk, sl->stream) ||
+        hipMemcpyAsync(st.data(), tmp + 64 * nk, 4 * nk, hipMemcpyDeviceToHost, sl->stream) != hipSuccess ||
+        hipStreamSynchronize(sl->stream) != hipSuccess)
+        rc = SBFT_GV_EDEVICE;
     (void)hipFree(tmp);
-    if (rc) return rc;
+    if (rc) {
+        (void)hipFree(block);
+        return rc;
+    }
+    sl->comb_alloc.push_back(block);
+    for (size_t i = 0; i < nk; ++i)
+        sl->comb.push_back(st[i] == 1 ? (void*)((uint8_t*)block + i * tb) : nullptr);
+    if (status_out)
+        for (uint32_t v : st) status_out->push_back(v == 1 ? 1 : 0);
     if (sl->keytab_cap < sl->comb.size()) {
         if (sl->d_keytab) sl->retired.push_back(sl->d_keytab);
         sl->d_keytab = nullptr;
@@ -753,44 +774,68 @@ int sign_wave(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_
 
 extern "C" {
 
-int sbft_gv_register_key(sbft_gv_ctx* ctx, const uint8_t qx[32], const uint8_t qy[32], uint32_t* key_id) {
-    if (!ctx || !qx || !qy || !key_id) return SBFT_GV_EINVAL;
-    *key_id = 0;
-    std::array<uint8_t, 64> k;
-    std::memcpy(k.data(), qx, 32);
-    std::memcpy(k.data() + 32, qy, 32);
+int sbft_gv_register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy, size_t n, uint32_t* key_ids) {
+    if (!ctx || (n && (!qx || !qy || !key_ids)) || n > 0xffffffu) return SBFT_GV_EINVAL;
     std::lock_guard<std::mutex> g(ctx->keys_mu);
-    for (size_t i = 1; i < ctx->keys.size(); ++i)
-        if (ctx->keys[i] == k) {
-            *key_id = (uint32_t)i;
-            return SBFT_GV_OK;
+    const size_t before = ctx->keys.size();
+    std::vector<size_t> pending;  // positions i whose key is new in this call
+    for (size_t i = 0; i < n; ++i) {
+        std::array<uint8_t, 64> k;
+        std::memcpy(k.data(), qx + 32 * i, 32);
+        std::memcpy(k.data() + 32, qy + 32 * i, 32);
+        auto it = ctx->key_index.find(k);
+        if (it != ctx->key_index.end()) {
+            key_ids[i] = it->second;  // resolved below for keys added by this call
+            continue;
         }
-    ctx->keys.push_back(k);
+        const uint32_t id = (uint32_t)ctx->keys.size();
+        ctx->key_index.emplace(k, id);
+        ctx->keys.push_back(k);
+        ctx->key_valid.push_back(0);
+        key_ids[i] = id;
+        pending.push_back(i);
+    }
     const size_t upto = ctx->keys.size();
     int rc = SBFT_GV_OK;
-    for (Slot* sl : ctx->slots) {
+    std::vector<uint8_t> st;
+    for (size_t si = 0; si < ctx->slots.size() && rc == SBFT_GV_OK; ++si) {
+        Slot* sl = ctx->slots[si];
         std::lock_guard<std::mutex> lk(sl->mu);
-        bool valid = true;
-        rc = build_tables(sl, ctx->keys, upto, &valid);
-        if (rc == SBFT_GV_OK && !valid) rc = SBFT_GV_EINVAL;
-        if (rc) break;
+        std::vector<uint8_t> sst;
+        rc = build_tables(sl, ctx->keys, upto, &sst);
+        // a device that had not built G's table yet built [0, upto): keep this call's tail
+        if (rc == SBFT_GV_OK && sl->comb.size() == upto && sst.size() >= upto - before)
+            st.assign(sst.end() - (upto - before), sst.end());
     }
+    if (rc == SBFT_GV_OK && st.size() != upto - before && upto > before) rc = SBFT_GV_EDEVICE;
     if (rc) {
-        // roll the key back on every device that built it
+        // forget this call's keys everywhere (tables of the batch are freed with their block)
         for (Slot* sl : ctx->slots) {
             std::lock_guard<std::mutex> lk(sl->mu);
-            if (sl->comb.size() == upto) {
+            if (sl->comb.size() > before) {
                 (void)hipSetDevice(sl->device);
-                (void)hipFree(sl->comb.back());
-                sl->comb.pop_back();
+                (void)hipFree(sl->comb_alloc.back());
+                sl->comb_alloc.pop_back();
+                sl->comb.resize(before);
             }
         }
-        ctx->keys.pop_back();
+        for (size_t id = before; id < upto; ++id) ctx->key_index.erase(ctx->keys[id]);
+        ctx->keys.resize(before);
+        ctx->key_valid.resize(before);
         return rc;
     }
+    for (size_t id = before; id < upto; ++id) ctx->key_valid[id] = st[id - before];
     ctx->nkeys = (uint32_t)upto;
-    *key_id = (uint32_t)(upto - 1);
+    for (size_t i = 0; i < n; ++i)
+        if (!ctx->key_valid[key_ids[i]]) key_ids[i] = 0;
     return SBFT_GV_OK;
+}
+
+int sbft_gv_register_key(sbft_gv_ctx* ctx, const uint8_t qx[32], const uint8_t qy[32], uint32_t* key_id) {
+    if (!ctx || !qx || !qy || !key_id) return SBFT_GV_EINVAL;
+    const int rc = sbft_gv_register_keys(ctx, qx, qy, 1, key_id);
+    if (rc) return rc;
+    return *key_id ? SBFT_GV_OK : SBFT_GV_EINVAL;
 }
 
 int sbft_gv_verify_p256_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* r, const uint8_t* s,

@@ -49,16 +49,19 @@ SBFT_DEV void to_affine_mont(fe& x, fe& y, const jp& p) {
     fp_canon(y, y);
 }
 
-// One lane per table entry (w, j): j * 2^(8w) * Q. status[0] = 1 iff Q is a valid key
-// (canonical coordinates on the curve); the table is written either way.
-__global__ __launch_bounds__(256) void p256_comb_build_kernel(const uint8_t* __restrict__ qxb,
-                                                              const uint8_t* __restrict__ qyb,
-                                                              uint4* __restrict__ table,
-                                                              uint32_t* __restrict__ status) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= COMB_WINDOWS * COMB_ENTRIES) return;
+// One lane per table entry (key, w, j): j * 2^(8w) * Q_key, for nk keys whose tables lie
+// contiguously from `tables` (COMB_KEY_U4 uint4 each). status[key] = 1 iff Q_key is a valid key
+// (canonical coordinates on the curve); the table is written either way (zeros if invalid).
+__global__ __launch_bounds__(256) void p256_comb_build_kernel(const uint8_t* __restrict__ qxs,
+                                                              const uint8_t* __restrict__ qys,
+                                                              uint4* __restrict__ tables,
+                                                              uint32_t* __restrict__ status, uint32_t nk) {
+    const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t key = (uint32_t)(gt / (COMB_WINDOWS * COMB_ENTRIES));
+    if (key >= nk) return;
+    const uint32_t t = (uint32_t)(gt % (COMB_WINDOWS * COMB_ENTRIES));
     const uint32_t w = t / COMB_ENTRIES, j = t % COMB_ENTRIES;
-    const fe qx = load_be32(qxb), qy = load_be32(qyb);
+    const fe qx = load_be32(qxs + 32ull * key), qy = load_be32(qys + 32ull * key);
     bool valid = fe_lt(qx, P256_P) && fe_lt(qy, P256_P);
     const fe r2p = fe_const(C_R2P);
     jp base;
@@ -78,8 +81,8 @@ __global__ __launch_bounds__(256) void p256_comb_build_kernel(const uint8_t* __r
         fp_canon(rhs, rhs);
         valid = valid && fe_eq(lhs, rhs);
     }
-    if (t == 0) status[0] = valid ? 1u : 0u;
-    uint4* out = table + (size_t)t * COMB_ENTRY_U4;
+    if (t == 0) status[key] = valid ? 1u : 0u;
+    uint4* out = tables + (size_t)key * COMB_KEY_U4 + (size_t)t * COMB_ENTRY_U4;
     if (!valid || j == 0) {
         const uint4 z = make_uint4(0, 0, 0, 0);
         out[0] = z;
@@ -309,8 +312,9 @@ __global__ __launch_bounds__(128) void p256_verify_keyed_wave_kernel(
     const fe r = load_be32(rr + 32ull * t);
     const fe s = load_be32(ss + 32ull * t);
     const uint32_t kid = key[t];
+    // an invalid registered key has a null table pointer
     const bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
-                       kid >= 1 && kid < nkeys;
+                       kid >= 1 && kid < nkeys && keytab[kid] != nullptr;
     fe e_raw;
     if (wave == 1) {
         // w = s^-1 (plain)
@@ -472,11 +476,13 @@ extern "C" int sbft_launch_p256_sign_wave(const uint8_t* d_d, const uint8_t* d_k
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int sbft_launch_comb_build(const uint8_t* d_qx, const uint8_t* d_qy, void* d_table,
-                                      uint32_t* d_status, hipStream_t stream) {
-    const unsigned threads = 256, blocks = (COMB_WINDOWS * COMB_ENTRIES) / threads;
-    hipLaunchKernelGGL(sbft::p256_comb_build_kernel, dim3(blocks), dim3(threads), 0, stream, d_qx, d_qy,
-                       (uint4*)d_table, d_status);
+extern "C" int sbft_launch_comb_build(const uint8_t* d_qx, const uint8_t* d_qy, void* d_tables,
+                                      uint32_t* d_status, uint32_t nk, hipStream_t stream) {
+    if (nk == 0) return 0;
+    const unsigned threads = 256;
+    const uint64_t total = (uint64_t)nk * COMB_WINDOWS * COMB_ENTRIES;
+    hipLaunchKernelGGL(sbft::p256_comb_build_kernel, dim3((unsigned)(total / threads)), dim3(threads), 0, stream,
+                       d_qx, d_qy, (uint4*)d_tables, d_status, nk);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

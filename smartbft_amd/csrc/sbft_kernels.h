@@ -52,8 +52,8 @@ size_t sbft_comb_table_bytes(void);
 int sbft_launch_p256_sign_wave(const uint8_t* d_d, const uint8_t* d_k, const uint8_t* d_e,
                                const void* const* d_keytab, uint8_t* d_qx, uint8_t* d_qy, uint8_t* d_r,
                                uint8_t* d_s, uint8_t* d_status, uint32_t n, hipStream_t stream);
-int sbft_launch_comb_build(const uint8_t* d_qx, const uint8_t* d_qy, void* d_table, uint32_t* d_status,
-                           hipStream_t stream);
+int sbft_launch_comb_build(const uint8_t* d_qx, const uint8_t* d_qy, void* d_tables, uint32_t* d_status,
+                           uint32_t nk, hipStream_t stream);
 // Verify n tuples against registered keys: d_key[t] in [1, nkeys) indexes d_keytab (slot 0 = G).
 // Either d_digest (n x 32 B) or the messages (d_blob, d_off, d_len) hashed in the launch.
 int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint8_t* d_blob, const uint64_t* d_off,

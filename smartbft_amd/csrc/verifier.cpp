@@ -370,6 +370,52 @@ bool write_info(char*& w, char* end, const Req::Str& cid, const Req::Str& id) {
     return true;
 }
 
+// Open-addressing map from a 64-byte public key (x || y) to its engine key id: the
+// VerifyProposal lookup runs once per request (10k per proposal), so no per-lookup allocation.
+struct KeyMap {
+    std::vector<std::array<uint8_t, 64>> keys;
+    std::vector<uint32_t> ids;  // 0 = empty slot
+    size_t count = 0;
+    static size_t hash(const uint8_t* k) {
+        uint64_t a, b;
+        std::memcpy(&a, k + 24, 8);  // low words of x and y: uniformly distributed
+        std::memcpy(&b, k + 56, 8);
+        return (size_t)((a * 0x9E3779B97F4A7C15ull) ^ b);
+    }
+    uint32_t find(const uint8_t* k) const {
+        if (ids.empty()) return 0;
+        const size_t mask = ids.size() - 1;
+        for (size_t i = hash(k) & mask;; i = (i + 1) & mask) {
+            if (!ids[i]) return 0;
+            if (std::memcmp(keys[i].data(), k, 64) == 0) return ids[i];
+        }
+    }
+    void put(const uint8_t* k, uint32_t id) {
+        if (2 * (count + 1) > ids.size()) {
+            KeyMap bigger;
+            const size_t cap = std::max<size_t>(64, 2 * ids.size());
+            bigger.keys.resize(cap);
+            bigger.ids.assign(cap, 0);
+            for (size_t i = 0; i < ids.size(); ++i)
+                if (ids[i]) bigger.put(keys[i].data(), ids[i]);
+            *this = std::move(bigger);
+        }
+        const size_t mask = ids.size() - 1;
+        for (size_t i = hash(k) & mask;; i = (i + 1) & mask) {
+            if (!ids[i]) {
+                std::memcpy(keys[i].data(), k, 64);
+                ids[i] = id;
+                ++count;
+                return;
+            }
+            if (std::memcmp(keys[i].data(), k, 64) == 0) {
+                ids[i] = id;
+                return;
+            }
+        }
+    }
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------------- verifier
@@ -383,6 +429,9 @@ struct sbft_verifier {
         uint32_t kid = 0;
     };
     std::unordered_map<uint64_t, KeyEnt> keys;
+    // client-key registry (sbft_verifier_add_clients): request key -> engine key id
+    std::shared_mutex clients_mu;
+    KeyMap clients;
     // Proposal.Digest memo (view.go:435,443,524 recompute it per proposal): exact-content key
     std::mutex memo_mu;
     struct Memo {
@@ -690,6 +739,29 @@ int sbft_verifier_add_consenter(sbft_verifier* v, uint64_t id, const uint8_t pub
     return 0;
 }
 
+int sbft_verifier_add_clients(sbft_verifier* v, const uint8_t* pubkeys65, size_t n) {
+    if (!v || (n && !pubkeys65)) return SBFT_GV_EINVAL;
+    if (!v->ctx) return SBFT_GV_ENODEV;
+    std::vector<uint8_t> qx(32 * n), qy(32 * n);
+    std::vector<uint32_t> ids(n);
+    size_t m = 0;
+    std::vector<size_t> which;
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t* k = pubkeys65 + 65 * i;
+        if (k[0] != 0x04) continue;  // not SEC1 uncompressed: its requests stay on the generic path
+        std::memcpy(&qx[32 * m], k + 1, 32);
+        std::memcpy(&qy[32 * m], k + 33, 32);
+        which.push_back(i);
+        ++m;
+    }
+    const int rc = sbft_gv_register_keys(v->ctx, qx.data(), qy.data(), m, ids.data());
+    if (rc) return rc;
+    std::unique_lock<std::shared_mutex> g(v->clients_mu);
+    for (size_t j = 0; j < m; ++j)
+        if (ids[j]) v->clients.put(pubkeys65 + 65 * which[j] + 1, ids[j]);
+    return 0;
+}
+
 uint64_t sbft_verifier_verification_sequence(const sbft_verifier* v) { return v ? v->vseq.load() : 0; }
 void sbft_verifier_set_verification_sequence(sbft_verifier* v, uint64_t seq) {
     if (v) v->vseq = seq;
@@ -741,14 +813,57 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(SBFT_GV_ENODEV));
         return SBFT_GV_ENODEV;
     }
-    if (n) {
-        // one fused launch: the request bodies are hashed where they lie in the payload
-        const int rc = sbft_gv_sha256_verify_p256(v->ctx, p->payload, p->payload_len, off.data(), len.data(),
-                                                  r.data(), s.data(), qx.data(), qy.data(), n, ok.data(), nullptr);
-        if (rc) {
-            put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
-            return rc;
+    // requests whose key is a registered client key take the keyed launch (comb tables, no
+    // doublings); the rest the generic fused launch. The request bodies are hashed where they
+    // lie in the payload either way.
+    std::vector<uint32_t> kid;
+    size_t nk = 0;
+    {
+        std::shared_lock<std::shared_mutex> g(v->clients_mu);
+        if (v->clients.count) {
+            kid.resize(n);
+            for (size_t i = 0; i < n; ++i) nk += (kid[i] = v->clients.find(reqs[i].pub + 1)) != 0;
         }
+    }
+    int rc = 0;
+    if (n && nk == 0) {
+        rc = sbft_gv_sha256_verify_p256(v->ctx, p->payload, p->payload_len, off.data(), len.data(), r.data(),
+                                        s.data(), qx.data(), qy.data(), n, ok.data(), nullptr);
+    } else if (n) {
+        std::vector<size_t> wk, wg;
+        wk.reserve(nk);
+        wg.reserve(n - nk);
+        for (size_t i = 0; i < n; ++i) (kid[i] ? wk : wg).push_back(i);
+        auto pick64 = [](const std::vector<uint64_t>& a, const std::vector<size_t>& w) {
+            std::vector<uint64_t> o(w.size());
+            for (size_t i = 0; i < w.size(); ++i) o[i] = a[w[i]];
+            return o;
+        };
+        auto pick32 = [](const std::vector<uint32_t>& a, const std::vector<size_t>& w) {
+            std::vector<uint32_t> o(w.size());
+            for (size_t i = 0; i < w.size(); ++i) o[i] = a[w[i]];
+            return o;
+        };
+        auto pickf = [](const std::vector<uint8_t>& a, const std::vector<size_t>& w) {
+            std::vector<uint8_t> o(32 * w.size());
+            for (size_t i = 0; i < w.size(); ++i) std::memcpy(&o[32 * i], &a[32 * w[i]], 32);
+            return o;
+        };
+        std::vector<uint8_t> okk(wk.size()), okg(wg.size());
+        rc = sbft_gv_sha256_verify_p256_keyed(v->ctx, p->payload, p->payload_len, pick64(off, wk).data(),
+                                              pick32(len, wk).data(), pickf(r, wk).data(), pickf(s, wk).data(),
+                                              pick32(kid, wk).data(), wk.size(), okk.data());
+        if (!rc && !wg.empty())
+            rc = sbft_gv_sha256_verify_p256(v->ctx, p->payload, p->payload_len, pick64(off, wg).data(),
+                                            pick32(len, wg).data(), pickf(r, wg).data(), pickf(s, wg).data(),
+                                            pickf(qx, wg).data(), pickf(qy, wg).data(), wg.size(), okg.data(),
+                                            nullptr);
+        for (size_t i = 0; i < wk.size(); ++i) ok[wk[i]] = okk[i];
+        for (size_t i = 0; i < wg.size(); ++i) ok[wg[i]] = okg[i];
+    }
+    if (rc) {
+        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+        return rc;
     }
     for (size_t i = 0; i < n; ++i)
         if (!ok[i]) {

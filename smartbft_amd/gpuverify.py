@@ -21,7 +21,7 @@ EXPORTS = [
     "sbft_gv_normalize_hash", "sbft_gv_normalize_scalar", "sbft_gv_sign_p256", "sbft_gv_sign_p256_dev",
     "sbft_gv_selftest_field", "sbft_gv_verify_workspace_bytes",
     "sbft_gv_register_key", "sbft_gv_verify_p256_keyed", "sbft_gv_sha256_verify_p256_keyed",
-    "sbft_gv_kernel_timing", "sbft_gv_kernel_time",
+    "sbft_gv_kernel_timing", "sbft_gv_kernel_time", "sbft_gv_register_keys",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -78,6 +78,7 @@ def load_library():
     L.sbft_gv_normalize_scalar.argtypes = [_u8p, ctypes.c_size_t, _u8p]
     _u32p = ctypes.POINTER(ctypes.c_uint32)
     L.sbft_gv_register_key.argtypes = [_vp, _u8p, _u8p, _u32p]
+    L.sbft_gv_register_keys.argtypes = [_vp, _u8p, _u8p, ctypes.c_size_t, _u32p]
     L.sbft_gv_verify_p256_keyed.argtypes = [_vp] + [_u8p] * 3 + [_u32p, ctypes.c_size_t, _u8p]
     L.sbft_gv_sha256_verify_p256_keyed.argtypes = [_vp, _u8p, ctypes.c_size_t,
                                                    ctypes.POINTER(ctypes.c_uint64), _u32p, _u8p, _u8p,
@@ -160,6 +161,19 @@ class GpuVerifier:
         kid = ctypes.c_uint32()
         self._check(self.L.sbft_gv_register_key(self.ctx, kx, ky, ctypes.byref(kid)), "sbft_gv_register_key")
         return kid.value
+
+    def register_keys(self, qx, qy) -> np.ndarray:
+        """Batch registration (one table-build launch per device): key ids, 0 for invalid keys."""
+        n = len(qx)
+        if n and isinstance(qx[0], (bytes, bytearray)):
+            qx = np.frombuffer(b"".join(qx), dtype=np.uint8).reshape(n, 32)
+            qy = np.frombuffer(b"".join(qy), dtype=np.uint8).reshape(n, 32)
+        ax, ay = _soa(qx, n), _soa(qy, n)
+        ids = np.zeros(n, dtype=np.uint32)
+        self._check(self.L.sbft_gv_register_keys(self.ctx, _p(ax), _p(ay), n,
+                                                 ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))),
+                    "sbft_gv_register_keys")
+        return ids
 
     def verify_keyed(self, digest, r, s, key_ids) -> np.ndarray:
         n = len(digest)

@@ -116,6 +116,7 @@ def _lib():
     L.sbft_verifier_free.argtypes = [_vp]
     L.sbft_verifier_free.restype = None
     L.sbft_verifier_add_consenter.argtypes = [_vp, ctypes.c_uint64, _u8p]
+    L.sbft_verifier_add_clients.argtypes = [_vp, _u8p, ctypes.c_size_t]
     L.sbft_verifier_verification_sequence.restype = ctypes.c_uint64
     L.sbft_verifier_verification_sequence.argtypes = [_vp]
     L.sbft_verifier_set_verification_sequence.argtypes = [_vp, ctypes.c_uint64]
@@ -223,6 +224,14 @@ class Verifier:
     def add_consenter(self, node_id: int, pubkey65: bytes):
         keep = []
         assert self.L.sbft_verifier_add_consenter(self.h, node_id, _buf(pubkey65, keep)) == 0
+
+    def add_clients(self, pubkeys65: list[bytes]):
+        """Register client keys: their requests take the keyed (comb-table) launch."""
+        keep = []
+        blob = b"".join(pubkeys65)
+        rc = self.L.sbft_verifier_add_clients(self.h, _buf(blob, keep), len(pubkeys65))
+        if rc:
+            raise VerifyError(rc, "client key registration failed")
 
     def VerificationSequence(self) -> int:
         return self.L.sbft_verifier_verification_sequence(self.h)

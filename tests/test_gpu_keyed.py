@@ -45,7 +45,12 @@ def test_register_key_validation(gpu):
     with pytest.raises(GpuVerifyError):
         gpu.register_key(bytes(32), bytes(32))      # (0, 0) is not on the curve
     qx2, qy2 = oracle.pubkey(999)
-    assert gpu.register_key(qx2, qy2) == k1 + 1    # a rejected key consumes no id
+    k2 = gpu.register_key(qx2, qy2)
+    assert k2 > k1
+    # batch registration: known keys keep their id, invalid ones map to 0, new ones get ids
+    qx3, qy3 = oracle.pubkey(4242)
+    ids = gpu.register_keys([qx, _be(P + 3), qx3, qx3], [qy, qy, qy3, qy3])
+    assert ids[0] == k1 and ids[1] == 0 and ids[2] > k2 and ids[3] == ids[2]
 
 
 def _register_all(gpu, f):

@@ -273,3 +273,27 @@ def test_request_batcher_coalesces_concurrent_callers(net):
     assert b.VerifyRequest(reqs[0]).ID == "fw0"
     assert b.stats() == (launches + 1, 65)
     b.close()
+
+
+# ---- client-key registry: VerifyProposal on the keyed launch ------------------------------
+def test_verify_proposal_registered_clients(gpu, net):
+    """With the clients' keys registered (sbft_verifier_add_clients), VerifyProposal verifies
+    their requests on the comb-table launch: same RequestInfos, same rejection (index and text)
+    as the generic path; a mix of registered and unregistered clients is split over both."""
+    _, nodes, clients = net
+    v = plugin.Verifier(gpu, 3)
+    p, reqs = _proposal(clients, 120)
+    generic = v.VerifyProposal(p)
+    v.add_clients([c.public_key() for c in clients[:5]] + [b"\x04" + b"\x01" * 64])  # last: off-curve
+    assert v.VerifyProposal(p) == generic
+    bad, _ = _proposal(clients, 120, tamper=41)   # client 41 % 8 = 1: registered
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(bad)
+    assert ei.value.index == 41 and "has an invalid signature" in str(ei.value)
+    bad, _ = _proposal(clients, 120, tamper=46)   # client 6: not registered
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(bad)
+    assert ei.value.index == 46
+    v.add_clients([c.public_key() for c in clients])  # all registered (re-registering is a no-op)
+    assert v.VerifyProposal(p) == generic
+    v.close()
