@@ -1,7 +1,9 @@
 /*
  * p256_oracle.c — plain-C restatement of Go 1.24.1 crypto/ecdsa.Verify (P-256)
  * and crypto/sha256. TEST INFRASTRUCTURE ONLY (see oracle.h for the provenance,
- * the pinning story and who may load this).
+ * the pinning story and who may load this). Parity unpinned by the reference (it
+ * holds no vectors for this path and Go is absent); cross-checked against OpenSSL
+ * 3.0.2 and Node crypto on every committed fixture.
  *
  * Deliberately simple and independent of the GPU kernels: 4x64-bit limbs,
  * generic CIOS Montgomery multiplication for both p and n, Jacobian points with
