@@ -51,8 +51,13 @@ typedef struct sbft_gv_ctx sbft_gv_ctx;
 typedef struct sbft_gv_opts {
     uint32_t device_mask;   /* bit d selects HIP device d; 0 = all visible devices */
     uint32_t min_split;     /* batches smaller than this stay on one device (0 = default 65536) */
-    uint64_t reserved[4];
+    int32_t pair_max;       /* per-device batches of at most this many tuples run the latency kernel
+                               (two lanes per tuple); 0 = default SBFT_GV_PAIR_MAX_DEFAULT, < 0 = never */
+    uint32_t reserved32;
+    uint64_t reserved[3];
 } sbft_gv_opts;
+
+#define SBFT_GV_PAIR_MAX_DEFAULT 32768u
 
 /* Create a context (per-device stream + device/pinned staging grown on demand).
  * opts may be NULL. Replaces: the plugin construction a Go app does before handing its

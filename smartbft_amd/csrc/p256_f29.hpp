@@ -491,6 +491,138 @@ SBFT_DEV void p29_add_aff_lean(jp29& acc, const f29& x2, const f29& y2) {
     else p29_add_aff_lean_s(acc, x2, y2);
 }
 
+// ---------------------------------------------------------------- lane pairs (latency kernel)
+// p256_verify_pair_kernel runs one verify on two adjacent lanes (2t, 2t+1). Both hold the
+// same point; at each step the two lanes compute two independent products of the formula,
+// each with its own operands (f29_pick), and f29_unpair hands both results to both lanes
+// (two quad_perm DPP moves per limb). A doubling is 4 such steps instead of 8 products, a
+// mixed addition 6 instead of 11: the per-lane instruction stream of a small batch, which is
+// what its latency is, shrinks by ~40%.
+//
+// With one product per lane per step there is no second product to interleave with, and a
+// product column is a chain of dependent 64-bit mads (a wait state each on gfx950). So the
+// pair forms use f29_mul_ilp / f29_sqr_ilp: the 17 product columns are summed first as
+// independent chains, then the Montgomery pass adds carry and reduction terms column by column
+// (one extra 64-bit add per column, no wait states in the product part).
+template <bool SQ>
+SBFT_DEV void f29_mulsq_ilp(f29& r, const f29& a, const f29& b) {
+    const f29_red K = f29_red_consts();
+    u32 d[9];
+    if (SQ)
+#pragma unroll
+        for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
+    i64 col[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) col[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int k = 0; k < 17; ++k) {
+            const int j = k - i;
+            if (SQ) {
+                if (j > i && j <= 8) col[k] = smad(a.v[i], d[j], col[k]);
+                if (j == i) col[k] = smad(a.v[i], a.v[i], col[k]);
+            } else {
+                if (j >= 0 && j <= 8) col[k] = smad(a.v[i], b.v[j], col[k]);
+            }
+        }
+    // Reduction terms first (m[k-3..] are ready columns ahead), the carry last: the serial
+    // chain is one 64-bit add and one shift per column.
+    u32 m[9];
+    i64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+        i64 x = col[k];
+        if (k >= 3 && k - 3 <= 8) x = smad(m[k - 3], K.c9, x);
+        if (k >= 6 && k - 6 <= 8) x = smad(m[k - 6], K.c18, x);
+        if (k >= 7 && k - 7 <= 8) x = smad(m[k - 7], K.c7, x);
+        if (k >= 8 && k - 8 <= 8) x = smad(m[k - 8], K.c8, x);
+        acc = k == 0 ? x : x + acc;
+        if (k < 9) m[k] = lo29(acc);
+        else r.v[k - 9] = lo29(acc);
+        acc = sar29(acc);
+    }
+    r.v[8] = (u32)acc;
+}
+SBFT_DEV void f29_mul_ilp(f29& r, const f29& a, const f29& b) { f29_mulsq_ilp<false>(r, a, b); }
+SBFT_DEV void f29_sqr_ilp(f29& r, const f29& a) { f29_mulsq_ilp<true>(r, a, a); }
+
+SBFT_DEV f29 f29_pick(bool odd, const f29& even_v, const f29& odd_v) {
+    f29 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = odd ? odd_v.v[i] : even_v.v[i];
+    return r;
+}
+// o = the even lane's value in the even lane, the odd lane's in the odd lane ->
+// e = even lane's value, d = odd lane's value, in both lanes of the pair.
+SBFT_DEV void f29_unpair(const f29& o, f29& e, f29& d) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        e.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)o.v[i], 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
+        d.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)o.v[i], 0xF5, 0xF, 0xF, false);  // quad_perm [1,1,3,3]
+    }
+}
+
+// p29_dbl_b on a lane pair (same products, same bounds):
+//   1: d = Z^2 | g = Y^2     2: b2 = X (2g) | a' = (X - d)(X + d)
+//   3: alpha^2 | gamma^2     4: alpha (2 b2 - X3) | Z3 = 2 Y Z
+SBFT_DEV void p29_dbl_pair(jp29& r, const jp29& p, bool odd) {
+    f29 o, d, g, t0, t1, a1, al, b2, m, l, x3, z3;
+    f29_sqr_ilp(o, f29_pick(odd, p.z, p.y));                        // 2^29.2^2
+    f29_unpair(o, d, g);
+    f29_add(t0, g, g);                                          // 2g < 2^30
+    f29_sub(t1, p.x, d);                                        // |.| < 2^29.2
+    f29_add(a1, p.x, d);                                        // < 2^30.1
+    f29_mul_ilp(o, f29_pick(odd, p.x, t1), f29_pick(odd, t0, a1));  // 2^29.2 x 2^30 | 2^29.2 x 2^30.1
+    f29_unpair(o, b2, a1);
+    f29_muls(al, a1, 3);                                        // 3a' < 2^30.6
+    f29_normalize(al, al);                                      // alpha (N')
+    f29_sqr_ilp(o, f29_pick(odd, al, g));                           // 2^29.2^2
+    f29_unpair(o, m, l);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t1.v[i] = m.v[i] - (b2.v[i] << 2);  // (-2^31, 2^29)
+    f29_normalize(x3, t1);                                      // X3 (N')
+#pragma unroll
+    for (int i = 0; i < 9; ++i) l.v[i] <<= 2;                  // 4L < 2^31
+    f29_normalize(l, l);                                        // 4L (N')
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t0.v[i] = (b2.v[i] << 1) - x3.v[i];  // (-2^29.2, 2^30 + 2^26)
+    f29_add(t1, p.y, p.y);                                      // 2Y < 2^30.2
+    f29_mul_ilp(o, f29_pick(odd, al, t1), f29_pick(odd, t0, p.z));  // 2^29.2 x 2^30.1 | 2^30.2 x 2^29.2
+    f29_unpair(o, m, z3);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t1.v[i] = m.v[i] - (l.v[i] << 1);  // (-2^30.2, 2^29 + 2^27)
+    f29_normalize(r.y, t1);                                     // Y3 (N')
+    r.x = x3;
+    r.z = z3;
+}
+
+// p29_add_aff_lean on a lane pair (same products, same bounds, no case analysis):
+//   1: Z1^2 (both)          2: U2 = x2 Z1^2 | Z1^3     3: HH = H^2 | S2 = y2 Z1^3
+//   4: V = X1 HH | HHH      5: r^2 | Z3 = Z1 H          6: r (V - X3) | Y1 HHH
+SBFT_DEV void p29_add_aff_pair(jp29& acc, const f29& x2, const f29& y2, bool odd) {
+    f29 o, z1z1, u2, s2, h, rr, hh, hhh, v, r2, z3, t, s;
+    f29_sqr_ilp(z1z1, acc.z);
+    f29_mul_ilp(o, f29_pick(odd, x2, acc.z), z1z1);
+    f29_unpair(o, u2, s2);
+    f29_sub(h, u2, acc.x);                                      // (-2^29.2, 2^29 + 2^26)
+    f29_mul_ilp(o, f29_pick(odd, h, y2), f29_pick(odd, h, s2));
+    f29_unpair(o, hh, s2);
+    f29_sub(rr, s2, acc.y);                                     // (-2^29.2, 2^29.2)
+    f29_mul_ilp(o, f29_pick(odd, acc.x, hh), f29_pick(odd, hh, h));
+    f29_unpair(o, v, hhh);
+    f29_mul_ilp(o, f29_pick(odd, rr, acc.z), f29_pick(odd, rr, h));
+    f29_unpair(o, r2, z3);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] = r2.v[i] - hhh.v[i] - (v.v[i] << 1);  // (-3 2^29, 2^29)
+    f29_normalize(acc.x, t);
+    f29_sub(t, v, acc.x);                                       // (-2^29.2, 2^29 + 2^26)
+    f29_mul_ilp(o, f29_pick(odd, rr, acc.y), f29_pick(odd, t, hhh));
+    f29_unpair(o, t, s);
+    f29_sub(acc.y, t, s);                                       // N+-
+    acc.z = z3;
+}
+
 // ---------------------------------------------------------------- co-Z table building
 // Odd multiples [1, 3, ..., 2^w - 1]Q with Meloni's co-Z additions (2007): every point of the
 // chain shares the Z of the running 2Q, so an addition costs 4M + 2S and only the Z ratios

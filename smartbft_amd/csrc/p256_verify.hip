@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256) void p256_gcomb_build_kernel(uint4* __restrict
     e[4] = make_uint4(my.v[6], my.v[7], my.v[8], 0u);
 }
 
-// ------------------------------------------------------------ the kernel
+// ------------------------------------------------------------ the kernels
 #ifndef SBFT_DBL_UNROLL
 #define SBFT_DBL_UNROLL 1
 #endif
@@ -423,108 +423,91 @@ constexpr int kQDigits = (255 + kQWin - 1) / kQWin; // windows over u2 >> 1 (< 2
 #ifndef SBFT_VERIFY_WAVES
 #define SBFT_VERIFY_WAVES 4
 #endif
-__global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(const uint8_t* __restrict__ digest,
-                                                          const uint8_t* __restrict__ rr,
-                                                          const uint8_t* __restrict__ ss,
-                                                          const uint8_t* __restrict__ qxx,
-                                                          const uint8_t* __restrict__ qyy,
-                                                          uint8_t* __restrict__ ok, uint32_t n,
-                                                          uint32_t* __restrict__ work, sinv_ws ws,
-                                                          const uint4* __restrict__ gcomb) {
-    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
-    inv::stage_divstep_table(dtab);  // ends with a barrier
-    const int tid = threadIdx.x;
 
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool active = gid < n;
-    const uint32_t idx = active ? gid : (n - 1);
-
-    const fe e_raw = load_be32(digest + 32ull * idx);
-    const fe r = load_be32(rr + 32ull * idx);
-    const fe s = load_be32(ss + 32ull * idx);
-    const fe qx = load_be32(qxx + 32ull * idx);
-    const fe qy = load_be32(qyy + 32ull * idx);
-
-    // 1. range checks
+// 1. range checks and the on-curve check y^2 == x^3 - 3x + b (8 x 32 Montgomery domain)
+SBFT_DEV bool verify_inputs_valid(const fe& r, const fe& s, const fe& qx, const fe& qy) {
     bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
                  fe_lt(qx, P256_P) && fe_lt(qy, P256_P);
+    const fe r2p = fe_const(C_R2P);
+    fe x, y, lhs, rhs, t;
+    fp_mul(x, qx, r2p);
+    fp_mul(y, qy, r2p);
+    fp_sqr(lhs, y);
+    fp_sqr(rhs, x);
+    fp_mul(rhs, rhs, x);
+    fp_add(t, x, x);
+    fp_add(t, t, x);
+    fp_sub(rhs, rhs, t);
+    fp_add(rhs, rhs, fe_const(C_BM));
+    fp_canon(lhs, lhs);
+    fp_canon(rhs, rhs);
+    return valid && fe_eq(lhs, rhs);
+}
 
-    // on-curve check y^2 == x^3 - 3x + b (8 x 32 Montgomery domain, once per verify)
-    {
-        const fe r2p = fe_const(C_R2P);
-        fe x, y, lhs, rhs, t;
-        fp_mul(x, qx, r2p);
-        fp_mul(y, qy, r2p);
-        fp_sqr(lhs, y);
-        fp_sqr(rhs, x);
-        fp_mul(rhs, rhs, x);
-        fp_add(t, x, x);
-        fp_add(t, t, x);
-        fp_sub(rhs, rhs, t);
-        fp_add(rhs, rhs, fe_const(C_BM));
-        fp_canon(lhs, lhs);
-        fp_canon(rhs, rhs);
-        valid = valid && fe_eq(lhs, rhs);
+// The odd multiples [1,3,...,2^w - 1]Q in the radix-2^29 Montgomery domain of the ladder
+// (p256_f29.hpp), affine. Invalid lanes run a harmless stand-in (Q = 2G); their verdict is
+// masked by `valid` at the end. Built with co-Z additions (DBLU, then ZADDU of the running 2Q:
+// 4M + 2S each), then made affine with ONE inversion per lane (safegcd mod p of the final Z;
+// the earlier Z's follow from the recorded ratios h_k).
+SBFT_DEV void build_q_table(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, const fe& qy, bool valid,
+                            const uint32_t* dtab) {
+    const f29 r2 = f29_const(C29_R2);
+    f29 qxm, qym;
+    f29_mul(qxm, f29_from_u256(qx), r2);
+    f29_mul(qym, f29_from_u256(qy), r2);
+    if (!valid) {
+        qxm = f29_const(C29_G2X);
+        qym = f29_const(C29_G2Y);
     }
+    tx[0] = qxm;
+    ty[0] = qym;
+    f29 dx, dy, cx, cy, z;  // D = 2Q and the current odd multiple, co-Z (Z = z)
+    p29_dblu(qxm, qym, dx, dy, cx, cy, z);
+    f29 hs[kQTab - 1];      // Z ratios: Z(T_k) = Z(T_{k-1}) h_k
+#pragma unroll 1
+    for (int k = 1; k < kQTab; ++k) {
+        f29 h;
+        p29_zaddu(cx, cy, dx, dy, h);  // T_k = T_{k-1} + 2Q
+        tx[k] = cx;
+        ty[k] = cy;
+        hs[k - 1] = h;
+        f29_mul(z, z, h);              // 2^30 (first) x 2^29.3
+    }
+    f29 inv;  // 1 / Z(T_last), Montgomery form
+    {
+        const fe zp = f29_canon_plain(z);
+        fe zi;
+        inv::inv_mod_p(zi.v, zp.v, dtab);
+        f29_mul(inv, f29_from_u256(zi), r2);
+    }
+#pragma unroll 1
+    for (int k = kQTab - 1; k >= 1; --k) {
+        f29 zi2, zi3;
+        f29_sqr(zi2, inv);
+        f29_mul(zi3, zi2, inv);
+        f29_mul(tx[k], tx[k], zi2);
+        f29_mul(ty[k], ty[k], zi3);
+        f29_mul(inv, inv, hs[k - 1]);  // 1 / Z(T_{k-1})
+    }
+}
 
-    // Q in the radix-2^29 Montgomery domain of the ladder (p256_f29.hpp). Invalid lanes run a
-    // harmless stand-in (Q = 2G, u1 = u2 = 1); their verdict is masked by `valid` at the end.
-    // The odd multiples [1,3,...,2^w - 1]Q are built with co-Z additions (DBLU, then ZADDU of
-    // the running 2Q: 4M + 2S each), then made affine with ONE inversion per lane (safegcd
-    // mod p of the final Z; the earlier Z's follow from the recorded ratios h_k). Every Q digit
-    // of the ladder is then a mixed addition (8M + 3S).
-    f29 tx[kQTab], ty[kQTab];  // affine odd multiples (scratch)
-    {
-        const f29 r2 = f29_const(C29_R2);
-        f29 qxm, qym;
-        f29_mul(qxm, f29_from_u256(qx), r2);
-        f29_mul(qym, f29_from_u256(qy), r2);
-        if (!valid) {
-            qxm = f29_const(C29_G2X);
-            qym = f29_const(C29_G2Y);
-        }
-        tx[0] = qxm;
-        ty[0] = qym;
-        f29 dx, dy, cx, cy, z;  // D = 2Q and the current odd multiple, co-Z (Z = z)
-        p29_dblu(qxm, qym, dx, dy, cx, cy, z);
-        f29 hs[kQTab - 1];      // Z ratios: Z(T_k) = Z(T_{k-1}) h_k
-#pragma unroll 1
-        for (int k = 1; k < kQTab; ++k) {
-            f29 h;
-            p29_zaddu(cx, cy, dx, dy, h);  // T_k = T_{k-1} + 2Q
-            tx[k] = cx;
-            ty[k] = cy;
-            hs[k - 1] = h;
-            f29_mul(z, z, h);              // 2^30 (first) x 2^29.3
-        }
-        f29 inv;  // 1 / Z(T_last), Montgomery form
-        {
-            const fe zp = f29_canon_plain(z);
-            fe zi;
-            inv::inv_mod_p(zi.v, zp.v, dtab);
-            f29_mul(inv, f29_from_u256(zi), r2);
-        }
-#pragma unroll 1
-        for (int k = kQTab - 1; k >= 1; --k) {
-            f29 zi2, zi3;
-            f29_sqr(zi2, inv);
-            f29_mul(zi3, zi2, inv);
-            f29_mul(tx[k], tx[k], zi2);
-            f29_mul(ty[k], ty[k], zi3);
-            f29_mul(inv, inv, hs[k - 1]);  // 1 / Z(T_{k-1})
-        }
-    }
-    // 3. w = s^-1 from the launch-wide Montgomery trick (see p256_sinv_* kernels)
+// 2-3. w = s^-1 of tuple t from the launch-wide Montgomery trick (p256_sinv_* kernels: 256
+// tuples per scan block), then u1 = e w, u2 = r w, recoded for the signed-odd ladders: an even
+// u becomes n - u with the base negated ((n-u)(-P) = uP); u == 0 becomes n, whose ladder
+// cancels to infinity. Invalid lanes get u1 = u2 = 1.
+SBFT_DEV void verify_scalars(const sinv_ws& ws, uint32_t t, uint32_t n, bool active, bool valid, const fe& e_raw,
+                             const fe& r, fe& u1, fe& u2, bool& neg1, bool& neg2) {
     fe w;
     {
-        const fe kb = ld_fe(ws.kb + 2ull * blockIdx.x);
+        const uint32_t pos = t & 255u;
+        const fe kb = ld_fe(ws.kb + 2ull * (t >> 8));
         const fe one = fe_const(C_ONEN);
-        const fe pre = (tid > 0 && active) ? ld_fe(ws.pre + 2ull * (gid - 1)) : one;
-        const fe suf = (tid < 255 && active && gid + 1 < n) ? ld_fe(ws.suf + 2ull * (gid + 1)) : one;
+        const fe pre = (pos > 0 && active) ? ld_fe(ws.pre + 2ull * (t - 1)) : one;
+        const fe suf = (pos < 255 && active && t + 1 < n) ? ld_fe(ws.suf + 2ull * (t + 1)) : one;
         fn_mul(w, kb, pre);
         fn_mul(w, w, suf);  // s^-1 * R (garbage for lanes whose s is invalid: masked by `valid`)
     }
-    fe e, u1, u2;
+    fe e;
     fn_canon(e, e_raw);
     fn_mul(u1, e, w);  // e*s^-1 (plain)
     fn_mul(u2, r, w);  // r*s^-1 (plain)
@@ -535,126 +518,165 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
         u1.v[0] = 1;
         u2 = u1;
     }
-    // Signed-odd (regular) recoding needs odd scalars: u even -> use n - u with the base
-    // negated ((n-u)(-P) = uP). u == 0 becomes n, whose ladder cancels to infinity.
-    const bool neg1 = (u1.v[0] & 1u) == 0;
-    const bool neg2 = (u2.v[0] & 1u) == 0;
-    {
-        fe t1, t2;
-        u64 b1 = 0, b2 = 0;
+    neg1 = (u1.v[0] & 1u) == 0;
+    neg2 = (u2.v[0] & 1u) == 0;
+    fe t1, t2;
+    u64 b1 = 0, b2 = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const u64 d1 = (u64)P256_N[k] - u1.v[k] - b1;
-            const u64 d2 = (u64)P256_N[k] - u2.v[k] - b2;
-            t1.v[k] = lo32(d1);
-            t2.v[k] = lo32(d2);
-            b1 = d1 >> 63;
-            b2 = d2 >> 63;
-        }
-        fe_sel(u1, neg1, t1);
-        fe_sel(u2, neg2, t2);
+    for (int k = 0; k < 8; ++k) {
+        const u64 d1 = (u64)P256_N[k] - u1.v[k] - b1;
+        const u64 d2 = (u64)P256_N[k] - u2.v[k] - b2;
+        t1.v[k] = lo32(d1);
+        t2.v[k] = lo32(d2);
+        b1 = d1 >> 63;
+        b2 = d2 >> 63;
     }
+    fe_sel(u1, neg1, t1);
+    fe_sel(u2, neg2, t2);
+}
+
+// Radix-2^w signed-odd digit i of u2 (u2 = sum_{i<K} d_i 2^(w i) + 2^(w K),
+// d_i = 2*((u2 >> (w i + 1)) & (2^w - 1)) - (2^w - 1), odd and nonzero).
+SBFT_DEV int q_digit(const fe& k2, int i) {
+    const int b = kQWin * i + 1, lw = b >> 5;
+    const u32 lo = k2.v[lw], hi = lw < 7 ? k2.v[lw + 1] : 0u;
+    return 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & (2 * kQTab - 1)) - (2 * kQTab - 1);
+}
+
+// u1*G by the fixed-base comb in HBM (no doublings): u1 = sum_{i<16} d_i 2^(16 i) + 2^256
+// with d_i = 2*((u1 >> (16 i + 1)) & 0xFFFF) - 0xFFFF (odd, nonzero), i.e. 16 mixed additions
+// of table[i][(|d_i| - 1) / 2] = |d_i| 2^(16 i) G plus one of table[16][0] = 2^256 G.
+// The next entry's five 16-B loads are issued before the current addition. add(acc, x, y) is
+// the mixed addition of the calling kernel.
+template <class AddAff>
+SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __restrict__ gcomb, AddAff add) {
+    fe k1 = u1;
+    uint4 cur[5], nxt[5];
+    int dneg_cur = 0, dneg_nxt = 0;
+    // digit i of u1 -> (entry pointer, negative?)
+    auto digit = [&](int i, const uint4*& ptr, int& neg) {
+        if (i < 16) {
+            const u32 bits = (k1.v[0] >> 1) & 0xFFFFu;  // bits 16i+1 .. 16i+16 (k1 shifted)
+            const int d = 2 * (int)bits - 0xFFFF;
+            const u32 j = (u32)((d < 0 ? -d : d) >> 1);
+            ptr = gcomb + ((size_t)i * SBFT_GCOMB_ENTRIES + j) * 5;
+            neg = d < 0;
+            // k1 >>= 16 for the next window
+#pragma unroll
+            for (int k = 0; k < 7; ++k) k1.v[k] = __builtin_amdgcn_alignbit(k1.v[k + 1], k1.v[k], 16);
+            k1.v[7] >>= 16;
+        } else {
+            ptr = gcomb + (size_t)16 * SBFT_GCOMB_ENTRIES * 5;
+            neg = 0;
+        }
+    };
+    const uint4* ptr;
+    digit(0, ptr, dneg_nxt);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
+#pragma unroll 1
+    for (int i = 0; i < 17; ++i) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) cur[k] = nxt[k];
+        dneg_cur = dneg_nxt;
+        if (i < 16) {
+            digit(i + 1, ptr, dneg_nxt);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
+        }
+        f29 gx, gy;
+        const u32* w = reinterpret_cast<const u32*>(cur);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            gx.v[k] = w[k];
+            gy.v[k] = w[10 + k];
+        }
+        if ((dneg_cur != 0) != neg1) f29_neg(gy, gy);
+        add(acc, gx, gy);
+    }
+}
+
+// 5. The lean additions leave Z = 0 from the first exceptional case on (P + P, P + (-P),
+// R = infinity), so Z == 0 (mod p) flags the tuple for the general path (exc). Otherwise
+// x(R) mod n == r is checked projectively: X == r Z^2 or, when r + n < p, X == (r + n) Z^2.
+SBFT_DEV bool verify_final(const jp29& acc, const fe& rv, bool& exc) {
+    exc = fe_is_zero_raw(f29_canon_plain(acc.z));
+    const f29 r2 = f29_const(C29_R2);
+    f29 z2, lhs, rm;
+    f29_sqr(z2, acc.z);
+    const fe xc = f29_canon_plain(acc.x);
+    f29_mul(rm, f29_from_u256(rv), r2);
+    f29_mul(lhs, rm, z2);
+    bool accept = fe_eq(f29_canon_plain(lhs), xc);
+    // R.x in [n, p): compare with r + n as well when r + n < p
+    fe rn;
+    u64 c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        c = (u64)rv.v[k] + P256_N[k] + c;
+        rn.v[k] = lo32(c);
+        c >>= 32;
+    }
+    if (c == 0 && fe_lt(rn, P256_P)) {
+        f29_mul(rm, f29_from_u256(rn), r2);
+        f29_mul(lhs, rm, z2);
+        accept = accept || fe_eq(f29_canon_plain(lhs), xc);
+    }
+    return accept;
+}
+
+// Throughput kernel: one verify per lane, 256-thread workgroups (one s^-1 scan block each).
+__global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(const uint8_t* __restrict__ digest,
+                                                          const uint8_t* __restrict__ rr,
+                                                          const uint8_t* __restrict__ ss,
+                                                          const uint8_t* __restrict__ qxx,
+                                                          const uint8_t* __restrict__ qyy,
+                                                          uint8_t* __restrict__ ok, uint32_t n,
+                                                          uint32_t* __restrict__ work, sinv_ws ws,
+                                                          const uint4* __restrict__ gcomb) {
+    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    inv::stage_divstep_table(dtab);  // ends with a barrier
+
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = gid < n;
+    const uint32_t idx = active ? gid : (n - 1);
+
+    const fe e_raw = load_be32(digest + 32ull * idx);
+    const fe r = load_be32(rr + 32ull * idx);
+    const fe s = load_be32(ss + 32ull * idx);
+    const fe qx = load_be32(qxx + 32ull * idx);
+    const fe qy = load_be32(qyy + 32ull * idx);
+    const bool valid = verify_inputs_valid(r, s, qx, qy);
+
+    f29 tx[kQTab], ty[kQTab];  // affine odd multiples (scratch)
+    build_q_table(tx, ty, qx, qy, valid, dtab);
+    fe u1, u2;
+    bool neg1, neg2;
+    verify_scalars(ws, gid, n, active, valid, e_raw, r, u1, u2, neg1, neg2);
+
     jp29 acc;  // reloaded from scratch: keeps q out of registers during the setup
     acc.x = tx[0];
     acc.y = ty[0];
     acc.z = f29_const(C29_ONE);
     if (neg2) f29_neg(acc.y, acc.y);
-    // u2 = sum_{i<K} d_i 2^(w i) + 2^(w K), d_i = 2*((u2 >> (w i + 1)) & (2^w - 1)) - (2^w - 1)
-    // (odd, nonzero), K = ceil(255 / w): the accumulator starts at +-Q (the 2^(wK) term).
-    fe k2 = u2;
+    // the accumulator starts at +-Q (the 2^(wK) term of u2)
+    const fe k2 = u2;
 #pragma unroll 1
     for (int i = kQDigits - 1; i >= 0; --i) {
 #pragma unroll kDblUnroll
         for (int d = 0; d < kQWin; ++d) p29_dbl(acc, acc);
-        const int b = kQWin * i + 1, lw = b >> 5;
-        const u32 lo = k2.v[lw], hi = lw < 7 ? k2.v[lw + 1] : 0u;
-        const int d2 = 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & (2 * kQTab - 1)) - (2 * kQTab - 1);
+        const int d2 = q_digit(k2, i);
         const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
         const f29 x2 = tx[m2];
         f29 y2 = ty[m2];
         if ((d2 < 0) != neg2) f29_neg(y2, y2);
         p29_add_aff_lean(acc, x2, y2);
     }
-    // u1*G by the fixed-base comb in HBM (no doublings): u1 = sum_{i<16} d_i 2^(16 i) + 2^256
-    // with d_i = 2*((u1 >> (16 i + 1)) & 0xFFFF) - 0xFFFF (odd, nonzero), i.e. 16 mixed
-    // additions of table[i][(|d_i| - 1) / 2] = |d_i| 2^(16 i) G plus one of table[16][0] = 2^256 G.
-    // The next entry's five 16-B loads are issued before the current addition.
-    {
-        fe k1 = u1;
-        uint4 cur[5], nxt[5];
-        int dneg_cur = 0, dneg_nxt = 0;
-        // digit i of u1 -> (entry pointer, negative?)
-        auto digit = [&](int i, const uint4*& ptr, int& neg) {
-            if (i < 16) {
-                const u32 bits = (k1.v[0] >> 1) & 0xFFFFu;  // bits 16i+1 .. 16i+16 (k1 shifted)
-                const int d = 2 * (int)bits - 0xFFFF;
-                const u32 j = (u32)((d < 0 ? -d : d) >> 1);
-                ptr = gcomb + ((size_t)i * SBFT_GCOMB_ENTRIES + j) * 5;
-                neg = d < 0;
-                // k1 >>= 16 for the next window
-#pragma unroll
-                for (int k = 0; k < 7; ++k) k1.v[k] = __builtin_amdgcn_alignbit(k1.v[k + 1], k1.v[k], 16);
-                k1.v[7] >>= 16;
-            } else {
-                ptr = gcomb + (size_t)16 * SBFT_GCOMB_ENTRIES * 5;
-                neg = 0;
-            }
-        };
-        const uint4* ptr;
-        digit(0, ptr, dneg_nxt);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
-#pragma unroll 1
-        for (int i = 0; i < 17; ++i) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) cur[k] = nxt[k];
-            dneg_cur = dneg_nxt;
-            if (i < 16) {
-                digit(i + 1, ptr, dneg_nxt);
-#pragma unroll
-                for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
-            }
-            f29 gx, gy;
-            const u32* w = reinterpret_cast<const u32*>(cur);
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                gx.v[k] = w[k];
-                gy.v[k] = w[10 + k];
-            }
-            if ((dneg_cur != 0) != neg1) f29_neg(gy, gy);
-            p29_add_aff_lean(acc, gx, gy);
-        }
-    }
+    comb_add_u1g(acc, u1, neg1, gcomb,
+                 [](jp29& a, const f29& x, const f29& y) { p29_add_aff_lean(a, x, y); });
 
-    // 5. The lean additions leave Z = 0 from the first exceptional case on (P + P, P + (-P),
-    // R = infinity), so Z == 0 (mod p) flags the tuple for the general path. Otherwise
-    // x(R) mod n == r is checked projectively: X == r Z^2 or, when r + n < p, X == (r + n) Z^2.
-    const bool exc = fe_is_zero_raw(f29_canon_plain(acc.z));
-    bool accept;
-    {
-        const fe rv = load_be32(rr + 32ull * idx);  // reload: keeps r out of the loop's registers
-        const f29 r2 = f29_const(C29_R2);
-        f29 z2, lhs, rm;
-        f29_sqr(z2, acc.z);
-        const fe xc = f29_canon_plain(acc.x);
-        f29_mul(rm, f29_from_u256(rv), r2);
-        f29_mul(lhs, rm, z2);
-        accept = fe_eq(f29_canon_plain(lhs), xc);
-        // R.x in [n, p): compare with r + n as well when r + n < p
-        fe rn;
-        u64 c = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            c = (u64)rv.v[k] + P256_N[k] + c;
-            rn.v[k] = lo32(c);
-            c >>= 32;
-        }
-        if (c == 0 && fe_lt(rn, P256_P)) {
-            f29_mul(rm, f29_from_u256(rn), r2);
-            f29_mul(lhs, rm, z2);
-            accept = accept || fe_eq(f29_canon_plain(lhs), xc);
-        }
-    }
+    bool exc;
+    const bool accept = verify_final(acc, load_be32(rr + 32ull * idx), exc);  // r reloaded
     if (active) {
         if (exc && valid) {
             const uint32_t slot = atomicAdd(work, 1u);
@@ -665,6 +687,99 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     }
 }
 
+// Latency kernel for small batches (sbft_launch_p256_verify with pair = true): one verify on
+// two adjacent lanes, the doublings and mixed additions split between them (p29_dbl_pair,
+// p29_add_aff_pair). A batch of a few thousand tuples gives each busy SIMD one wave, so the
+// launch takes one wave's instruction stream; the pair form cuts that stream by ~40% at the
+// price of twice the lanes. Setup (checks, Q table, scalars) and the final comparison run
+// redundantly on both lanes. The Q table lives in LDS (one copy per pair). One wavefront per
+// workgroup (32 tuples) spreads a small batch over as many CUs as possible.
+constexpr int kPairTuples = 32;  // tuples per 64-lane workgroup
+__global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __restrict__ digest,
+                                                              const uint8_t* __restrict__ rr,
+                                                              const uint8_t* __restrict__ ss,
+                                                              const uint8_t* __restrict__ qxx,
+                                                              const uint8_t* __restrict__ qyy,
+                                                              uint8_t* __restrict__ ok, uint32_t n,
+                                                              uint32_t* __restrict__ work, sinv_ws ws,
+                                                              const uint4* __restrict__ gcomb) {
+    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    // [entry][x limbs 0..8, y limbs 0..8][pair]: the two lanes of a pair read the same word,
+    // the 32 pairs of the wave 32 consecutive words
+    __shared__ u32 qtab[kQTab * 18 * kPairTuples];
+    inv::stage_divstep_table(dtab);  // ends with a barrier
+
+    const int pr = threadIdx.x >> 1;
+    const bool odd = (threadIdx.x & 1) != 0;
+    const uint32_t t = blockIdx.x * kPairTuples + pr;
+    const bool active = t < n;
+    const uint32_t idx = active ? t : (n - 1);
+
+    const fe e_raw = load_be32(digest + 32ull * idx);
+    const fe r = load_be32(rr + 32ull * idx);
+    const fe s = load_be32(ss + 32ull * idx);
+    const fe qx = load_be32(qxx + 32ull * idx);
+    const fe qy = load_be32(qyy + 32ull * idx);
+    const bool valid = verify_inputs_valid(r, s, qx, qy);
+    {
+        f29 tx[kQTab], ty[kQTab];
+        build_q_table(tx, ty, qx, qy, valid, dtab);
+#pragma unroll
+        for (int m = 0; m < kQTab; ++m)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {  // both lanes store the same words
+                qtab[(m * 18 + k) * kPairTuples + pr] = tx[m].v[k];
+                qtab[(m * 18 + 9 + k) * kPairTuples + pr] = ty[m].v[k];
+            }
+    }
+    __syncthreads();
+    fe u1, u2;
+    bool neg1, neg2;
+    verify_scalars(ws, t, n, active, valid, e_raw, r, u1, u2, neg1, neg2);
+
+    jp29 acc;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        acc.x.v[k] = qtab[k * kPairTuples + pr];
+        acc.y.v[k] = qtab[(9 + k) * kPairTuples + pr];
+    }
+    acc.z = f29_const(C29_ONE);
+    if (neg2) f29_neg(acc.y, acc.y);
+    const fe k2 = u2;
+#ifndef SBFT_PAIR_LADDER_DIGITS  // development: time the phases (tools/pair_probe.py --no-check)
+#define SBFT_PAIR_LADDER_DIGITS kQDigits
+#endif
+#pragma unroll 1
+    for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 0; --i) {
+#pragma unroll
+        for (int d = 0; d < kQWin; ++d) p29_dbl_pair(acc, acc, odd);
+        const int d2 = q_digit(k2, i);
+        const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
+        f29 x2, y2;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            x2.v[k] = qtab[(m2 * 18 + k) * kPairTuples + pr];
+            y2.v[k] = qtab[(m2 * 18 + 9 + k) * kPairTuples + pr];
+        }
+        if ((d2 < 0) != neg2) f29_neg(y2, y2);
+        p29_add_aff_pair(acc, x2, y2, odd);
+    }
+#ifndef SBFT_PAIR_NO_COMB
+    comb_add_u1g(acc, u1, neg1, gcomb,
+                 [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); });
+#endif
+
+    bool exc;
+    const bool accept = verify_final(acc, r, exc);
+    if (active && !odd) {
+        if (exc && valid) {
+            const uint32_t slot = atomicAdd(work, 1u);
+            work[1 + slot] = t;
+        } else {
+            ok[t] = (valid && accept) ? 1 : 0;
+        }
+    }
+}
 }  // namespace sbft
 
 // Workspace layout (sbft_verify_work_bytes): [0, 4(n+1)) fixup counter + list, then the
@@ -674,7 +789,7 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
 extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                        const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
                                        uint32_t n, uint32_t* d_work, const void* d_gcomb, hipStream_t stream,
-                                       hipEvent_t ev0, hipEvent_t ev1) {
+                                       hipEvent_t ev0, hipEvent_t ev1, bool pair) {
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned blocks = (n + threads - 1) / threads;
@@ -704,8 +819,14 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
     hipLaunchKernelGGL(sbft::p256_sinv_totals_kernel, dim3(1), dim3(threads), 0, stream, (uint32_t)blocks, ws);
     SBFT_STEP("totals");
     if (ev0 && hipEventRecord(ev0, stream) != hipSuccess) return -1;
-    hipLaunchKernelGGL(sbft::p256_verify_kernel, dim3(blocks), dim3(threads), 0, stream, d_digest, d_r,
-                       d_s, d_qx, d_qy, d_ok, n, d_work, ws, (const uint4*)d_gcomb);
+    if (pair) {  // two lanes per tuple, 32 tuples per 64-lane workgroup
+        const unsigned pblocks = (n + sbft::kPairTuples - 1) / sbft::kPairTuples;
+        hipLaunchKernelGGL(sbft::p256_verify_pair_kernel, dim3(pblocks), dim3(64), 0, stream, d_digest, d_r,
+                           d_s, d_qx, d_qy, d_ok, n, d_work, ws, (const uint4*)d_gcomb);
+    } else {
+        hipLaunchKernelGGL(sbft::p256_verify_kernel, dim3(blocks), dim3(threads), 0, stream, d_digest, d_r,
+                           d_s, d_qx, d_qy, d_ok, n, d_work, ws, (const uint4*)d_gcomb);
+    }
     if (ev1 && hipEventRecord(ev1, stream) != hipSuccess) return -1;
     SBFT_STEP("verify");
     const unsigned fix_blocks = blocks < 64 ? blocks : 64;

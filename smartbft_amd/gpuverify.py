@@ -34,7 +34,8 @@ class GpuVerifyError(RuntimeError):
 
 class Opts(ctypes.Structure):
     _fields_ = [("device_mask", ctypes.c_uint32), ("min_split", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint64 * 4)]
+                ("pair_max", ctypes.c_int32), ("reserved32", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint64 * 3)]
 
 
 _LIB = None
@@ -117,10 +118,12 @@ class GpuVerifier:
     """One sbft_gv_ctx. Host-array calls are synchronous; *_dev calls take torch tensors
     (device-resident) and enqueue on the given (or current) stream."""
 
-    def __init__(self, device_mask: int = 0, min_split: int = 0):
+    def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0):
+        """pair_max: per-device batches of at most this many tuples run the two-lanes-per-tuple
+        latency kernel (0 = library default, negative = never)."""
         self.L = load_library()
         ctx = _vp()
-        opts = Opts(device_mask, min_split)
+        opts = Opts(device_mask, min_split, pair_max)
         rc = self.L.sbft_gv_init(ctypes.byref(opts), ctypes.byref(ctx))
         if rc:
             raise GpuVerifyError(f"sbft_gv_init: {self.L.sbft_gv_strerror(rc).decode()} ({rc})")

@@ -232,3 +232,43 @@ def test_bench_workload_properties(gpu):
     assert 0.07 < frac < 0.13
     f = wl.host_fields(0, 3000)
     assert np.array_equal(oracle.verify_batch(*f), ok[:3000].cpu().numpy())
+
+
+# ---- both verify kernels at every size: the one-lane throughput kernel (pair_max < 0) and the
+# two-lanes-per-tuple latency kernel (p256_verify_pair_kernel, forced on for big batches)
+@pytest.fixture(scope="module", params=["lane", "pair"])
+def gpu_kernel(request):
+    import torch
+    from smartbft_amd import GpuVerifier
+    assert torch.cuda.is_available(), "gpu-marked test needs a visible MI355X"
+    v = GpuVerifier(pair_max=-1 if request.param == "lane" else (1 << 30))
+    yield v
+    v.close()
+
+
+def test_kernels_golden_vectors(gpu_kernel, p256_vectors):
+    f, exp, cat, names = p256_vectors
+    got = gpu_kernel.verify(*split_fields(f))
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, {names[c]: int((cat[bad] == c).sum()) for c in np.unique(cat[bad])}
+
+
+@pytest.mark.parametrize("n", [1, 2, 31, 32, 33, 255, 256, 257, 4097])
+def test_kernels_ragged_sizes(gpu_kernel, p256_vectors, n):
+    f, exp, cat, names = p256_vectors
+    idx = np.arange(n) * 5 % len(exp)
+    assert np.array_equal(gpu_kernel.verify(*split_fields(f[idx])), exp[idx])
+
+
+def test_kernels_random_batch(gpu_kernel):
+    f = _rand_tuples(2000, seed=23, corrupt_frac=0.3)
+    exp = oracle.verify_batch(*split_fields(f))
+    assert np.array_equal(gpu_kernel.verify(*split_fields(f)), exp)
+
+
+def test_kernels_large_tiled(gpu_kernel, p256_vectors):
+    """Many waves per SIMD for both kernels: 64 tiled copies of the fixtures (209k tuples)."""
+    f, exp, cat, names = p256_vectors
+    reps = 64
+    got = gpu_kernel.verify(*split_fields(np.tile(f, (reps, 1))))
+    assert np.array_equal(got.reshape(reps, -1), np.tile(exp, (reps, 1)))
