@@ -65,8 +65,9 @@ struct s30 {
 #define SBFT_PINV30 0x3fffffffu
 
 // The modulus of an inversion: P = false for the group order n, true for the field prime p.
-template <bool P>
-SBFT_HD void mod30(int32_t m[9]) {
+// P is a run-time flag so that the two lanes of a verify pair can invert mod p and mod n in
+// the same instruction stream (p256_verify_pair_kernel); constant P folds away when inlined.
+SBFT_HD void mod30(int32_t m[9], bool P) {
     const int32_t N30[9] = SBFT_N30_INIT, P30[9] = SBFT_P30_INIT;
     for (int i = 0; i < 9; ++i) m[i] = P ? P30[i] : N30[i];
 }
@@ -138,10 +139,9 @@ SBFT_HD void update_fg(s30& f, s30& g, int32_t u, int32_t v, int32_t q, int32_t 
 // (d, e) <- (T (d, e) + (md, me) m) / 2^30 with md, me chosen to clear the low 30 bits
 // (m = n, or p when P). |d|, |e| grow by at most m per batch (|u| + |v| <= 2^30), so 25
 // batches stay below 2^262.
-template <bool P>
-SBFT_HD void update_de(s30& d, s30& e, int32_t u, int32_t v, int32_t q, int32_t r) {
+SBFT_HD void update_de(s30& d, s30& e, int32_t u, int32_t v, int32_t q, int32_t r, bool P) {
     int32_t N30[9];
-    mod30<P>(N30);
+    mod30(N30, P);
     const uint32_t minv = P ? SBFT_PINV30 : SBFT_NINV30;
     int64_t cd = mac(mac(0, u, d.v[0]), v, e.v[0]);
     int64_t ce = mac(mac(0, q, d.v[0]), r, e.v[0]);
@@ -170,10 +170,9 @@ SBFT_HD bool is_zero30(const s30& a) {
 }
 
 // a += k * m for a small signed k (m = n, or p when P), renormalising limbs 0..7 to [0, 2^30)
-template <bool P>
-SBFT_HD void add_kn(s30& a, int32_t k) {
+SBFT_HD void add_kn(s30& a, int32_t k, bool P) {
     int32_t N30[9];
-    mod30<P>(N30);
+    mod30(N30, P);
     int64_t c = 0;
     for (int i = 0; i < 8; ++i) {
         c += (int64_t)a.v[i] + (int64_t)k * N30[i];
@@ -184,14 +183,13 @@ SBFT_HD void add_kn(s30& a, int32_t k) {
 }
 
 // a (normalised, |a| < 2^262) -> [0, m), then 8 x 32-bit limbs
-template <bool P>
-SBFT_HD void reduce_unpack(uint32_t out[8], s30 a) {
+SBFT_HD void reduce_unpack(uint32_t out[8], s30 a, bool P) {
     // a = t * 2^240 + low with t = a.v[8]; m = 2^256 - c with c < 2^225 (n: c < 2^128), so
     // k = -floor(a / 2^256) gets within a few m of [0, m)
-    add_kn<P>(a, -(a.v[8] >> 16));
-    for (int it = 0; it < 4 && a.v[8] < 0; ++it) add_kn<P>(a, 1);
+    add_kn(a, -(a.v[8] >> 16), P);
+    for (int it = 0; it < 4 && a.v[8] < 0; ++it) add_kn(a, 1, P);
     int32_t N30[9];
-    mod30<P>(N30);
+    mod30(N30, P);
     for (int it = 0; it < 4; ++it) {
         // a >= n ?
         bool ge = true;
@@ -202,7 +200,7 @@ SBFT_HD void reduce_unpack(uint32_t out[8], s30 a) {
             }
         }
         if (!ge) break;
-        add_kn<P>(a, -1);
+        add_kn(a, -1, P);
     }
     for (int w = 0; w < 8; ++w) {
         const int bit = 32 * w, i = bit / 30, sh = bit % 30;
@@ -215,10 +213,9 @@ SBFT_HD void reduce_unpack(uint32_t out[8], s30 a) {
 
 // out = x^-1 mod m for 0 < x < m (8 x 32-bit little-endian limbs; m = n, or p when P).
 // x = 0 gives 0. tab: SBFT_DIVSTEP5_TABLE (p256_inv_table.inc).
-template <bool P>
-SBFT_HD void inv_mod(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) {
+SBFT_HD void inv_mod(uint32_t out[8], const uint32_t x[8], const uint32_t* tab, bool P) {
     s30 f, g, d, e;
-    mod30<P>(f.v);
+    mod30(f.v, P);
     pack30(g, x);
     for (int i = 0; i < 9; ++i) {
         d.v[i] = 0;
@@ -230,18 +227,18 @@ SBFT_UNROLL1
     for (int batch = 0; batch < 26 && !is_zero30(g); ++batch) {
         int32_t u, v, q, r;
         delta = divsteps30(delta, (uint32_t)f.v[0], (uint32_t)g.v[0], tab, u, v, q, r);
-        update_de<P>(d, e, u, v, q, r);
+        update_de(d, e, u, v, q, r, P);
         update_fg(f, g, u, v, q, r);
     }
     // f = +-1: x^-1 = f * d
     if (f.v[8] < 0) {
         for (int i = 0; i < 9; ++i) d.v[i] = -d.v[i];
-        add_kn<P>(d, 0);  // renormalise limbs
+        add_kn(d, 0, P);  // renormalise limbs
     }
-    reduce_unpack<P>(out, d);
+    reduce_unpack(out, d, P);
 }
-SBFT_HD void inv_mod_n(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) { inv_mod<false>(out, x, tab); }
-SBFT_HD void inv_mod_p(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) { inv_mod<true>(out, x, tab); }
+SBFT_HD void inv_mod_n(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) { inv_mod(out, x, tab, false); }
+SBFT_HD void inv_mod_p(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) { inv_mod(out, x, tab, true); }
 
 #if defined(__HIPCC__)
 __device__ __constant__ static const uint32_t C_DIVSTEP5[SBFT_DIVSTEP5_WORDS] = SBFT_DIVSTEP5_TABLE;

@@ -449,8 +449,10 @@ SBFT_DEV bool verify_inputs_valid(const fe& r, const fe& s, const fe& qx, const 
 // masked by `valid` at the end. Built with co-Z additions (DBLU, then ZADDU of the running 2Q:
 // 4M + 2S each), then made affine with ONE inversion per lane (safegcd mod p of the final Z;
 // the earlier Z's follow from the recorded ratios h_k).
+// inv_p(z) returns z^-1 mod p (plain 8 x 32 limbs) for the plain canonical z.
+template <class InvP>
 SBFT_DEV void build_q_table(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, const fe& qy, bool valid,
-                            const uint32_t* dtab) {
+                            InvP inv_p) {
     const f29 r2 = f29_const(C29_R2);
     f29 qxm, qym;
     f29_mul(qxm, f29_from_u256(qx), r2);
@@ -475,9 +477,7 @@ SBFT_DEV void build_q_table(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, co
     }
     f29 inv;  // 1 / Z(T_last), Montgomery form
     {
-        const fe zp = f29_canon_plain(z);
-        fe zi;
-        inv::inv_mod_p(zi.v, zp.v, dtab);
+        const fe zi = inv_p(f29_canon_plain(z));
         f29_mul(inv, f29_from_u256(zi), r2);
     }
 #pragma unroll 1
@@ -495,18 +495,20 @@ SBFT_DEV void build_q_table(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, co
 // tuples per scan block), then u1 = e w, u2 = r w, recoded for the signed-odd ladders: an even
 // u becomes n - u with the base negated ((n-u)(-P) = uP); u == 0 becomes n, whose ladder
 // cancels to infinity. Invalid lanes get u1 = u2 = 1.
-SBFT_DEV void verify_scalars(const sinv_ws& ws, uint32_t t, uint32_t n, bool active, bool valid, const fe& e_raw,
-                             const fe& r, fe& u1, fe& u2, bool& neg1, bool& neg2) {
+SBFT_DEV fe sinv_from_ws(const sinv_ws& ws, uint32_t t, uint32_t n, bool active) {
     fe w;
-    {
-        const uint32_t pos = t & 255u;
-        const fe kb = ld_fe(ws.kb + 2ull * (t >> 8));
-        const fe one = fe_const(C_ONEN);
-        const fe pre = (pos > 0 && active) ? ld_fe(ws.pre + 2ull * (t - 1)) : one;
-        const fe suf = (pos < 255 && active && t + 1 < n) ? ld_fe(ws.suf + 2ull * (t + 1)) : one;
-        fn_mul(w, kb, pre);
-        fn_mul(w, w, suf);  // s^-1 * R (garbage for lanes whose s is invalid: masked by `valid`)
-    }
+    const uint32_t pos = t & 255u;
+    const fe kb = ld_fe(ws.kb + 2ull * (t >> 8));
+    const fe one = fe_const(C_ONEN);
+    const fe pre = (pos > 0 && active) ? ld_fe(ws.pre + 2ull * (t - 1)) : one;
+    const fe suf = (pos < 255 && active && t + 1 < n) ? ld_fe(ws.suf + 2ull * (t + 1)) : one;
+    fn_mul(w, kb, pre);
+    fn_mul(w, w, suf);  // s^-1 * R (garbage for lanes whose s is invalid: masked by `valid`)
+    return w;
+}
+// w = s^-1 R mod n (Montgomery form)
+SBFT_DEV void verify_scalars(const fe& w, bool valid, const fe& e_raw, const fe& r, fe& u1, fe& u2, bool& neg1,
+                             bool& neg2) {
     fe e;
     fn_canon(e, e_raw);
     fn_mul(u1, e, w);  // e*s^-1 (plain)
@@ -596,6 +598,31 @@ SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __re
     }
 }
 
+// Latency path: one 4-byte load from each cache line of the 17 comb entries u1 selects,
+// issued before the Q ladder, so that the comb additions after it find the lines (and their
+// pages) cached instead of paying an HBM miss per dependent step. The caller consumes the
+// returned word after the ladder.
+SBFT_DEV u32 comb_touch(const fe& u1, const uint4* __restrict__ gcomb) {
+    fe k1 = u1;
+    u32 acc = 0;
+    const u32* base = reinterpret_cast<const u32*>(gcomb);
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+        size_t e;
+        if (i < 16) {
+            const int d = 2 * (int)((k1.v[0] >> 1) & 0xFFFFu) - 0xFFFF;
+            e = (size_t)i * SBFT_GCOMB_ENTRIES + (u32)((d < 0 ? -d : d) >> 1);
+#pragma unroll
+            for (int k = 0; k < 7; ++k) k1.v[k] = __builtin_amdgcn_alignbit(k1.v[k + 1], k1.v[k], 16);
+            k1.v[7] >>= 16;
+        } else {
+            e = (size_t)16 * SBFT_GCOMB_ENTRIES;
+        }
+        acc ^= base[e * 20] ^ base[e * 20 + 19];  // first and last word of the 80-B entry
+    }
+    return acc;
+}
+
 // 5. The lean additions leave Z = 0 from the first exceptional case on (P + P, P + (-P),
 // R = infinity), so Z == 0 (mod p) flags the tuple for the general path (exc). Otherwise
 // x(R) mod n == r is checked projectively: X == r Z^2 or, when r + n < p, X == (r + n) Z^2.
@@ -649,10 +676,14 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     const bool valid = verify_inputs_valid(r, s, qx, qy);
 
     f29 tx[kQTab], ty[kQTab];  // affine odd multiples (scratch)
-    build_q_table(tx, ty, qx, qy, valid, dtab);
+    build_q_table(tx, ty, qx, qy, valid, [&](const fe& zp) {
+        fe zi;
+        inv::inv_mod_p(zi.v, zp.v, dtab);
+        return zi;
+    });
     fe u1, u2;
     bool neg1, neg2;
-    verify_scalars(ws, gid, n, active, valid, e_raw, r, u1, u2, neg1, neg2);
+    verify_scalars(sinv_from_ws(ws, gid, n, active), valid, e_raw, r, u1, u2, neg1, neg2);
 
     jp29 acc;  // reloaded from scratch: keeps q out of registers during the setup
     acc.x = tx[0];
@@ -701,7 +732,7 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
                                                               const uint8_t* __restrict__ qxx,
                                                               const uint8_t* __restrict__ qyy,
                                                               uint8_t* __restrict__ ok, uint32_t n,
-                                                              uint32_t* __restrict__ work, sinv_ws ws,
+                                                              uint32_t* __restrict__ work,
                                                               const uint4* __restrict__ gcomb) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     // [entry][x limbs 0..8, y limbs 0..8][pair]: the two lanes of a pair read the same word,
@@ -721,9 +752,26 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
     const fe qx = load_be32(qxx + 32ull * idx);
     const fe qy = load_be32(qyy + 32ull * idx);
     const bool valid = verify_inputs_valid(r, s, qx, qy);
+    // The table's one inversion mod p (even lane) and s^-1 mod n (odd lane) run as one safegcd
+    // instruction stream; no launch-wide s^-1 batching kernels in front of this one.
+    fe s_inv;  // plain s^-1 mod n (1 for an invalid s: masked by `valid`)
     {
         f29 tx[kQTab], ty[kQTab];
-        build_q_table(tx, ty, qx, qy, valid, dtab);
+        build_q_table(tx, ty, qx, qy, valid, [&](const fe& zp) {
+            fe x = zp, y, zi;
+            if (odd) {
+                x = fe_zero();
+                x.v[0] = 1;
+                if (valid) x = s;
+            }
+            inv::inv_mod(y.v, x.v, dtab, !odd);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                zi.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)y.v[k], 0xA0, 0xF, 0xF, false);     // even lane's
+                s_inv.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)y.v[k], 0xF5, 0xF, 0xF, false);  // odd lane's
+            }
+            return zi;
+        });
 #pragma unroll
         for (int m = 0; m < kQTab; ++m)
 #pragma unroll
@@ -735,7 +783,14 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
     __syncthreads();
     fe u1, u2;
     bool neg1, neg2;
-    verify_scalars(ws, t, n, active, valid, e_raw, r, u1, u2, neg1, neg2);
+    {
+        fe w;
+        fn_mul(w, s_inv, fe_const(C_R2N));  // s^-1 R
+        verify_scalars(w, valid, e_raw, r, u1, u2, neg1, neg2);
+    }
+#ifndef SBFT_PAIR_NO_TOUCH
+    const u32 touch = comb_touch(u1, gcomb);
+#endif
 
     jp29 acc;
 #pragma unroll
@@ -764,6 +819,9 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
         if ((d2 < 0) != neg2) f29_neg(y2, y2);
         p29_add_aff_pair(acc, x2, y2, odd);
     }
+#ifndef SBFT_PAIR_NO_TOUCH
+    asm volatile("" ::"v"(touch));
+#endif
 #ifndef SBFT_PAIR_NO_COMB
     comb_add_u1g(acc, u1, neg1, gcomb,
                  [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); });
@@ -814,15 +872,18 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
 #endif
     if (hipMemsetAsync(d_work, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     SBFT_STEP("memset");
-    hipLaunchKernelGGL(sbft::p256_sinv_prep_kernel, dim3(blocks), dim3(threads), 0, stream, d_s, n, ws);
-    SBFT_STEP("prep");
-    hipLaunchKernelGGL(sbft::p256_sinv_totals_kernel, dim3(1), dim3(threads), 0, stream, (uint32_t)blocks, ws);
-    SBFT_STEP("totals");
+    if (!pair) {  // the pair kernel inverts s itself
+        hipLaunchKernelGGL(sbft::p256_sinv_prep_kernel, dim3(blocks), dim3(threads), 0, stream, d_s, n, ws);
+        SBFT_STEP("prep");
+        hipLaunchKernelGGL(sbft::p256_sinv_totals_kernel, dim3(1), dim3(threads), 0, stream, (uint32_t)blocks,
+                           ws);
+        SBFT_STEP("totals");
+    }
     if (ev0 && hipEventRecord(ev0, stream) != hipSuccess) return -1;
     if (pair) {  // two lanes per tuple, 32 tuples per 64-lane workgroup
         const unsigned pblocks = (n + sbft::kPairTuples - 1) / sbft::kPairTuples;
         hipLaunchKernelGGL(sbft::p256_verify_pair_kernel, dim3(pblocks), dim3(64), 0, stream, d_digest, d_r,
-                           d_s, d_qx, d_qy, d_ok, n, d_work, ws, (const uint4*)d_gcomb);
+                           d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb);
     } else {
         hipLaunchKernelGGL(sbft::p256_verify_kernel, dim3(blocks), dim3(threads), 0, stream, d_digest, d_r,
                            d_s, d_qx, d_qy, d_ok, n, d_work, ws, (const uint4*)d_gcomb);
