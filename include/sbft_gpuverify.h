@@ -85,6 +85,17 @@ int sbft_gv_sha256_verify_p256(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blo
                                const uint8_t* s, const uint8_t* qx, const uint8_t* qy, size_t n,
                                uint8_t* ok_out, uint8_t* dig_out);
 
+/* Fused hash + verify of framed messages, whose tuples live inside the blob: message k is
+ * blob[off[k], off[k] + len[k]), its signature r || s the 64 bytes at off[k] + len[k] + sig_rel
+ * and its public key x || y the 64 bytes at off[k] + len[k] + pub_rel (both inside the blob,
+ * else SBFT_GV_EINVAL). The device gathers the verify inputs itself, so only the blob and the
+ * offsets cross PCIe. For the signed-request format of sbft_verifier.h (public key at the end
+ * of the signed body, signature right after it): sig_rel = 0, pub_rel = -64.
+ * Replaces: the per-request loop of an api.Verifier's VerifyProposal (pkg/api/dependencies.go:56). */
+int sbft_gv_sha256_verify_p256_framed(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len,
+                                      const uint64_t* off, const uint32_t* len, size_t n, int32_t sig_rel,
+                                      int32_t pub_rel, uint8_t* ok_out);
+
 /* Bytes of device workspace the verify pipeline uses for a batch of n tuples (fixup list +
  * batched-inversion arrays, ~65 B per tuple). The device-resident entry points keep one such
  * workspace per caller stream inside the context. */

@@ -422,15 +422,31 @@ int enqueue_verify(const Chunk& c, const uint8_t* digest, const uint8_t* r, cons
 
 // Hash (and optionally verify) messages [c.begin, +c.count). Offsets are rebased to the
 // chunk's first message so each device receives only its slice of the blob.
+// framed: verify inputs are gathered on the device from the blob itself (r || s at message
+// end + sig_rel, x || y at message end + pub_rel) instead of copied from r, s, qx, qy.
+struct Framing {
+    bool on = false;
+    int32_t sig_rel = 0, pub_rel = 0;
+};
 int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uint64_t* off,
                  const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint8_t* qx,
-                 const uint8_t* qy, uint8_t* ok_out, uint8_t* dig_out, std::vector<uint64_t>& rebased) {
+                 const uint8_t* qy, uint8_t* ok_out, uint8_t* dig_out, std::vector<uint64_t>& rebased,
+                 Framing fr = Framing()) {
     Slot* sl = c.slot;
     uint64_t lo = UINT64_MAX, hi = 0;
     for (size_t k = c.begin; k < c.begin + c.count; ++k) {
-        if (off[k] + len[k] > blob_len) return SBFT_GV_EINVAL;
+        if (off[k] + len[k] > blob_len || off[k] + len[k] < off[k]) return SBFT_GV_EINVAL;
         lo = std::min(lo, off[k]);
         hi = std::max(hi, off[k] + len[k]);
+        if (fr.on) {
+            const int64_t end = (int64_t)(off[k] + len[k]);
+            for (int32_t rel : {fr.sig_rel, fr.pub_rel}) {
+                const int64_t a = end + rel;
+                if (a < 0 || (uint64_t)a + 64 > blob_len) return SBFT_GV_EINVAL;
+                lo = std::min(lo, (uint64_t)a);
+                hi = std::max(hi, (uint64_t)a + 64);
+            }
+        }
     }
     if (c.count == 0) return SBFT_GV_OK;
     rebased.resize(c.count);
@@ -457,10 +473,17 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
         return SBFT_GV_ELAUNCH;
     if (verify) {
         uint8_t* v = d_dig + fd;
-        const uint8_t* src[4] = {r, s, qx, qy};
-        for (int k = 0; k < 4; ++k)
-            HIPCHK(hipMemcpyAsync(v + k * fd, src[k] + 32 * c.begin, 32 * c.count, hipMemcpyHostToDevice,
-                                  sl->stream));
+        if (fr.on) {
+            if (sbft_launch_gather_framed(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len,
+                                          (uint32_t)c.count, fr.sig_rel, fr.pub_rel, v, v + fd, v + 2 * fd,
+                                          v + 3 * fd, sl->stream))
+                return SBFT_GV_ELAUNCH;
+        } else {
+            const uint8_t* src[4] = {r, s, qx, qy};
+            for (int k = 0; k < 4; ++k)
+                HIPCHK(hipMemcpyAsync(v + k * fd, src[k] + 32 * c.begin, 32 * c.count, hipMemcpyHostToDevice,
+                                      sl->stream));
+        }
         uint8_t* d_ok = v + 4 * fd;
         uint32_t* work = (uint32_t*)(d_ok + align_up(c.count, 256));
         const void* gcomb = sl->gcomb_table();
@@ -588,6 +611,23 @@ int sbft_gv_sha256_verify_p256(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blo
     std::vector<std::vector<uint64_t>> rebased(ctx->slots.size() + 1);
     return run_chunks(ctx, n, [&](const Chunk& c, size_t i) {
         return enqueue_hash(c, blob, blob_len, off, len, r, s, qx, qy, ok_out, dig_out, rebased[i]);
+    });
+}
+
+int sbft_gv_sha256_verify_p256_framed(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len,
+                                      const uint64_t* off, const uint32_t* len, size_t n, int32_t sig_rel,
+                                      int32_t pub_rel, uint8_t* ok_out) {
+    if (!ctx) return SBFT_GV_EINVAL;
+    if (n == 0) return SBFT_GV_OK;
+    if (!blob || !off || !len || !ok_out || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    std::vector<std::vector<uint64_t>> rebased(ctx->slots.size() + 1);
+    Framing fr;
+    fr.on = true;
+    fr.sig_rel = sig_rel;
+    fr.pub_rel = pub_rel;
+    return run_chunks(ctx, n, [&](const Chunk& c, size_t i) {
+        return enqueue_hash(c, blob, blob_len, off, len, nullptr, nullptr, nullptr, nullptr, ok_out, nullptr,
+                            rebased[i], fr);
     });
 }
 

@@ -550,7 +550,10 @@ SBFT_DEV int q_digit(const fe& k2, int i) {
 // of table[i][(|d_i| - 1) / 2] = |d_i| 2^(16 i) G plus one of table[16][0] = 2^256 G.
 // The next entry's five 16-B loads are issued before the current addition. add(acc, x, y) is
 // the mixed addition of the calling kernel.
-template <class AddAff>
+// PINGPONG (latency kernel): two entry buffers in fixed registers, loop unrolled by two, so
+// that the next entry's loads are never waited on to shuffle registers (at one wave per SIMD
+// the rotated one-buffer loop exposed an HBM round trip per addition).
+template <bool PINGPONG = false, class AddAff>
 SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __restrict__ gcomb, AddAff add) {
     fe k1 = u1;
     uint4 cur[5], nxt[5];
@@ -573,6 +576,35 @@ SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __re
         }
     };
     const uint4* ptr;
+    if (PINGPONG) {
+        auto add_entry = [&](const uint4 (&en)[5], int dn) {
+            f29 gx, gy;
+            const u32* w = reinterpret_cast<const u32*>(en);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                gx.v[k] = w[k];
+                gy.v[k] = w[10 + k];
+            }
+            if ((dn != 0) != neg1) f29_neg(gy, gy);
+            add(acc, gx, gy);
+        };
+        digit(0, ptr, dneg_cur);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) cur[k] = ptr[k];
+#pragma unroll 1
+        for (int i = 0; i < 16; i += 2) {
+            digit(i + 1, ptr, dneg_nxt);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
+            add_entry(cur, dneg_cur);
+            digit(i + 2, ptr, dneg_cur);  // i + 2 <= 16: entry 16 is 2^256 G
+#pragma unroll
+            for (int k = 0; k < 5; ++k) cur[k] = ptr[k];
+            add_entry(nxt, dneg_nxt);
+        }
+        add_entry(cur, dneg_cur);
+        return;
+    }
     digit(0, ptr, dneg_nxt);
 #pragma unroll
     for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
@@ -757,6 +789,15 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
     fe s_inv;  // plain s^-1 mod n (1 for an invalid s: masked by `valid`)
     {
         f29 tx[kQTab], ty[kQTab];
+#ifdef SBFT_PAIR_NO_TABLE  // development: phase timing only (wrong verdicts)
+        s_inv = s;
+#pragma unroll
+        for (int m = 0; m < kQTab; ++m) {
+            tx[m] = f29_from_u256(qx);
+            ty[m] = f29_from_u256(qy);
+        }
+        if (0)
+#endif
         build_q_table(tx, ty, qx, qy, valid, [&](const fe& zp) {
             fe x = zp, y, zi;
             if (odd) {
@@ -788,7 +829,7 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
         fn_mul(w, s_inv, fe_const(C_R2N));  // s^-1 R
         verify_scalars(w, valid, e_raw, r, u1, u2, neg1, neg2);
     }
-#ifndef SBFT_PAIR_NO_TOUCH
+#ifdef SBFT_PAIR_TOUCH
     const u32 touch = comb_touch(u1, gcomb);
 #endif
 
@@ -819,12 +860,12 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
         if ((d2 < 0) != neg2) f29_neg(y2, y2);
         p29_add_aff_pair(acc, x2, y2, odd);
     }
-#ifndef SBFT_PAIR_NO_TOUCH
+#ifdef SBFT_PAIR_TOUCH
     asm volatile("" ::"v"(touch));
 #endif
 #ifndef SBFT_PAIR_NO_COMB
-    comb_add_u1g(acc, u1, neg1, gcomb,
-                 [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); });
+    comb_add_u1g<true>(acc, u1, neg1, gcomb,
+                       [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); });
 #endif
 
     bool exc;

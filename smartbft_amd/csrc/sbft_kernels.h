@@ -34,6 +34,12 @@ int sbft_launch_gcomb_build(void* d_table, hipStream_t stream);
 // device u32 of scratch private to the stream (zeroed by the launch).
 int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
                        const uint32_t* d_order, uint8_t* d_dig, uint32_t n, uint32_t* d_ctr, hipStream_t stream);
+// SoA verify inputs (32-byte fields, 16-B aligned outputs) gathered from framed messages in
+// the blob: r || s at off[k] + len[k] + sig_rel, x || y at off[k] + len[k] + pub_rel (the
+// caller has bounds-checked both against the blob).
+int sbft_launch_gather_framed(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len, uint32_t n,
+                              int32_t sig_rel, int32_t pub_rel, uint8_t* d_r, uint8_t* d_s, uint8_t* d_qx,
+                              uint8_t* d_qy, hipStream_t stream);
 // Key derivation + ECDSA sign with caller nonces: Q = d*G, (r, s); status 1 = ok.
 int sbft_launch_p256_sign(const uint8_t* d_d, const uint8_t* d_k, const uint8_t* d_e, uint8_t* d_qx,
                           uint8_t* d_qy, uint8_t* d_r, uint8_t* d_s, uint8_t* d_status, uint32_t n,

@@ -87,7 +87,43 @@ __global__ __launch_bounds__(256) void sha256_stream_kernel(const uint8_t* __res
     }
 }
 
+// Framed tuples: message k's signature r || s is the 64 bytes at off[k] + len[k] + sig_rel
+// of the blob and its public key x || y the 64 bytes at off[k] + len[k] + pub_rel. One thread
+// per (message, 32-byte field) copies the field into the SoA verify inputs (byte loads: the
+// fields are not aligned in the payload).
+__global__ __launch_bounds__(256) void gather_framed_kernel(const uint8_t* __restrict__ blob,
+                                                            const uint64_t* __restrict__ off,
+                                                            const uint32_t* __restrict__ len, uint32_t n,
+                                                            int32_t sig_rel, int32_t pub_rel,
+                                                            uint8_t* __restrict__ r, uint8_t* __restrict__ s,
+                                                            uint8_t* __restrict__ qx, uint8_t* __restrict__ qy) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= 4u * n) return;
+    const uint32_t k = gid >> 2, f = gid & 3u;
+    const int64_t end = (int64_t)(off[k] + len[k]);
+    const uint8_t* src = blob + end + (f < 2 ? sig_rel : pub_rel) + 32 * (f & 1u);
+    uint8_t* dst = (f == 0 ? r : f == 1 ? s : f == 2 ? qx : qy) + 32ull * k;
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        w[j] = (uint32_t)src[4 * j] | ((uint32_t)src[4 * j + 1] << 8) | ((uint32_t)src[4 * j + 2] << 16) |
+               ((uint32_t)src[4 * j + 3] << 24);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
 }  // namespace sbft
+
+extern "C" int sbft_launch_gather_framed(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
+                                         uint32_t n, int32_t sig_rel, int32_t pub_rel, uint8_t* d_r, uint8_t* d_s,
+                                         uint8_t* d_qx, uint8_t* d_qy, hipStream_t stream) {
+    if (n == 0) return 0;
+    const unsigned blocks = (unsigned)((4ull * n + 255) / 256);
+    hipLaunchKernelGGL(sbft::gather_framed_kernel, dim3(blocks), dim3(256), 0, stream, d_blob, d_off, d_len, n,
+                       sig_rel, pub_rel, d_r, d_s, d_qx, d_qy);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 extern "C" int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
                                   const uint32_t* d_order, uint8_t* d_dig, uint32_t n, uint32_t* d_ctr,

@@ -794,7 +794,7 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     const size_t n = reqs.size();
     std::vector<uint64_t> off(n);
     std::vector<uint32_t> len(n);
-    std::vector<uint8_t> r(32 * n), s(32 * n), qx(32 * n), qy(32 * n), ok(n);
+    std::vector<uint8_t> ok(n);
     for (size_t i = 0; i < n; ++i) {
         if (reqs[i].pub[0] != 0x04) {
             if (bad_index) *bad_index = (int64_t)i;
@@ -804,10 +804,6 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
         }
         off[i] = reqs[i].body_off;
         len[i] = (uint32_t)reqs[i].body_len;
-        std::memcpy(&r[32 * i], reqs[i].sig, 32);
-        std::memcpy(&s[32 * i], reqs[i].sig + 32, 32);
-        std::memcpy(&qx[32 * i], reqs[i].pub + 1, 32);
-        std::memcpy(&qy[32 * i], reqs[i].pub + 33, 32);
     }
     if (n && !v->ctx) {
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(SBFT_GV_ENODEV));
@@ -826,9 +822,9 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
         }
     }
     int rc = 0;
-    if (n && nk == 0) {
-        rc = sbft_gv_sha256_verify_p256(v->ctx, p->payload, p->payload_len, off.data(), len.data(), r.data(),
-                                        s.data(), qx.data(), qy.data(), n, ok.data(), nullptr);
+    if (n && nk == 0) {  // the tuples are gathered on the device from the payload itself
+        rc = sbft_gv_sha256_verify_p256_framed(v->ctx, p->payload, p->payload_len, off.data(), len.data(), n,
+                                               0, -64, ok.data());
     } else if (n) {
         std::vector<size_t> wk, wg;
         wk.reserve(nk);
@@ -844,20 +840,18 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
             for (size_t i = 0; i < w.size(); ++i) o[i] = a[w[i]];
             return o;
         };
-        auto pickf = [](const std::vector<uint8_t>& a, const std::vector<size_t>& w) {
-            std::vector<uint8_t> o(32 * w.size());
-            for (size_t i = 0; i < w.size(); ++i) std::memcpy(&o[32 * i], &a[32 * w[i]], 32);
-            return o;
-        };
+        std::vector<uint8_t> rk(32 * wk.size()), sk(32 * wk.size());
+        for (size_t i = 0; i < wk.size(); ++i) {
+            std::memcpy(&rk[32 * i], reqs[wk[i]].sig, 32);
+            std::memcpy(&sk[32 * i], reqs[wk[i]].sig + 32, 32);
+        }
         std::vector<uint8_t> okk(wk.size()), okg(wg.size());
         rc = sbft_gv_sha256_verify_p256_keyed(v->ctx, p->payload, p->payload_len, pick64(off, wk).data(),
-                                              pick32(len, wk).data(), pickf(r, wk).data(), pickf(s, wk).data(),
-                                              pick32(kid, wk).data(), wk.size(), okk.data());
+                                              pick32(len, wk).data(), rk.data(), sk.data(), pick32(kid, wk).data(),
+                                              wk.size(), okk.data());
         if (!rc && !wg.empty())
-            rc = sbft_gv_sha256_verify_p256(v->ctx, p->payload, p->payload_len, pick64(off, wg).data(),
-                                            pick32(len, wg).data(), pickf(r, wg).data(), pickf(s, wg).data(),
-                                            pickf(qx, wg).data(), pickf(qy, wg).data(), wg.size(), okg.data(),
-                                            nullptr);
+            rc = sbft_gv_sha256_verify_p256_framed(v->ctx, p->payload, p->payload_len, pick64(off, wg).data(),
+                                                   pick32(len, wg).data(), wg.size(), 0, -64, okg.data());
         for (size_t i = 0; i < wk.size(); ++i) ok[wk[i]] = okk[i];
         for (size_t i = 0; i < wg.size(); ++i) ok[wg[i]] = okg[i];
     }

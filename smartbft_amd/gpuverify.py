@@ -22,6 +22,7 @@ EXPORTS = [
     "sbft_gv_selftest_field", "sbft_gv_verify_workspace_bytes",
     "sbft_gv_register_key", "sbft_gv_verify_p256_keyed", "sbft_gv_sha256_verify_p256_keyed",
     "sbft_gv_kernel_timing", "sbft_gv_kernel_time", "sbft_gv_register_keys",
+    "sbft_gv_sha256_verify_p256_framed",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -63,6 +64,10 @@ def load_library():
                                              ctypes.POINTER(ctypes.c_uint64),
                                              ctypes.POINTER(ctypes.c_uint32)] + [_u8p] * 4 + \
                                             [ctypes.c_size_t, _u8p, _u8p]
+    L.sbft_gv_sha256_verify_p256_framed.argtypes = [_vp, _u8p, ctypes.c_size_t,
+                                                    ctypes.POINTER(ctypes.c_uint64),
+                                                    ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t,
+                                                    ctypes.c_int32, ctypes.c_int32, _u8p]
     L.sbft_gv_verify_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 5 + [ctypes.c_size_t, _vp, _vp]
     L.sbft_gv_sha256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 4 + [ctypes.c_size_t, _vp, _vp]
     L.sbft_gv_sha256_verify_p256_dev.argtypes = [_vp, ctypes.c_int] + [_vp] * 8 + \
@@ -254,6 +259,21 @@ class GpuVerifier:
             ln.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), *[_p(a) for a in arrs], n, _p(ok),
             _p(dig) if dig is not None else None), "sbft_gv_sha256_verify_p256")
         return (ok, dig) if want_digests else ok
+
+    def sha256_verify_framed(self, blob, off, ln, sig_rel: int, pub_rel: int) -> np.ndarray:
+        """Hash + verify of messages whose r || s and x || y sit in the blob at message end
+        + sig_rel / + pub_rel (sbft_gv_sha256_verify_p256_framed)."""
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(ln, dtype=np.uint32)
+        n = off.shape[0]
+        ok = np.zeros(n, dtype=np.uint8)
+        self._check(self.L.sbft_gv_sha256_verify_p256_framed(
+            self.ctx, _p(blob) if blob.size else None, blob.size,
+            off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+            ln.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n, sig_rel, pub_rel, _p(ok)),
+            "sbft_gv_sha256_verify_p256_framed")
+        return ok
 
     # ---- device-resident (torch tensors on a HIP device) ----
     @staticmethod

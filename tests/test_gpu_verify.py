@@ -272,3 +272,43 @@ def test_kernels_large_tiled(gpu_kernel, p256_vectors):
     reps = 64
     got = gpu_kernel.verify(*split_fields(np.tile(f, (reps, 1))))
     assert np.array_equal(got.reshape(reps, -1), np.tile(exp, (reps, 1)))
+
+
+@pytest.mark.parametrize("pair", [False, True])
+def test_framed_hash_then_verify(pair):
+    """sbft_gv_sha256_verify_p256_framed: tuples gathered on the device from the blob in the
+    signed-request layout (x || y closing the signed body, r || s right after it), both
+    kernels; a frame reaching past the blob is rejected, not read."""
+    import torch
+    from smartbft_amd import GpuVerifier
+    assert torch.cuda.is_available(), "gpu-marked test needs a visible MI355X"
+    gv = GpuVerifier(pair_max=(1 << 30) if pair else -1)
+    rng = np.random.default_rng(31)
+    n = 500
+    parts, off, lens, exp = [], [], [], []
+    pos = 3  # unaligned start
+    for i in range(n):
+        d = int.from_bytes(rng.bytes(32), "big") % oracle.N or 1
+        k = int.from_bytes(rng.bytes(32), "big") % oracle.N or 1
+        qx, qy = oracle.pubkey(d)
+        body = rng.bytes(int(rng.integers(0, 300))) + qx + qy  # the key closes the signed body
+        r, s = oracle.sign(d, k, hashlib.sha256(body).digest())
+        sig = r + s
+        if i % 7 == 3:
+            sig = bytes([sig[0] ^ 1]) + sig[1:]
+        if i % 11 == 5:
+            body = body[:-1] + bytes([body[-1] ^ 0x80])  # key damaged after signing
+        cols = (hashlib.sha256(body).digest(), sig[:32], sig[32:], body[-64:-32], body[-32:])
+        exp.append(oracle.verify_batch(*[np.frombuffer(x, dtype=np.uint8).reshape(1, 32) for x in cols])[0])
+        off.append(pos)
+        lens.append(len(body))
+        parts.append(body + sig)
+        pos += len(body) + 64
+    exp = np.array(exp, dtype=np.uint8)
+    blob = np.frombuffer(b"\0\0\0" + b"".join(parts), dtype=np.uint8)
+    got = gv.sha256_verify_framed(blob, np.array(off), np.array(lens), 0, -64)
+    assert np.array_equal(got, exp)
+    assert 0 < exp.sum() < n
+    with pytest.raises(Exception):
+        gv.sha256_verify_framed(blob, np.array(off), np.array(lens), 1, -64)
+    gv.close()
