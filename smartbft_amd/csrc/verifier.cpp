@@ -295,6 +295,20 @@ struct Req {
     const uint8_t* sig = nullptr;       // 64 bytes r||s
 };
 
+// Per-thread scratch for the proposal paths: a 10k-request proposal needs ~0.8 MB of
+// request views and offsets, and fresh vectors of that size are mmap'd and page-faulted on
+// every call (~0.1-0.25 ms); reused ones keep their pages.
+struct ProposalScratch {
+    std::vector<Req> reqs;
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    std::vector<uint8_t> ok;
+};
+ProposalScratch& proposal_scratch() {
+    thread_local ProposalScratch s;
+    return s;
+}
+
 const char* REQ_MAGIC = "SBR1";
 const char* MSG_MAGIC = "SBC1";
 
@@ -770,7 +784,7 @@ void sbft_verifier_set_verification_sequence(sbft_verifier* v, uint64_t seq) {
 int sbft_verifier_requests_from_proposal(sbft_verifier* v, const sbft_proposal* p, char* infos,
                                          size_t infos_cap, size_t* count) {
     if (!v || !p || !count) return SBFT_GV_EINVAL;
-    std::vector<Req> reqs;
+    std::vector<Req>& reqs = proposal_scratch().reqs;
     *count = 0;
     if (!parse_payload(p->payload, p->payload_len, reqs)) return SBFT_V_EFORMAT;
     char* w = infos;
@@ -786,15 +800,19 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     if (!v || !p || !count) return SBFT_GV_EINVAL;
     *count = 0;
     if (bad_index) *bad_index = -1;
-    std::vector<Req> reqs;
+    ProposalScratch& scr = proposal_scratch();
+    std::vector<Req>& reqs = scr.reqs;
     if (!parse_payload(p->payload, p->payload_len, reqs)) {
         put_err(err, err_cap, "malformed proposal payload");
         return SBFT_V_EFORMAT;
     }
     const size_t n = reqs.size();
-    std::vector<uint64_t> off(n);
-    std::vector<uint32_t> len(n);
-    std::vector<uint8_t> ok(n);
+    std::vector<uint64_t>& off = scr.off;
+    std::vector<uint32_t>& len = scr.len;
+    std::vector<uint8_t>& ok = scr.ok;
+    off.resize(n);
+    len.resize(n);
+    ok.assign(n, 0);
     for (size_t i = 0; i < n; ++i) {
         if (reqs[i].pub[0] != 0x04) {
             if (bad_index) *bad_index = (int64_t)i;
