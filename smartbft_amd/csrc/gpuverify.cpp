@@ -11,17 +11,80 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <new>
 #include <vector>
 
 #include "../../include/sbft_gpuverify.h"
+#include "engine_internal.h"
 #include "sbft_kernels.h"
 
 namespace {
+
+// One helper thread per context for host work that can overlap a caller's PCIe copy (the
+// proposal parse of sbft_gv_framed_overlapped). A submitted job runs at once if the helper is
+// idle; a second concurrent caller finds it busy and runs its job inline. After a job the
+// helper spins ~2 ms before sleeping, so back-to-back proposals do not pay a wake-up.
+struct Helper {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::thread th;
+    std::function<void()> job;
+    std::atomic<int> state{0};  // 0 idle, 1 job queued, 2 job done
+    std::atomic<bool> busy{false};
+    bool stop = false;
+
+    void loop() {
+        for (;;) {
+            const auto t0 = std::chrono::steady_clock::now();
+            while (state.load(std::memory_order_acquire) != 1 &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2))
+                std::this_thread::yield();
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return stop || state.load() == 1; });
+                if (stop) return;
+                f = std::move(job);
+            }
+            f();
+            state.store(2, std::memory_order_release);
+        }
+    }
+    // false: the helper is busy with another caller's job (run it inline instead)
+    bool try_submit(std::function<void()> f) {
+        bool expect = false;
+        if (!busy.compare_exchange_strong(expect, true)) return false;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!th.joinable()) th = std::thread([this] { loop(); });
+            job = std::move(f);
+            state.store(1, std::memory_order_release);
+        }
+        cv.notify_one();
+        return true;
+    }
+    void wait() {
+        while (state.load(std::memory_order_acquire) != 2) std::this_thread::yield();
+        state.store(0);
+        busy.store(false);
+    }
+    ~Helper() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv.notify_one();
+        if (th.joinable()) th.join();
+    }
+};
 
 struct Workspace {
     void* ptr = nullptr;
@@ -101,6 +164,22 @@ struct Slot {
         return SBFT_GV_OK;
     }
 
+    // device copy of a whole payload for sbft_gv_framed_overlapped (kept apart from dbuf,
+    // which that call grows after the copy has started)
+    uint8_t* bbuf = nullptr;
+    size_t bcap = 0;
+    int reserve_blob(size_t bytes) {
+        if (bytes <= bcap) return SBFT_GV_OK;
+        if (bbuf) (void)hipFree(bbuf);
+        bbuf = nullptr;
+        bcap = 0;
+        size_t want = std::max(bytes, (size_t)1 << 22);
+        want = (want + 4095) & ~(size_t)4095;
+        if (hipMalloc(&bbuf, want) != hipSuccess) return SBFT_GV_ENOMEM;
+        bcap = want;
+        return SBFT_GV_OK;
+    }
+
     int reserve(size_t bytes) {
         if (bytes <= dcap) return SBFT_GV_OK;
         if (dbuf) (void)hipFree(dbuf);
@@ -151,6 +230,7 @@ struct sbft_gv_ctx {
     };
     std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_index;
     std::atomic<uint32_t> nkeys{1};
+    Helper helper;  // host work overlapped with a caller's copies (sbft_gv_framed_overlapped)
 };
 
 extern "C" {
@@ -215,6 +295,7 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
         (void)hipSetDevice(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
         if (s->dbuf) (void)hipFree(s->dbuf);
+        if (s->bbuf) (void)hipFree(s->bbuf);
         for (void* t : s->comb_alloc) (void)hipFree(t);
         if (s->d_keytab) (void)hipFree(s->d_keytab);
         for (void* t : s->retired) (void)hipFree(t);
@@ -632,6 +713,76 @@ int sbft_gv_sha256_verify_p256_framed(sbft_gv_ctx* ctx, const uint8_t* blob, siz
 }
 
 }  // extern "C"
+
+int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, int32_t sig_rel,
+                              int32_t pub_rel,
+                              const std::function<int(std::vector<uint64_t>&, std::vector<uint32_t>&)>& prepare,
+                              std::vector<uint8_t>& ok) {
+    if (!ctx || (!blob && blob_len)) return SBFT_GV_EINVAL;
+    // this thread's scratch, bound to references: a lambda running on the helper thread must
+    // see these objects, not the helper's own thread_local instances
+    thread_local std::vector<uint64_t> off_tl;
+    thread_local std::vector<uint32_t> len_tl;
+    std::vector<uint64_t>& off = off_tl;
+    std::vector<uint32_t>& len = len_tl;
+    off.clear();
+    len.clear();
+    Slot* sl = ctx->slots[ctx->rr.fetch_add(1) % ctx->slots.size()];
+    std::unique_lock<std::mutex> lk(sl->mu);
+    HIPCHK(hipSetDevice(sl->device));
+    int rc = sl->reserve_blob(blob_len + 256);  // + the hash kernel's funnel over-read
+    if (rc) return rc;
+    // the parse runs on the helper while this thread stages the payload for the DMA
+    int prc = 0;
+    const bool async = ctx->helper.try_submit([&] { prc = prepare(off, len); });
+    const hipError_t ce =
+        blob_len ? hipMemcpyAsync(sl->bbuf, blob, blob_len, hipMemcpyHostToDevice, sl->stream) : hipSuccess;
+    if (async)
+        ctx->helper.wait();
+    else
+        prc = prepare(off, len);
+    const int sync_rc = hipStreamSynchronize(sl->stream) == hipSuccess && ce == hipSuccess ? SBFT_GV_OK
+                                                                                           : SBFT_GV_EDEVICE;
+    if (prc) return prc;
+    if (sync_rc) return sync_rc;
+    const size_t n = off.size();
+    ok.assign(n, 0);
+    if (n == 0) return SBFT_GV_OK;
+    if (len.size() != n || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    if (n >= ctx->min_split && ctx->slots.size() > 1) {  // large: the multi-device split path
+        lk.unlock();
+        return sbft_gv_sha256_verify_p256_framed(ctx, blob, blob_len, off.data(), len.data(), n, sig_rel, pub_rel,
+                                                 ok.data());
+    }
+    for (size_t k = 0; k < n; ++k) {
+        if (off[k] + len[k] > blob_len || off[k] + len[k] < off[k]) return SBFT_GV_EINVAL;
+        const int64_t end = (int64_t)(off[k] + len[k]);
+        for (int32_t rel : {sig_rel, pub_rel})
+            if (end + rel < 0 || (uint64_t)(end + rel) + 64 > blob_len) return SBFT_GV_EINVAL;
+    }
+    // off | len | hash counter | digests | r | s | qx | qy | ok | verify workspace
+    const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256), fd = align_up(32 * n, 256);
+    rc = sl->reserve(fo + fl + 256 + 5 * fd + align_up(n, 256) + sbft_verify_work_bytes(n));
+    if (rc) return rc;
+    uint8_t* b = sl->dbuf;
+    uint8_t *d_off = b, *d_len = b + fo, *d_ctr = d_len + fl, *d_dig = d_ctr + 256, *v = d_dig + fd;
+    uint8_t* d_ok = v + 4 * fd;
+    uint32_t* work = (uint32_t*)(d_ok + align_up(n, 256));
+    const void* gcomb = sl->gcomb_table();
+    if (!gcomb) return SBFT_GV_ENOMEM;
+    HIPCHK(hipMemcpyAsync(d_off, off.data(), 8 * n, hipMemcpyHostToDevice, sl->stream));
+    HIPCHK(hipMemcpyAsync(d_len, len.data(), 4 * n, hipMemcpyHostToDevice, sl->stream));
+    if (sbft_launch_sha256(sl->bbuf, (const uint64_t*)d_off, (const uint32_t*)d_len, nullptr, d_dig, (uint32_t)n,
+                           (uint32_t*)d_ctr, sl->stream) ||
+        sbft_launch_gather_framed(sl->bbuf, (const uint64_t*)d_off, (const uint32_t*)d_len, (uint32_t)n, sig_rel,
+                                  pub_rel, v, v + fd, v + 2 * fd, v + 3 * fd, sl->stream) ||
+        sbft_launch_p256_verify(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_ok, (uint32_t)n, work, gcomb,
+                                sl->stream, nullptr, nullptr, n <= ctx->pair_max))
+        return SBFT_GV_ELAUNCH;
+    HIPCHK(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, sl->stream));
+    HIPCHK(hipStreamSynchronize(sl->stream));
+    return SBFT_GV_OK;
+}
 
 // ---------------------------------------------------------------- registered keys
 namespace {

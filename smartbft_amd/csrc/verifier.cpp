@@ -6,6 +6,7 @@
 // launch (view.go:631, :834). The host side only parses formats, checks bindings and builds
 // the structure-of-arrays batches; there is no CPU verification path.
 #include "../../include/sbft_verifier.h"
+#include "engine_internal.h"
 
 #include <cpuid.h>
 #include <immintrin.h>
@@ -382,6 +383,27 @@ bool write_info(char*& w, char* end, const Req::Str& cid, const Req::Str& id) {
     w += id.n;
     *w++ = 0;
     return true;
+}
+
+// VerifyProposal's result: the first request with a 0 verdict fails the whole proposal (with
+// its index and ids in the message), else the RequestInfos in payload order.
+int finish_proposal(const std::vector<Req>& reqs, const std::vector<uint8_t>& ok, char* infos, size_t infos_cap,
+                    size_t* count, int64_t* bad_index, char* err, size_t err_cap) {
+    const size_t n = reqs.size();
+    if (ok.size() != n) return SBFT_GV_EINVAL;
+    for (size_t i = 0; i < n; ++i)
+        if (!ok[i]) {
+            if (bad_index) *bad_index = (int64_t)i;
+            put_err(err, err_cap, "request %zu (%.*s:%.*s) has an invalid signature", i, reqs[i].client_id.n,
+                    reqs[i].client_id.p, reqs[i].req_id.n, reqs[i].req_id.p);
+            return SBFT_V_EVERIFY;
+        }
+    char* w = infos;
+    char* end = infos + infos_cap;
+    for (auto& q : reqs)
+        if (!write_info(w, end, q.client_id, q.req_id)) return SBFT_V_ESPACE;
+    *count = n;
+    return 0;
 }
 
 // Open-addressing map from a 64-byte public key (x || y) to its engine key id: the
@@ -800,29 +822,49 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     if (!v || !p || !count) return SBFT_GV_EINVAL;
     *count = 0;
     if (bad_index) *bad_index = -1;
-    ProposalScratch& scr = proposal_scratch();
+    ProposalScratch& scr = proposal_scratch();  // this thread's, also when prepare runs elsewhere
     std::vector<Req>& reqs = scr.reqs;
-    if (!parse_payload(p->payload, p->payload_len, reqs)) {
-        put_err(err, err_cap, "malformed proposal payload");
-        return SBFT_V_EFORMAT;
-    }
-    const size_t n = reqs.size();
-    std::vector<uint64_t>& off = scr.off;
-    std::vector<uint32_t>& len = scr.len;
     std::vector<uint8_t>& ok = scr.ok;
-    off.resize(n);
-    len.resize(n);
-    ok.assign(n, 0);
-    for (size_t i = 0; i < n; ++i) {
-        if (reqs[i].pub[0] != 0x04) {
-            if (bad_index) *bad_index = (int64_t)i;
-            put_err(err, err_cap, "request %zu (%.*s:%.*s): public key is not SEC1 uncompressed", i,
-                    reqs[i].client_id.n, reqs[i].client_id.p, reqs[i].req_id.n, reqs[i].req_id.p);
+    // parse + per-request format checks -> the body offsets / lengths of the framed requests
+    auto prepare = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
+        if (!parse_payload(p->payload, p->payload_len, reqs)) {
+            put_err(err, err_cap, "malformed proposal payload");
             return SBFT_V_EFORMAT;
         }
-        off[i] = reqs[i].body_off;
-        len[i] = (uint32_t)reqs[i].body_len;
+        const size_t n = reqs.size();
+        off.resize(n);
+        len.resize(n);
+        for (size_t i = 0; i < n; ++i) {
+            if (reqs[i].pub[0] != 0x04) {
+                if (bad_index) *bad_index = (int64_t)i;
+                put_err(err, err_cap, "request %zu (%.*s:%.*s): public key is not SEC1 uncompressed", i,
+                        reqs[i].client_id.n, reqs[i].client_id.p, reqs[i].req_id.n, reqs[i].req_id.p);
+                return SBFT_V_EFORMAT;
+            }
+            off[i] = reqs[i].body_off;
+            len[i] = (uint32_t)reqs[i].body_len;
+        }
+        return 0;
+    };
+    bool registered;
+    {
+        std::shared_lock<std::shared_mutex> g(v->clients_mu);
+        registered = v->clients.count != 0;
     }
+    if (v->ctx && !registered) {
+        // no registered client keys: one framed launch, the parse overlapped with the payload copy
+        const int rc = sbft_gv_framed_overlapped(v->ctx, p->payload, p->payload_len, 0, -64, prepare, ok);
+        if (rc) {
+            if (rc != SBFT_V_EFORMAT) put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+            return rc;
+        }
+        return finish_proposal(reqs, ok, infos, infos_cap, count, bad_index, err, err_cap);
+    }
+    std::vector<uint64_t>& off = scr.off;
+    std::vector<uint32_t>& len = scr.len;
+    if (int prc = prepare(off, len)) return prc;
+    const size_t n = reqs.size();
+    ok.assign(n, 0);
     if (n && !v->ctx) {
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(SBFT_GV_ENODEV));
         return SBFT_GV_ENODEV;
@@ -877,19 +919,7 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
         return rc;
     }
-    for (size_t i = 0; i < n; ++i)
-        if (!ok[i]) {
-            if (bad_index) *bad_index = (int64_t)i;
-            put_err(err, err_cap, "request %zu (%.*s:%.*s) has an invalid signature", i, reqs[i].client_id.n,
-                    reqs[i].client_id.p, reqs[i].req_id.n, reqs[i].req_id.p);
-            return SBFT_V_EVERIFY;
-        }
-    char* w = infos;
-    char* end = infos + infos_cap;
-    for (auto& q : reqs)
-        if (!write_info(w, end, q.client_id, q.req_id)) return SBFT_V_ESPACE;
-    *count = n;
-    return 0;
+    return finish_proposal(reqs, ok, infos, infos_cap, count, bad_index, err, err_cap);
 }
 
 int sbft_verifier_verify_request(sbft_verifier* v, const uint8_t* req, size_t len, char* info, size_t info_cap,
