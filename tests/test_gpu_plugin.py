@@ -297,3 +297,39 @@ def test_verify_proposal_registered_clients(gpu, net):
     v.add_clients([c.public_key() for c in clients])  # all registered (re-registering is a no-op)
     assert v.VerifyProposal(p) == generic
     v.close()
+
+
+def test_verify_proposal_format_errors_and_concurrent_callers(net):
+    """The overlapped path (parse on the engine's helper thread): format errors found there come
+    back with their own code and text, and concurrent callers (helper busy -> inline parse)
+    each get their own proposal's verdicts."""
+    import threading
+    v, nodes, clients = net
+    good, _ = _proposal(clients, 60)
+    bad, _ = _proposal(clients, 40, tamper=11)
+    trunc = plugin.Proposal(good.Payload[:-1], good.Header, good.Metadata, good.VerificationSequence)
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(trunc)
+    assert ei.value.code == plugin.EFORMAT and "malformed" in str(ei.value)
+    results, errors = {}, []
+
+    def worker(k):
+        try:
+            for it in range(6):
+                if (k + it) % 2:
+                    assert len(v.VerifyProposal(good)) == 60
+                else:
+                    with pytest.raises(plugin.VerifyError) as e:
+                        v.VerifyProposal(bad)
+                    assert e.value.index == 11 and e.value.code == plugin.EVERIFY
+            results[k] = True
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    assert len(results) == 4
