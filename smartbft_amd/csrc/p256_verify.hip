@@ -491,6 +491,102 @@ SBFT_DEV void build_q_table(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, co
     }
 }
 
+// build_q_table on a lane pair (p256_verify_pair_kernel): the same products and bounds, two
+// per step (see p29_dbl_pair). Conversion 1 step instead of 2, DBLU 4 instead of 6, each ZADDU
+// 3 instead of 6, the product of the Z ratios a 4-step tree instead of a 7-product chain, and
+// each affine conversion 3 steps instead of 5.
+template <class InvP>
+SBFT_DEV void build_q_table_pair(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, const fe& qy, bool valid,
+                                 bool odd, InvP inv_p) {
+    static_assert(kQTab == 8, "the Z-ratio product tree below is written for 7 ratios");
+    // e = a0 b0 (even lane's product), d = a1 b1 (odd lane's), both in both lanes
+    auto pmul = [odd](f29& e, f29& d, const f29& a0, const f29& b0, const f29& a1, const f29& b1) {
+        f29 o;
+        f29_mul_ilp(o, f29_pick(odd, a0, a1), f29_pick(odd, b0, b1));
+        f29_unpair(o, e, d);
+    };
+    const f29 r2 = f29_const(C29_R2);
+    f29 qxm, qym;
+    pmul(qxm, qym, f29_from_u256(qx), r2, f29_from_u256(qy), r2);
+    if (!valid) {
+        qxm = f29_const(C29_G2X);
+        qym = f29_const(C29_G2Y);
+    }
+    tx[0] = qxm;
+    ty[0] = qym;
+    f29 dx, dy, cx, cy, z;  // D = 2Q and the current odd multiple, co-Z (Z = z)
+    {                        // DBLU (p29_dblu): B = x^2 | E = y^2, L = E^2 | x E, M^2, M (S - X2)
+        f29 b, e, l, t, m, m2;
+        pmul(b, e, qxm, qxm, qym, qym);
+        pmul(l, t, e, e, qxm, e);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t.v[i] <<= 2;  // 4xE < 2^31
+        f29_normalize(cx, t);                       // S (N')
+        const f29 one = f29_const(C29_ONE);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) m.v[i] = 3 * (b.v[i] - one.v[i]);  // |.| < 2^30.6
+        f29_normalize(m, m);                        // M (N')
+        f29_mul_ilp(m2, m, m);                      // 2^29.2^2
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t.v[i] = m2.v[i] - (cx.v[i] << 1);
+        f29_normalize(dx, t);                       // X2 (N')
+#pragma unroll
+        for (int i = 0; i < 9; ++i) l.v[i] <<= 2;  // 4L < 2^31
+        f29_normalize(l, l);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) l.v[i] <<= 1;  // 8L, |.| < 2^30.2
+        f29_normalize(cy, l);                       // 8L (N')
+        f29_sub(t, cx, dx);                         // S - X2, |.| < 2^29.3
+        f29_mul_ilp(m2, m, t);                      // 2^29.2 x 2^29.3
+        f29_sub(t, m2, cy);
+        f29_normalize(dy, t);                       // Y2 (N')
+        f29_add(z, qym, qym);                       // Z = 2y
+    }
+    f29 hs[kQTab - 1];  // Z ratios: Z(T_k) = Z(T_{k-1}) h_k
+#pragma unroll 1
+    for (int k = 1; k < kQTab; ++k) {  // ZADDU (p29_zaddu): H^2 | R^2, W1 | W2, A1 | R (W1 - X3)
+        f29 h, r, c, dd, w1, w2, t, u, a1, c2;
+        f29_sub(h, dx, cx);               // |.| < 2^29.3
+        f29_sub(r, dy, cy);               // |.| < 2^29.3
+        pmul(c, dd, h, h, r, r);
+        pmul(w1, w2, dx, c, cx, c);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t.v[i] = dd.v[i] - w1.v[i] - w2.v[i];  // (-2^30, 2^29)
+        f29_normalize(cx, t);             // X3 (N')
+        f29_sub(u, w1, w2);               // |.| < 2^29
+        f29_sub(t, w1, cx);               // |.| < 2^29.2
+        pmul(a1, c2, dy, u, r, t);
+        f29_sub(t, c2, a1);
+        f29_normalize(cy, t);             // Y3 (N')
+        dx = w1;
+        dy = a1;
+        tx[k] = cx;
+        ty[k] = cy;
+        hs[k - 1] = h;
+    }
+    {  // Z(T_7) = z h_1 ... h_7 as a tree (limbs: z < 2^30, h < 2^29.3, products N)
+        f29 p0, p1, p2, p3;
+        pmul(p0, p1, z, hs[0], hs[1], hs[2]);
+        pmul(p2, p3, hs[3], hs[4], hs[5], hs[6]);
+        pmul(p0, p1, p0, p1, p2, p3);
+        f29_mul_ilp(z, p0, p1);
+    }
+    f29 inv;  // 1 / Z(T_last), Montgomery form
+    {
+        const fe zi = inv_p(f29_canon_plain(z));
+        f29_mul_ilp(inv, f29_from_u256(zi), r2);
+    }
+#pragma unroll 1
+    for (int k = kQTab - 1; k >= 1; --k) {  // inv^2 | inv h_k, zi2 inv | x zi2, y zi3
+        f29 zi2, nxt, zi3, xa;
+        pmul(zi2, nxt, inv, inv, inv, hs[k - 1]);
+        pmul(zi3, xa, zi2, inv, tx[k], zi2);
+        f29_mul_ilp(ty[k], ty[k], zi3);
+        tx[k] = xa;
+        inv = nxt;  // 1 / Z(T_{k-1})
+    }
+}
+
 // 2-3. w = s^-1 of tuple t from the launch-wide Montgomery trick (p256_sinv_* kernels: 256
 // tuples per scan block), then u1 = e w, u2 = r w, recoded for the signed-odd ladders: an even
 // u becomes n - u with the base negated ((n-u)(-P) = uP); u == 0 becomes n, whose ladder
@@ -798,7 +894,7 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
         }
         if (0)
 #endif
-        build_q_table(tx, ty, qx, qy, valid, [&](const fe& zp) {
+        build_q_table_pair(tx, ty, qx, qy, valid, odd, [&](const fe& zp) {
             fe x = zp, y, zi;
             if (odd) {
                 x = fe_zero();
