@@ -53,11 +53,14 @@ typedef struct sbft_gv_opts {
     uint32_t min_split;     /* batches smaller than this stay on one device (0 = default 65536) */
     int32_t pair_max;       /* per-device batches of at most this many tuples run the latency kernel
                                (two lanes per tuple); 0 = default SBFT_GV_PAIR_MAX_DEFAULT, < 0 = never */
-    uint32_t reserved32;
+    int32_t quad_max;       /* ... and of at most this many, its four-lane form (the u1*G comb on
+                               lanes 2-3; measured no faster than the pair form, so off by default);
+                               0 = default SBFT_GV_QUAD_MAX_DEFAULT, < 0 = never */
     uint64_t reserved[3];
 } sbft_gv_opts;
 
 #define SBFT_GV_PAIR_MAX_DEFAULT 32768u
+#define SBFT_GV_QUAD_MAX_DEFAULT 0u
 
 /* Create a context (per-device stream + device/pinned staging grown on demand).
  * opts may be NULL. Replaces: the plugin construction a Go app does before handing its

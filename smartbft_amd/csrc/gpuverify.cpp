@@ -215,7 +215,9 @@ struct sbft_gv_ctx {
     // batches (per device) of at most this many tuples use the two-lanes-per-tuple latency
     // kernel; 0 = never (sbft_gv_opts.pair_max)
     uint32_t pair_max = SBFT_GV_PAIR_MAX_DEFAULT;
+    uint32_t quad_max = SBFT_GV_QUAD_MAX_DEFAULT;  // ... four lanes per tuple (sbft_gv_opts.quad_max)
     std::atomic<uint32_t> rr{0};
+    int lanes_for(size_t n) const { return n <= quad_max ? 4 : n <= pair_max ? 2 : 1; }
     // registered public keys (x || y big-endian); index = key id, entry 0 = the generator
     std::mutex keys_mu;
     std::vector<std::array<uint8_t, 64>> keys;
@@ -257,6 +259,7 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     if (!ctx) return SBFT_GV_ENOMEM;
     if (opts && opts->min_split) ctx->min_split = opts->min_split;
     if (opts && opts->pair_max) ctx->pair_max = opts->pair_max < 0 ? 0u : (uint32_t)opts->pair_max;
+    if (opts && opts->quad_max) ctx->quad_max = opts->quad_max < 0 ? 0u : (uint32_t)opts->quad_max;
     for (int d = 0; d < ndev && d < 32; ++d) {
         if (!(mask & (1u << d))) continue;
         auto* s = new Slot();
@@ -397,7 +400,7 @@ int sbft_gv_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_digest, 
     }
     return sbft_launch_p256_verify((const uint8_t*)d_digest, (const uint8_t*)d_r, (const uint8_t*)d_s,
                                    (const uint8_t*)d_qx, (const uint8_t*)d_qy, (uint8_t*)d_ok,
-                                   (uint32_t)n, work, gcomb, (hipStream_t)stream, ev0, ev1, n <= ctx->pair_max)
+                                   (uint32_t)n, work, gcomb, (hipStream_t)stream, ev0, ev1, ctx->lanes_for(n))
                ? SBFT_GV_ELAUNCH
                : SBFT_GV_OK;
 }
@@ -453,7 +456,7 @@ struct Chunk {
     Slot* slot;
     size_t begin, count;
     size_t out_off = 0;  // keyed path: verdict offset inside the slot's pinned staging
-    bool pair = false;   // small chunk: the two-lanes-per-tuple latency kernel
+    int lanes = 1;       // verify kernel: 1 lane per tuple, or the 2 / 4-lane latency kernel
 };
 
 std::vector<Chunk> plan(sbft_gv_ctx* ctx, size_t n) {
@@ -461,12 +464,12 @@ std::vector<Chunk> plan(sbft_gv_ctx* ctx, size_t n) {
     const size_t nd = ctx->slots.size();
     if (n < ctx->min_split || nd == 1) {
         const uint32_t k = ctx->rr.fetch_add(1) % nd;
-        out.push_back({ctx->slots[k], 0, n, 0, n <= ctx->pair_max});
+        out.push_back({ctx->slots[k], 0, n, 0, ctx->lanes_for(n)});
         return out;
     }
     for (size_t d = 0; d < nd; ++d) {
         const size_t b = n * d / nd, e = n * (d + 1) / nd;
-        if (e > b) out.push_back({ctx->slots[d], b, e - b, 0, e - b <= ctx->pair_max});
+        if (e > b) out.push_back({ctx->slots[d], b, e - b, 0, ctx->lanes_for(e - b)});
     }
     return out;
 }
@@ -495,7 +498,7 @@ int enqueue_verify(const Chunk& c, const uint8_t* digest, const uint8_t* r, cons
         HIPCHK(hipMemcpyAsync(base + k * f, src[k] + 32 * c.begin, 32 * c.count, hipMemcpyHostToDevice,
                               sl->stream));
     if (sbft_launch_p256_verify(base, base + f, base + 2 * f, base + 3 * f, base + 4 * f, base + 5 * f,
-                                (uint32_t)c.count, work, gcomb, sl->stream, nullptr, nullptr, c.pair))
+                                (uint32_t)c.count, work, gcomb, sl->stream, nullptr, nullptr, c.lanes))
         return SBFT_GV_ELAUNCH;
     HIPCHK(hipMemcpyAsync(ok_out + c.begin, base + 5 * f, c.count, hipMemcpyDeviceToHost, sl->stream));
     return SBFT_GV_OK;
@@ -570,7 +573,7 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
         const void* gcomb = sl->gcomb_table();
         if (!gcomb) return SBFT_GV_ENOMEM;
         if (sbft_launch_p256_verify(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_ok, (uint32_t)c.count,
-                                    work, gcomb, sl->stream, nullptr, nullptr, c.pair))
+                                    work, gcomb, sl->stream, nullptr, nullptr, c.lanes))
             return SBFT_GV_ELAUNCH;
         HIPCHK(hipMemcpyAsync(ok_out + c.begin, d_ok, c.count, hipMemcpyDeviceToHost, sl->stream));
     }
@@ -777,7 +780,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         sbft_launch_gather_framed(sl->bbuf, (const uint64_t*)d_off, (const uint32_t*)d_len, (uint32_t)n, sig_rel,
                                   pub_rel, v, v + fd, v + 2 * fd, v + 3 * fd, sl->stream) ||
         sbft_launch_p256_verify(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_ok, (uint32_t)n, work, gcomb,
-                                sl->stream, nullptr, nullptr, n <= ctx->pair_max))
+                                sl->stream, nullptr, nullptr, ctx->lanes_for(n)))
         return SBFT_GV_ELAUNCH;
     HIPCHK(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, sl->stream));
     HIPCHK(hipStreamSynchronize(sl->stream));

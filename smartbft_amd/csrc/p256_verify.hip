@@ -846,31 +846,41 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     }
 }
 
-// Latency kernel for small batches (sbft_launch_p256_verify with pair = true): one verify on
-// two adjacent lanes, the doublings and mixed additions split between them (p29_dbl_pair,
-// p29_add_aff_pair). A batch of a few thousand tuples gives each busy SIMD one wave, so the
-// launch takes one wave's instruction stream; the pair form cuts that stream by ~40% at the
-// price of twice the lanes. Setup (checks, Q table, scalars) and the final comparison run
-// redundantly on both lanes. The Q table lives in LDS (one copy per pair). One wavefront per
-// workgroup (32 tuples) spreads a small batch over as many CUs as possible.
-constexpr int kPairTuples = 32;  // tuples per 64-lane workgroup
-__global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __restrict__ digest,
-                                                              const uint8_t* __restrict__ rr,
-                                                              const uint8_t* __restrict__ ss,
-                                                              const uint8_t* __restrict__ qxx,
-                                                              const uint8_t* __restrict__ qyy,
-                                                              uint8_t* __restrict__ ok, uint32_t n,
-                                                              uint32_t* __restrict__ work,
-                                                              const uint4* __restrict__ gcomb) {
+// Latency kernels for small batches (sbft_launch_p256_verify with lanes = 2 or 4). A batch of
+// a few thousand tuples gives each busy SIMD one wave, so the launch takes one wave's
+// instruction stream; these kernels shorten that stream at the price of more lanes.
+//   LPT = 2 (pair): one verify on two adjacent lanes, the doublings and mixed additions split
+//     between them (p29_dbl_pair, p29_add_aff_pair); u1*G by the comb after the ladder.
+//   LPT = 4 (quad): lanes 0-1 of the quad run the Q ladder as the pair does, while lanes 2-3
+//     run the same instruction stream on the comb: their accumulator starts at the first comb
+//     entry and takes one comb entry at each of the first 16 digits' mixed additions (their
+//     doublings and later additions are discarded by a select). One lean Jacobian addition of
+//     the two halves ends it: the 17 comb additions leave the critical path.
+// Setup (checks, Q table, scalars) and the final comparison run redundantly on all lanes of a
+// tuple. The Q table lives in LDS (one copy per tuple). One wavefront per workgroup spreads a
+// small batch over as many CUs as possible.
+template <int LPT>
+__global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __restrict__ digest,
+                                                               const uint8_t* __restrict__ rr,
+                                                               const uint8_t* __restrict__ ss,
+                                                               const uint8_t* __restrict__ qxx,
+                                                               const uint8_t* __restrict__ qyy,
+                                                               uint8_t* __restrict__ ok, uint32_t n,
+                                                               uint32_t* __restrict__ work,
+                                                               const uint4* __restrict__ gcomb) {
+    static_assert(LPT == 2 || LPT == 4, "two or four lanes per tuple");
+    constexpr bool kQuad = LPT == 4;
+    constexpr int kTuples = 64 / LPT;  // tuples per 64-lane workgroup
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
-    // [entry][x limbs 0..8, y limbs 0..8][pair]: the two lanes of a pair read the same word,
-    // the 32 pairs of the wave 32 consecutive words
-    __shared__ u32 qtab[kQTab * 18 * kPairTuples];
+    // [entry][x limbs 0..8, y limbs 0..8][tuple]: the lanes of a tuple read the same word, the
+    // tuples of the wave consecutive words
+    __shared__ u32 qtab[kQTab * 18 * kTuples];
     inv::stage_divstep_table(dtab);  // ends with a barrier
 
-    const int pr = threadIdx.x >> 1;
+    const int pr = threadIdx.x / LPT;
     const bool odd = (threadIdx.x & 1) != 0;
-    const uint32_t t = blockIdx.x * kPairTuples + pr;
+    const bool comb_role = kQuad && (threadIdx.x & 2) != 0;
+    const uint32_t t = blockIdx.x * kTuples + pr;
     const bool active = t < n;
     const uint32_t idx = active ? t : (n - 1);
 
@@ -912,9 +922,9 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
 #pragma unroll
         for (int m = 0; m < kQTab; ++m)
 #pragma unroll
-            for (int k = 0; k < 9; ++k) {  // both lanes store the same words
-                qtab[(m * 18 + k) * kPairTuples + pr] = tx[m].v[k];
-                qtab[(m * 18 + 9 + k) * kPairTuples + pr] = ty[m].v[k];
+            for (int k = 0; k < 9; ++k) {  // all lanes of the tuple store the same words
+                qtab[(m * 18 + k) * kTuples + pr] = tx[m].v[k];
+                qtab[(m * 18 + 9 + k) * kTuples + pr] = ty[m].v[k];
             }
     }
     __syncthreads();
@@ -929,44 +939,131 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
     const u32 touch = comb_touch(u1, gcomb);
 #endif
 
+    // comb entry i of u1 (see comb_add_u1g): |d_i| 2^(16 i) G for i < 16, 2^256 G for i = 16
+    auto comb_entry = [&](int i, uint4 (&en)[5], bool& dneg) {
+        const uint4* ptr;
+        if (i < 16) {
+            const int b = 16 * i + 1, lw = b >> 5;
+            const u32 lo = u1.v[lw], hi = lw < 7 ? u1.v[lw + 1] : 0u;
+            const int d = 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & 0xFFFFu) - 0xFFFF;
+            ptr = gcomb + ((size_t)i * SBFT_GCOMB_ENTRIES + (u32)((d < 0 ? -d : d) >> 1)) * 5;
+            dneg = d < 0;
+        } else {
+            ptr = gcomb + (size_t)16 * SBFT_GCOMB_ENTRIES * 5;
+            dneg = false;
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) en[k] = ptr[k];
+    };
+    auto entry_point = [&](const uint4 (&en)[5], bool dneg, f29& x, f29& y) {
+        const u32* w = reinterpret_cast<const u32*>(en);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            x.v[k] = w[k];
+            y.v[k] = w[10 + k];
+        }
+        if (dneg != neg1) f29_neg(y, y);
+    };
+
     jp29 acc;
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
-        acc.x.v[k] = qtab[k * kPairTuples + pr];
-        acc.y.v[k] = qtab[(9 + k) * kPairTuples + pr];
+        acc.x.v[k] = qtab[k * kTuples + pr];
+        acc.y.v[k] = qtab[(9 + k) * kTuples + pr];
     }
     acc.z = f29_const(C29_ONE);
     if (neg2) f29_neg(acc.y, acc.y);
+    // quad: the tuple's 17 comb points (signs applied) staged in LDS over the divstep table,
+    // which the inversions are done with: [entry][x limbs, y limbs][tuple]
+    u32* const ctab = dtab;
+    static_assert(!kQuad || 17 * 18 * kTuples <= SBFT_DIVSTEP5_WORDS, "comb points fit the divstep table");
+    if constexpr (kQuad) {
+        __syncthreads();  // every lane of the workgroup is past its inversions
+        for (int e = threadIdx.x & 3; e < 17; e += 4) {
+            uint4 en[5];
+            bool dn;
+            comb_entry(e, en, dn);
+            f29 gx, gy;
+            entry_point(en, dn, gx, gy);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                ctab[(e * 18 + k) * kTuples + pr] = gx.v[k];
+                ctab[(e * 18 + 9 + k) * kTuples + pr] = gy.v[k];
+            }
+        }
+        __syncthreads();
+        if (comb_role)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                acc.x.v[k] = ctab[k * kTuples + pr];
+                acc.y.v[k] = ctab[(9 + k) * kTuples + pr];
+            }
+    }
     const fe k2 = u2;
 #ifndef SBFT_PAIR_LADDER_DIGITS  // development: time the phases (tools/pair_probe.py --no-check)
 #define SBFT_PAIR_LADDER_DIGITS kQDigits
 #endif
 #pragma unroll 1
     for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 0; --i) {
+        const int j = SBFT_PAIR_LADDER_DIGITS - 1 - i;  // additions done so far
 #pragma unroll
-        for (int d = 0; d < kQWin; ++d) p29_dbl_pair(acc, acc, odd);
+        for (int d = 0; d < kQWin; ++d) {
+            if constexpr (kQuad) {
+                jp29 tt;
+                p29_dbl_pair(tt, acc, odd);
+                if (!comb_role) acc = tt;
+            } else {
+                p29_dbl_pair(acc, acc, odd);
+            }
+        }
         const int d2 = q_digit(k2, i);
         const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
         f29 x2, y2;
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
-            x2.v[k] = qtab[(m2 * 18 + k) * kPairTuples + pr];
-            y2.v[k] = qtab[(m2 * 18 + 9 + k) * kPairTuples + pr];
+            x2.v[k] = qtab[(m2 * 18 + k) * kTuples + pr];
+            y2.v[k] = qtab[(m2 * 18 + 9 + k) * kTuples + pr];
         }
         if ((d2 < 0) != neg2) f29_neg(y2, y2);
-        p29_add_aff_pair(acc, x2, y2, odd);
+        if constexpr (kQuad) {
+            // comb lanes: entry j + 1 while j + 1 <= 16, then their accumulator is final
+            const int ce = j + 1 <= 16 ? j + 1 : 16;
+            if (comb_role)
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    x2.v[k] = ctab[(ce * 18 + k) * kTuples + pr];
+                    y2.v[k] = ctab[(ce * 18 + 9 + k) * kTuples + pr];
+                }
+            jp29 tt = acc;
+            p29_add_aff_pair(tt, x2, y2, odd);
+            if (!comb_role || j + 1 <= 16) acc = tt;
+        } else {
+            p29_add_aff_pair(acc, x2, y2, odd);
+        }
     }
 #ifdef SBFT_PAIR_TOUCH
     asm volatile("" ::"v"(touch));
 #endif
+    if constexpr (kQuad) {
+        // lanes 0-1 add lanes 2-3's u1*G (quad_perm [2,3,2,3]); lanes 2-3 compute a discarded copy
+        jp29 g;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            g.x.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.x.v[k], 0xEE, 0xF, 0xF, false);
+            g.y.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.y.v[k], 0xEE, 0xF, 0xF, false);
+            g.z.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.z.v[k], 0xEE, 0xF, 0xF, false);
+        }
+        p29_add_jac_lean(acc, g);
+    } else {
 #ifndef SBFT_PAIR_NO_COMB
-    comb_add_u1g<true>(acc, u1, neg1, gcomb,
-                       [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); });
+        comb_add_u1g<true>(acc, u1, neg1, gcomb,
+                           [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); });
 #endif
+    }
 
     bool exc;
     const bool accept = verify_final(acc, r, exc);
-    if (active && !odd) {
+    if (active && (threadIdx.x % LPT) == 0) {
         if (exc && valid) {
             const uint32_t slot = atomicAdd(work, 1u);
             work[1 + slot] = t;
@@ -984,7 +1081,7 @@ __global__ __launch_bounds__(64) void p256_verify_pair_kernel(const uint8_t* __r
 extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                        const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
                                        uint32_t n, uint32_t* d_work, const void* d_gcomb, hipStream_t stream,
-                                       hipEvent_t ev0, hipEvent_t ev1, bool pair) {
+                                       hipEvent_t ev0, hipEvent_t ev1, int lanes) {
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned blocks = (n + threads - 1) / threads;
@@ -1009,7 +1106,7 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
 #endif
     if (hipMemsetAsync(d_work, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     SBFT_STEP("memset");
-    if (!pair) {  // the pair kernel inverts s itself
+    if (lanes < 2) {  // the small-batch kernels invert s themselves
         hipLaunchKernelGGL(sbft::p256_sinv_prep_kernel, dim3(blocks), dim3(threads), 0, stream, d_s, n, ws);
         SBFT_STEP("prep");
         hipLaunchKernelGGL(sbft::p256_sinv_totals_kernel, dim3(1), dim3(threads), 0, stream, (uint32_t)blocks,
@@ -1017,10 +1114,14 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
         SBFT_STEP("totals");
     }
     if (ev0 && hipEventRecord(ev0, stream) != hipSuccess) return -1;
-    if (pair) {  // two lanes per tuple, 32 tuples per 64-lane workgroup
-        const unsigned pblocks = (n + sbft::kPairTuples - 1) / sbft::kPairTuples;
-        hipLaunchKernelGGL(sbft::p256_verify_pair_kernel, dim3(pblocks), dim3(64), 0, stream, d_digest, d_r,
-                           d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb);
+    if (lanes == 2 || lanes == 4) {  // 64-lane workgroups of 32 or 16 tuples
+        const unsigned tpw = 64 / lanes, sblocks = (n + tpw - 1) / tpw;
+        if (lanes == 2)
+            hipLaunchKernelGGL(sbft::p256_verify_small_kernel<2>, dim3(sblocks), dim3(64), 0, stream, d_digest,
+                               d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb);
+        else
+            hipLaunchKernelGGL(sbft::p256_verify_small_kernel<4>, dim3(sblocks), dim3(64), 0, stream, d_digest,
+                               d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb);
     } else {
         hipLaunchKernelGGL(sbft::p256_verify_kernel, dim3(blocks), dim3(threads), 0, stream, d_digest, d_r,
                            d_s, d_qx, d_qy, d_ok, n, d_work, ws, (const uint4*)d_gcomb);

@@ -19,12 +19,13 @@ extern "C" {
 // d_gcomb: the device's fixed-base comb table for u1*G (sbft_gcomb_table_bytes() bytes, built
 // once by sbft_launch_gcomb_build; unused when that size is 0).
 // ev0/ev1 (may be NULL): events recorded on the stream right before / after the main
-// verify kernel (kernel timing, sbft_gv_kernel_time). pair: use the two-lanes-per-tuple
-// latency kernel (p256_verify_pair_kernel) instead of the one-lane throughput kernel.
+// verify kernel (kernel timing, sbft_gv_kernel_time). lanes: 1 = the one-lane throughput
+// kernel, 2 / 4 = the small-batch latency kernel with that many lanes per tuple
+// (p256_verify_small_kernel).
 int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                             const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok, uint32_t n,
                             uint32_t* d_work, const void* d_gcomb, hipStream_t stream,
-                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool pair = false);
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int lanes = 1);
 size_t sbft_gcomb_table_bytes(void);
 int sbft_launch_gcomb_build(void* d_table, hipStream_t stream);
 // SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable >= 68 bytes

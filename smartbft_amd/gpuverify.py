@@ -35,7 +35,7 @@ class GpuVerifyError(RuntimeError):
 
 class Opts(ctypes.Structure):
     _fields_ = [("device_mask", ctypes.c_uint32), ("min_split", ctypes.c_uint32),
-                ("pair_max", ctypes.c_int32), ("reserved32", ctypes.c_uint32),
+                ("pair_max", ctypes.c_int32), ("quad_max", ctypes.c_int32),
                 ("reserved", ctypes.c_uint64 * 3)]
 
 
@@ -123,12 +123,12 @@ class GpuVerifier:
     """One sbft_gv_ctx. Host-array calls are synchronous; *_dev calls take torch tensors
     (device-resident) and enqueue on the given (or current) stream."""
 
-    def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0):
-        """pair_max: per-device batches of at most this many tuples run the two-lanes-per-tuple
-        latency kernel (0 = library default, negative = never)."""
+    def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0, quad_max: int = 0):
+        """pair_max / quad_max: per-device batches of at most this many tuples run the latency
+        kernel with two / four lanes per tuple (0 = library default, negative = never)."""
         self.L = load_library()
         ctx = _vp()
-        opts = Opts(device_mask, min_split, pair_max)
+        opts = Opts(device_mask, min_split, pair_max, quad_max)
         rc = self.L.sbft_gv_init(ctypes.byref(opts), ctypes.byref(ctx))
         if rc:
             raise GpuVerifyError(f"sbft_gv_init: {self.L.sbft_gv_strerror(rc).decode()} ({rc})")

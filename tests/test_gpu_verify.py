@@ -234,14 +234,19 @@ def test_bench_workload_properties(gpu):
     assert np.array_equal(oracle.verify_batch(*f), ok[:3000].cpu().numpy())
 
 
-# ---- both verify kernels at every size: the one-lane throughput kernel (pair_max < 0) and the
-# two-lanes-per-tuple latency kernel (p256_verify_pair_kernel, forced on for big batches)
-@pytest.fixture(scope="module", params=["lane", "pair"])
+# ---- every verify kernel at every size: the one-lane throughput kernel and the small-batch
+# latency kernel with two and four lanes per tuple (p256_verify_small_kernel<2|4>, forced on
+# for big batches too)
+KERNEL_OPTS = {"lane": dict(pair_max=-1, quad_max=-1), "pair": dict(pair_max=1 << 30, quad_max=-1),
+               "quad": dict(quad_max=1 << 30)}
+
+
+@pytest.fixture(scope="module", params=list(KERNEL_OPTS))
 def gpu_kernel(request):
     import torch
     from smartbft_amd import GpuVerifier
     assert torch.cuda.is_available(), "gpu-marked test needs a visible MI355X"
-    v = GpuVerifier(pair_max=-1 if request.param == "lane" else (1 << 30))
+    v = GpuVerifier(**KERNEL_OPTS[request.param])
     yield v
     v.close()
 
@@ -274,15 +279,15 @@ def test_kernels_large_tiled(gpu_kernel, p256_vectors):
     assert np.array_equal(got.reshape(reps, -1), np.tile(exp, (reps, 1)))
 
 
-@pytest.mark.parametrize("pair", [False, True])
-def test_framed_hash_then_verify(pair):
+@pytest.mark.parametrize("mode", list(KERNEL_OPTS))
+def test_framed_hash_then_verify(mode):
     """sbft_gv_sha256_verify_p256_framed: tuples gathered on the device from the blob in the
     signed-request layout (x || y closing the signed body, r || s right after it), both
     kernels; a frame reaching past the blob is rejected, not read."""
     import torch
     from smartbft_amd import GpuVerifier
     assert torch.cuda.is_available(), "gpu-marked test needs a visible MI355X"
-    gv = GpuVerifier(pair_max=(1 << 30) if pair else -1)
+    gv = GpuVerifier(**KERNEL_OPTS[mode])
     rng = np.random.default_rng(31)
     n = 500
     parts, off, lens, exp = [], [], [], []
