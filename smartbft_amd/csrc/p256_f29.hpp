@@ -492,7 +492,7 @@ SBFT_DEV void p29_add_aff_lean(jp29& acc, const f29& x2, const f29& y2) {
 }
 
 // ---------------------------------------------------------------- lane pairs (latency kernel)
-// p256_verify_pair_kernel runs one verify on two adjacent lanes (2t, 2t+1). Both hold the
+// p256_verify_small_kernel<2> runs one verify on two adjacent lanes (2t, 2t+1). Both hold the
 // same point; at each step the two lanes compute two independent products of the formula,
 // each with its own operands (f29_pick), and f29_unpair hands both results to both lanes
 // (two quad_perm DPP moves per limb). A doubling is 4 such steps instead of 8 products, a

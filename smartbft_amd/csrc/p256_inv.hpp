@@ -66,7 +66,7 @@ struct s30 {
 
 // The modulus of an inversion: P = false for the group order n, true for the field prime p.
 // P is a run-time flag so that the two lanes of a verify pair can invert mod p and mod n in
-// the same instruction stream (p256_verify_pair_kernel); constant P folds away when inlined.
+// the same instruction stream (p256_verify_small_kernel<2>); constant P folds away when inlined.
 SBFT_HD void mod30(int32_t m[9], bool P) {
     const int32_t N30[9] = SBFT_N30_INIT, P30[9] = SBFT_P30_INIT;
     for (int i = 0; i < 9; ++i) m[i] = P ? P30[i] : N30[i];

@@ -491,7 +491,7 @@ SBFT_DEV void build_q_table(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, co
     }
 }
 
-// build_q_table on a lane pair (p256_verify_pair_kernel): the same products and bounds, two
+// build_q_table on a lane pair (p256_verify_small_kernel<2>): the same products and bounds, two
 // per step (see p29_dbl_pair). Conversion 1 step instead of 2, DBLU 4 instead of 6, each ZADDU
 // 3 instead of 6, the product of the Z ratios a 4-step tree instead of a 7-product chain, and
 // each affine conversion 3 steps instead of 5.
