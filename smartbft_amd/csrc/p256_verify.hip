@@ -726,31 +726,6 @@ SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __re
     }
 }
 
-// Latency path: one 4-byte load from each cache line of the 17 comb entries u1 selects,
-// issued before the Q ladder, so that the comb additions after it find the lines (and their
-// pages) cached instead of paying an HBM miss per dependent step. The caller consumes the
-// returned word after the ladder.
-SBFT_DEV u32 comb_touch(const fe& u1, const uint4* __restrict__ gcomb) {
-    fe k1 = u1;
-    u32 acc = 0;
-    const u32* base = reinterpret_cast<const u32*>(gcomb);
-#pragma unroll
-    for (int i = 0; i < 17; ++i) {
-        size_t e;
-        if (i < 16) {
-            const int d = 2 * (int)((k1.v[0] >> 1) & 0xFFFFu) - 0xFFFF;
-            e = (size_t)i * SBFT_GCOMB_ENTRIES + (u32)((d < 0 ? -d : d) >> 1);
-#pragma unroll
-            for (int k = 0; k < 7; ++k) k1.v[k] = __builtin_amdgcn_alignbit(k1.v[k + 1], k1.v[k], 16);
-            k1.v[7] >>= 16;
-        } else {
-            e = (size_t)16 * SBFT_GCOMB_ENTRIES;
-        }
-        acc ^= base[e * 20] ^ base[e * 20 + 19];  // first and last word of the 80-B entry
-    }
-    return acc;
-}
-
 // 5. The lean additions leave Z = 0 from the first exceptional case on (P + P, P + (-P),
 // R = infinity), so Z == 0 (mod p) flags the tuple for the general path (exc). Otherwise
 // x(R) mod n == r is checked projectively: X == r Z^2 or, when r + n < p, X == (r + n) Z^2.
@@ -935,9 +910,6 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
         fn_mul(w, s_inv, fe_const(C_R2N));  // s^-1 R
         verify_scalars(w, valid, e_raw, r, u1, u2, neg1, neg2);
     }
-#ifdef SBFT_PAIR_TOUCH
-    const u32 touch = comb_touch(u1, gcomb);
-#endif
 
     // comb entry i of u1 (see comb_add_u1g): |d_i| 2^(16 i) G for i < 16, 2^256 G for i = 16
     auto comb_entry = [&](int i, uint4 (&en)[5], bool& dneg) {
@@ -1041,9 +1013,6 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
             p29_add_aff_pair(acc, x2, y2, odd);
         }
     }
-#ifdef SBFT_PAIR_TOUCH
-    asm volatile("" ::"v"(touch));
-#endif
     if constexpr (kQuad) {
         // lanes 0-1 add lanes 2-3's u1*G (quad_perm [2,3,2,3]); lanes 2-3 compute a discarded copy
         jp29 g;
