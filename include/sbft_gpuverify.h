@@ -76,6 +76,14 @@ const char* sbft_gv_strerror(int code);
 int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* r, const uint8_t* s,
                         const uint8_t* qx, const uint8_t* qy, size_t n, uint8_t* ok_out);
 
+/* Page-locked host memory, visible to every device of the process (hipHostMalloc, portable).
+ * When all five input arrays of sbft_gv_verify_p256 live in such memory and a device's share
+ * is large, the call overlaps the H2D copies of later sub-batches with the verify kernels of
+ * earlier ones (a cgo caller allocates its batch buffers here instead of on the Go heap).
+ * No reference counterpart: Go's heap memory is pageable. */
+int sbft_gv_host_alloc(size_t bytes, void** out);
+void sbft_gv_host_free(void* p);
+
 /* Batched SHA-256 over variable-length messages: message k = blob[off[k] .. off[k]+len[k]).
  * Replaces crypto/sha256.Sum256 per request payload. */
 int sbft_gv_sha256(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, const uint64_t* off,

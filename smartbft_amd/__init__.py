@@ -5,4 +5,4 @@ Layout:
                -> libsbft_gpuverify.so (include/sbft_gpuverify.h)
   gpuverify.py ctypes binding of that C ABI (no CPU fallback)
 """
-from .gpuverify import GpuVerifier, GpuVerifyError, load_library  # noqa: F401
+from .gpuverify import GpuVerifier, GpuVerifyError, PinnedArray, load_library  # noqa: F401

@@ -128,6 +128,21 @@ struct Slot {
     void** d_keytab = nullptr;
     size_t keytab_cap = 0;
     std::vector<void*> retired;
+    // copy stream + per-sub-batch events of the pinned-input pipeline (enqueue_verify_piped)
+    hipStream_t copy_stream = nullptr;
+    std::vector<hipEvent_t> sub_ev;
+    int reserve_pipe(size_t subs) {
+        if (!copy_stream && hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking) != hipSuccess) {
+            copy_stream = nullptr;
+            return SBFT_GV_EDEVICE;
+        }
+        while (sub_ev.size() < subs) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return SBFT_GV_EDEVICE;
+            sub_ev.push_back(e);
+        }
+        return SBFT_GV_OK;
+    }
     // pinned host staging for the small-batch (latency) path: one H2D and one D2H per call
     uint8_t* pin = nullptr;
     size_t pin_cap = 0;
@@ -308,6 +323,11 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
             (void)hipStreamSynchronize(kv.first);
             if (kv.second.ptr) (void)hipFree(kv.second.ptr);
         }
+        for (hipEvent_t e : s->sub_ev) (void)hipEventDestroy(e);
+        if (s->copy_stream) {
+            (void)hipStreamSynchronize(s->copy_stream);
+            (void)hipStreamDestroy(s->copy_stream);
+        }
         if (s->stream) (void)hipStreamDestroy(s->stream);
         delete s;
     }
@@ -315,6 +335,21 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
 }
 
 size_t sbft_gv_verify_workspace_bytes(size_t n) { return sbft_verify_work_bytes(n); }
+
+int sbft_gv_host_alloc(size_t bytes, void** out) {
+    if (!out) return SBFT_GV_EINVAL;
+    *out = nullptr;
+    if (bytes == 0) return SBFT_GV_OK;
+    if (hipHostMalloc(out, bytes, hipHostMallocPortable) != hipSuccess) {
+        *out = nullptr;
+        return SBFT_GV_ENOMEM;
+    }
+    return SBFT_GV_OK;
+}
+
+void sbft_gv_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
 
 int sbft_gv_kernel_timing(sbft_gv_ctx* ctx, int enable) {
     if (!ctx) return SBFT_GV_EINVAL;
@@ -504,6 +539,61 @@ int enqueue_verify(const Chunk& c, const uint8_t* digest, const uint8_t* r, cons
     return SBFT_GV_OK;
 }
 
+// True if p is page-locked host memory (sbft_gv_host_alloc / hipHostMalloc / registered).
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error here; clear it
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// One device round of the one-lane verify kernel (256 CUs x 4 SIMDs x 4 waves x 64 lanes):
+// the pipelined path cuts its batch into sub-batches of this size so every launch but the
+// last fills the chip, and the first exposed copy is 42 MB.
+constexpr size_t kPipeSub = 262144;
+
+// enqueue_verify for pinned inputs: the H2D copies of sub-batch i+1 run on the slot's copy
+// stream while sub-batch i verifies on the compute stream (one event per sub-batch orders
+// them). Same device layout, so the verdicts are byte-identical to enqueue_verify's.
+int enqueue_verify_piped(const Chunk& c, const uint8_t* digest, const uint8_t* r, const uint8_t* s,
+                         const uint8_t* qx, const uint8_t* qy, uint8_t* ok_out) {
+    Slot* sl = c.slot;
+    const size_t f = align_up(32 * c.count, 256);
+    HIPCHK(hipSetDevice(sl->device));
+    const size_t fo = align_up(c.count, 256);
+    int rc = sl->reserve(5 * f + fo + sbft_verify_work_bytes(kPipeSub));
+    if (rc) return rc;
+    const size_t subs = (c.count + kPipeSub - 1) / kPipeSub;
+    if ((rc = sl->reserve_pipe(subs))) return rc;
+    const void* gcomb = sl->gcomb_table();
+    if (!gcomb) return SBFT_GV_ENOMEM;
+    uint8_t* base = sl->dbuf;
+    uint32_t* work = (uint32_t*)(base + 5 * f + fo);
+    const uint8_t* src[5] = {digest, r, s, qx, qy};
+    // the copy stream must not overwrite dbuf while earlier work on the compute stream reads it
+    HIPCHK(hipEventRecord(sl->sub_ev[0], sl->stream));
+    HIPCHK(hipStreamWaitEvent(sl->copy_stream, sl->sub_ev[0], 0));
+    for (size_t i = 0; i < subs; ++i) {
+        const size_t b = i * kPipeSub, m = std::min(kPipeSub, c.count - b);
+        for (int k = 0; k < 5; ++k)
+            HIPCHK(hipMemcpyAsync(base + k * f + 32 * b, src[k] + 32 * (c.begin + b), 32 * m,
+                                  hipMemcpyHostToDevice, sl->copy_stream));
+        HIPCHK(hipEventRecord(sl->sub_ev[i], sl->copy_stream));
+    }
+    for (size_t i = 0; i < subs; ++i) {
+        const size_t b = i * kPipeSub, m = std::min(kPipeSub, c.count - b);
+        HIPCHK(hipStreamWaitEvent(sl->stream, sl->sub_ev[i], 0));
+        if (sbft_launch_p256_verify(base + 32 * b, base + f + 32 * b, base + 2 * f + 32 * b,
+                                    base + 3 * f + 32 * b, base + 4 * f + 32 * b, base + 5 * f + b,
+                                    (uint32_t)m, work, gcomb, sl->stream, nullptr, nullptr, 1))
+            return SBFT_GV_ELAUNCH;
+    }
+    HIPCHK(hipMemcpyAsync(ok_out + c.begin, base + 5 * f, c.count, hipMemcpyDeviceToHost, sl->stream));
+    return SBFT_GV_OK;
+}
+
 // Hash (and optionally verify) messages [c.begin, +c.count). Offsets are rebased to the
 // chunk's first message so each device receives only its slice of the blob.
 // framed: verify inputs are gathered on the device from the blob itself (r || s at message
@@ -646,7 +736,11 @@ int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* 
     if (!ctx) return SBFT_GV_EINVAL;
     if (n == 0) return SBFT_GV_OK;
     if (!digest || !r || !s || !qx || !qy || !ok_out || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    const bool pinned = n >= 2 * kPipeSub && is_pinned(digest) && is_pinned(r) && is_pinned(s) &&
+                        is_pinned(qx) && is_pinned(qy);
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
+        if (pinned && c.lanes == 1 && c.count >= 2 * kPipeSub)
+            return enqueue_verify_piped(c, digest, r, s, qx, qy, ok_out);
         return enqueue_verify(c, digest, r, s, qx, qy, ok_out);
     });
 }

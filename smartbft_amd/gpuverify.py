@@ -22,7 +22,7 @@ EXPORTS = [
     "sbft_gv_selftest_field", "sbft_gv_verify_workspace_bytes",
     "sbft_gv_register_key", "sbft_gv_verify_p256_keyed", "sbft_gv_sha256_verify_p256_keyed",
     "sbft_gv_kernel_timing", "sbft_gv_kernel_time", "sbft_gv_register_keys",
-    "sbft_gv_sha256_verify_p256_framed",
+    "sbft_gv_sha256_verify_p256_framed", "sbft_gv_host_alloc", "sbft_gv_host_free",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -89,8 +89,40 @@ def load_library():
     L.sbft_gv_sha256_verify_p256_keyed.argtypes = [_vp, _u8p, ctypes.c_size_t,
                                                    ctypes.POINTER(ctypes.c_uint64), _u32p, _u8p, _u8p,
                                                    _u32p, ctypes.c_size_t, _u8p]
+    L.sbft_gv_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(_vp)]
+    L.sbft_gv_host_free.argtypes = [_vp]
+    L.sbft_gv_host_free.restype = None
     _LIB = L
     return L
+
+
+class PinnedArray:
+    """Page-locked host memory from sbft_gv_host_alloc, seen as a uint8 numpy array of the
+    given shape. Verify inputs held in these let sbft_gv_verify_p256 overlap its H2D copies
+    with the kernels. Free with close() (the numpy view must not be used afterwards)."""
+
+    def __init__(self, shape):
+        self.L = load_library()
+        n = int(np.prod(shape))
+        ptr = _vp()
+        rc = self.L.sbft_gv_host_alloc(n, ctypes.byref(ptr))
+        if rc:
+            raise GpuVerifyError(f"sbft_gv_host_alloc: {self.L.sbft_gv_strerror(rc).decode()} ({rc})")
+        self.ptr = ptr
+        buf = (ctypes.c_uint8 * max(n, 1)).from_address(ptr.value) if n else bytearray(1)
+        self.array = np.frombuffer(buf, dtype=np.uint8, count=n).reshape(shape)
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            self.L.sbft_gv_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _p(a: np.ndarray):

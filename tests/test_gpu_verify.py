@@ -317,3 +317,29 @@ def test_framed_hash_then_verify(mode):
     with pytest.raises(Exception):
         gv.sha256_verify_framed(blob, np.array(off), np.array(lens), 1, -64)
     gv.close()
+
+
+def test_pinned_inputs_pipelined_host_verify(gpu):
+    """sbft_gv_verify_p256 with all five inputs in sbft_gv_host_alloc memory takes the
+    copy/compute pipeline (sub-batches of 262,144 on a copy stream + events, gpuverify.cpp
+    enqueue_verify_piped): verdicts byte-identical to the pageable path and to the workload's
+    construction, including the ragged last sub-batch."""
+    import torch
+    from smartbft_amd import PinnedArray
+    from smartbft_amd.workload import make_workload
+    n = 2 * 262144 + 4321
+    wl = make_workload(gpu, n, start=777)
+    fields = wl.host_fields(0, n)
+    pins = [PinnedArray((n, 32)) for _ in range(5)]
+    try:
+        for p, a in zip(pins, fields):
+            p.array[:] = a
+        got = gpu.verify(*[p.array for p in pins])
+        ref = gpu.verify(*fields)
+        assert np.array_equal(got, ref)
+        assert np.array_equal(got, (~wl.corrupted).to(torch.uint8).cpu().numpy())
+        again = gpu.verify(*[p.array for p in pins])  # reuses the copy stream and events
+        assert np.array_equal(again, got)
+    finally:
+        for p in pins:
+            p.close()
