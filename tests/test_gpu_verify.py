@@ -343,3 +343,26 @@ def test_pinned_inputs_pipelined_host_verify(gpu):
     finally:
         for p in pins:
             p.close()
+
+
+def test_pinned_single_allocation_and_mixed_inputs(gpu):
+    """INTEGRATION.md's layout: the five arrays at offsets inside ONE sbft_gv_host_alloc
+    block (interior pointers must be recognised as pinned), and a call where one input is
+    pageable (falls back to the plain path). Both byte-identical to the workload verdicts."""
+    import torch
+    from smartbft_amd import PinnedArray
+    from smartbft_amd.workload import make_workload
+    n = 2 * 262144 + 99
+    wl = make_workload(gpu, n, start=4242)
+    fields = wl.host_fields(0, n)
+    want = (~wl.corrupted).to(torch.uint8).cpu().numpy()
+    block = PinnedArray((5, n, 32))
+    try:
+        for k, a in enumerate(fields):
+            block.array[k] = a
+        views = [block.array[k] for k in range(5)]
+        assert np.array_equal(gpu.verify(*views), want)
+        mixed = views[:4] + [np.array(fields[4])]
+        assert np.array_equal(gpu.verify(*mixed), want)
+    finally:
+        block.close()
