@@ -132,7 +132,7 @@ def host_path(gv, wl, dev, reps: int = 3):
         out["pinned"] = {"value": round(wl.n / bp, 1), "unit": "verifies/s", "ms": round(bp * 1e3, 3),
                          "mismatches": int((okp != want).sum()),
                          "path": "sbft_gv_verify_p256, inputs in sbft_gv_host_alloc memory, "
-                                 "copy stream overlapped with 262,144-tuple verify launches"}
+                                 "copy stream overlapped with sub-batch verify launches on two compute streams"}
     finally:
         for p in pins:
             p.close()

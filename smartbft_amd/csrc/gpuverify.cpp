@@ -128,12 +128,18 @@ struct Slot {
     void** d_keytab = nullptr;
     size_t keytab_cap = 0;
     std::vector<void*> retired;
-    // copy stream + per-sub-batch events of the pinned-input pipeline (enqueue_verify_piped)
+    // copy stream, second compute stream and per-sub-batch events of the pinned-input
+    // pipeline (enqueue_verify_piped)
     hipStream_t copy_stream = nullptr;
+    hipStream_t stream2 = nullptr;
     std::vector<hipEvent_t> sub_ev;
     int reserve_pipe(size_t subs) {
         if (!copy_stream && hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking) != hipSuccess) {
             copy_stream = nullptr;
+            return SBFT_GV_EDEVICE;
+        }
+        if (!stream2 && hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking) != hipSuccess) {
+            stream2 = nullptr;
             return SBFT_GV_EDEVICE;
         }
         while (sub_ev.size() < subs) {
@@ -324,9 +330,10 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
             if (kv.second.ptr) (void)hipFree(kv.second.ptr);
         }
         for (hipEvent_t e : s->sub_ev) (void)hipEventDestroy(e);
-        if (s->copy_stream) {
-            (void)hipStreamSynchronize(s->copy_stream);
-            (void)hipStreamDestroy(s->copy_stream);
+        for (hipStream_t st : {s->copy_stream, s->stream2}) {
+            if (!st) continue;
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
         }
         if (s->stream) (void)hipStreamDestroy(s->stream);
         delete s;
@@ -549,47 +556,62 @@ bool is_pinned(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
-// One device round of the one-lane verify kernel (256 CUs x 4 SIMDs x 4 waves x 64 lanes):
-// the pipelined path cuts its batch into sub-batches of this size so every launch but the
-// last fills the chip, and the first exposed copy is 42 MB.
+// One device round of the one-lane verify kernel (256 CUs x 4 SIMDs x 4 waves x 64 lanes).
+// The pipelined path cuts its batch into a small first sub-batch (its copy is the only one
+// exposed) and then sub-batches of one round each.
 constexpr size_t kPipeSub = 262144;
+// 64k first sub-batch (10 MB, ~0.2 ms exposed); measured (profiles/r01k_pipe_sweep.txt) against
+// 16k-256k first sub-batches and one compute stream
+constexpr size_t kPipeFirst = 65536;
 
-// enqueue_verify for pinned inputs: the H2D copies of sub-batch i+1 run on the slot's copy
-// stream while sub-batch i verifies on the compute stream (one event per sub-batch orders
-// them). Same device layout, so the verdicts are byte-identical to enqueue_verify's.
+// enqueue_verify for pinned inputs: the H2D copies run on the slot's copy stream, one event
+// per sub-batch; each sub-batch's verify waits on its event and runs on one of two compute
+// streams (alternating, each with its own workspace), so a partly filled launch overlaps
+// the next one. Same device layout, so the verdicts are byte-identical to enqueue_verify's.
 int enqueue_verify_piped(const Chunk& c, const uint8_t* digest, const uint8_t* r, const uint8_t* s,
                          const uint8_t* qx, const uint8_t* qy, uint8_t* ok_out) {
     Slot* sl = c.slot;
     const size_t f = align_up(32 * c.count, 256);
     HIPCHK(hipSetDevice(sl->device));
     const size_t fo = align_up(c.count, 256);
-    int rc = sl->reserve(5 * f + fo + sbft_verify_work_bytes(kPipeSub));
+    const size_t wb = align_up(sbft_verify_work_bytes(kPipeSub), 256);
+    int rc = sl->reserve(5 * f + fo + 2 * wb);
     if (rc) return rc;
-    const size_t subs = (c.count + kPipeSub - 1) / kPipeSub;
-    if ((rc = sl->reserve_pipe(subs))) return rc;
+    std::vector<size_t> cut{0};
+        for (size_t b = std::min(kPipeFirst, c.count); b < c.count; b = std::min(b + kPipeSub, c.count)) cut.push_back(b);
+    cut.push_back(c.count);
+    const size_t subs = cut.size() - 1;
+    if ((rc = sl->reserve_pipe(subs + 2))) return rc;
+    hipStream_t cs[2] = {sl->stream, sl->stream2};
     const void* gcomb = sl->gcomb_table();
     if (!gcomb) return SBFT_GV_ENOMEM;
     uint8_t* base = sl->dbuf;
-    uint32_t* work = (uint32_t*)(base + 5 * f + fo);
     const uint8_t* src[5] = {digest, r, s, qx, qy};
-    // the copy stream must not overwrite dbuf while earlier work on the compute stream reads it
-    HIPCHK(hipEventRecord(sl->sub_ev[0], sl->stream));
-    HIPCHK(hipStreamWaitEvent(sl->copy_stream, sl->sub_ev[0], 0));
+    hipEvent_t ev_start = sl->sub_ev[subs], ev_join = sl->sub_ev[subs + 1];
+    // the copy stream and the second compute stream start after earlier work on the slot's
+    // stream (which may still read dbuf)
+    HIPCHK(hipEventRecord(ev_start, sl->stream));
+    HIPCHK(hipStreamWaitEvent(sl->copy_stream, ev_start, 0));
+    HIPCHK(hipStreamWaitEvent(sl->stream2, ev_start, 0));
     for (size_t i = 0; i < subs; ++i) {
-        const size_t b = i * kPipeSub, m = std::min(kPipeSub, c.count - b);
+        const size_t b = cut[i], m = cut[i + 1] - b;
         for (int k = 0; k < 5; ++k)
             HIPCHK(hipMemcpyAsync(base + k * f + 32 * b, src[k] + 32 * (c.begin + b), 32 * m,
                                   hipMemcpyHostToDevice, sl->copy_stream));
         HIPCHK(hipEventRecord(sl->sub_ev[i], sl->copy_stream));
     }
     for (size_t i = 0; i < subs; ++i) {
-        const size_t b = i * kPipeSub, m = std::min(kPipeSub, c.count - b);
-        HIPCHK(hipStreamWaitEvent(sl->stream, sl->sub_ev[i], 0));
+        const size_t b = cut[i], m = cut[i + 1] - b;
+        hipStream_t st = cs[i & 1];
+        uint32_t* work = (uint32_t*)(base + 5 * f + fo + (i & 1) * wb);
+        HIPCHK(hipStreamWaitEvent(st, sl->sub_ev[i], 0));
         if (sbft_launch_p256_verify(base + 32 * b, base + f + 32 * b, base + 2 * f + 32 * b,
                                     base + 3 * f + 32 * b, base + 4 * f + 32 * b, base + 5 * f + b,
-                                    (uint32_t)m, work, gcomb, sl->stream, nullptr, nullptr, 1))
+                                    (uint32_t)m, work, gcomb, st, nullptr, nullptr, 1))
             return SBFT_GV_ELAUNCH;
     }
+    HIPCHK(hipEventRecord(ev_join, sl->stream2));
+    HIPCHK(hipStreamWaitEvent(sl->stream, ev_join, 0));
     HIPCHK(hipMemcpyAsync(ok_out + c.begin, base + 5 * f, c.count, hipMemcpyDeviceToHost, sl->stream));
     return SBFT_GV_OK;
 }

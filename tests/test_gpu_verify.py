@@ -321,8 +321,8 @@ def test_framed_hash_then_verify(mode):
 
 def test_pinned_inputs_pipelined_host_verify(gpu):
     """sbft_gv_verify_p256 with all five inputs in sbft_gv_host_alloc memory takes the
-    copy/compute pipeline (sub-batches of 262,144 on a copy stream + events, gpuverify.cpp
-    enqueue_verify_piped): verdicts byte-identical to the pageable path and to the workload's
+    copy/compute pipeline (a 65,536 then 262,144-tuple sub-batches on a copy stream + events,
+    verified on two alternating compute streams: gpuverify.cpp enqueue_verify_piped): verdicts byte-identical to the pageable path and to the workload's
     construction, including the ragged last sub-batch."""
     import torch
     from smartbft_amd import PinnedArray
