@@ -68,3 +68,15 @@ def test_verify_workspace_layout():
         blocks = (n + 255) // 256
         want = ((4 * (n + 1) + 255) // 256) * 256 + 64 * n + 64 * blocks
         assert lib.sbft_gv_verify_workspace_bytes(n) == want, n
+
+
+def test_host_alloc_argument_handling():
+    """sbft_gv_host_alloc: a NULL out pointer is EINVAL, a zero-byte request succeeds with
+    *out = NULL (neither touches the device); sbft_gv_host_free(NULL) is a no-op."""
+    from smartbft_amd import gpuverify
+    lib = gpuverify.load_library()
+    assert lib.sbft_gv_host_alloc(16, None) == -1  # SBFT_GV_EINVAL
+    p = ctypes.c_void_p(1)
+    assert lib.sbft_gv_host_alloc(0, ctypes.byref(p)) == 0
+    assert p.value is None
+    lib.sbft_gv_host_free(None)
