@@ -27,14 +27,15 @@ namespace sbft {
 // Inclusive product scan mod n (Montgomery form) over the 256 lanes of the workgroup
 // (Hillis-Steele, 8 steps through LDS). suffix = true scans from lane 255 down. On return
 // buf[k][lane] holds every lane's inclusive value. Called by all 256 threads.
-SBFT_DEV void block_scan_mul_n(fe& x, u32 (*buf)[256], int tid, bool suffix) {
+template <int W>
+SBFT_DEV void block_scan_mul_n(fe& x, u32 (*buf)[W], int tid, bool suffix) {
 #pragma unroll 1
-    for (int off = 1; off < 256; off <<= 1) {
+    for (int off = 1; off < W; off <<= 1) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) buf[k][tid] = x.v[k];
         __syncthreads();
         const int src = suffix ? tid + off : tid - off;
-        if (suffix ? (src < 256) : (src >= 0)) {
+        if (suffix ? (src < W) : (src >= 0)) {
             fe y;
 #pragma unroll
             for (int k = 0; k < 8; ++k) y.v[k] = buf[k][src];
@@ -256,24 +257,63 @@ SBFT_DEV fe ld_fe(const uint4* p) {
     return r;
 }
 
-__global__ __launch_bounds__(256) void p256_sinv_prep_kernel(const uint8_t* __restrict__ ss, uint32_t n,
-                                                             sinv_ws ws) {
-    __shared__ u32 buf[8][256];
-    const int tid = threadIdx.x;
-    const uint32_t gid = blockIdx.x * 256 + tid;
-    SBFT_CHECK(blockDim.x == 256, "prep geometry", blockDim.x, 256);
-    fe x = fe_const(C_ONEN);
-    if (gid < n) {
-        const fe s = load_be32(ss + 32ull * gid);
-        if (!fe_is_zero_raw(s) && fe_lt(s, P256_N)) fn_mul(x, s, fe_const(C_R2N));
+// One wavefront per 256-tuple workgroup of the verify kernel, four consecutive tuples per
+// lane: serial prefix / suffix over the lane's four, a 64-lane scan of the lane products,
+// then each lane applies its exclusive neighbour product (~7.5 products per tuple instead of
+// the 17 of a 256-lane Hillis-Steele pair). Output as before: inclusive pre / suf within
+// the 256-tuple block, tot[b] = the block product (padding lanes contribute 1).
+__global__ __launch_bounds__(64) void p256_sinv_prep_kernel(const uint8_t* __restrict__ ss, uint32_t n,
+                                                            sinv_ws ws) {
+    __shared__ u32 buf[8][64];
+    const int lane = threadIdx.x;
+    SBFT_CHECK(blockDim.x == 64, "prep geometry", blockDim.x, 64);
+    const uint32_t g0 = blockIdx.x * 256 + lane * 4;
+    const fe one = fe_const(C_ONEN);
+    fe x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        x[j] = one;
+        if (g0 + j < n) {
+            const fe s = load_be32(ss + 32ull * (g0 + j));
+            if (!fe_is_zero_raw(s) && fe_lt(s, P256_N)) fn_mul(x[j], s, fe_const(C_R2N));
+        }
     }
-    const fe x0 = x;
-    block_scan_mul_n(x, buf, tid, false);
-    if (gid < n) st_fe(ws.pre + 2ull * gid, x);
-    if (tid == 255) st_fe(ws.tot + 2ull * blockIdx.x, x);
-    x = x0;
-    block_scan_mul_n(x, buf, tid, true);
-    if (gid < n) st_fe(ws.suf + 2ull * gid, x);
+    // prefix: p_j = x_0..x_j inside the lane, scanned across lanes
+    fe p[4];
+    p[0] = x[0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) fn_mul(p[j], p[j - 1], x[j]);
+    fe c = p[3];
+    block_scan_mul_n(c, buf, lane, false);  // inclusive over lanes; buf holds every lane's value
+    if (lane == 63) st_fe(ws.tot + 2ull * blockIdx.x, c);
+    if (lane > 0) {
+        fe e;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e.v[k] = buf[k][lane - 1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fn_mul(p[j], p[j], e);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (g0 + j < n) st_fe(ws.pre + 2ull * (g0 + j), p[j]);
+    __syncthreads();  // buf is reused by the suffix scan
+    // suffix: q_j = x_j..x_3 inside the lane, scanned across lanes from lane 63 down
+    fe q[4];
+    q[3] = x[3];
+#pragma unroll
+    for (int j = 2; j >= 0; --j) fn_mul(q[j], x[j], q[j + 1]);
+    c = q[0];
+    block_scan_mul_n(c, buf, lane, true);
+    if (lane < 63) {
+        fe e;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e.v[k] = buf[k][lane + 1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fn_mul(q[j], q[j], e);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (g0 + j < n) st_fe(ws.suf + 2ull * (g0 + j), q[j]);
 }
 
 __global__ __launch_bounds__(256) void p256_sinv_totals_kernel(uint32_t nb, sinv_ws ws) {
@@ -1076,7 +1116,7 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
     if (hipMemsetAsync(d_work, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     SBFT_STEP("memset");
     if (lanes < 2) {  // the small-batch kernels invert s themselves
-        hipLaunchKernelGGL(sbft::p256_sinv_prep_kernel, dim3(blocks), dim3(threads), 0, stream, d_s, n, ws);
+        hipLaunchKernelGGL(sbft::p256_sinv_prep_kernel, dim3(blocks), dim3(64), 0, stream, d_s, n, ws);
         SBFT_STEP("prep");
         hipLaunchKernelGGL(sbft::p256_sinv_totals_kernel, dim3(1), dim3(threads), 0, stream, (uint32_t)blocks,
                            ws);
