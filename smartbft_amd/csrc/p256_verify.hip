@@ -257,62 +257,67 @@ SBFT_DEV fe ld_fe(const uint4* p) {
     return r;
 }
 
-// One wavefront per 256-tuple workgroup of the verify kernel, four consecutive tuples per
-// lane: serial prefix / suffix over the lane's four, a 64-lane scan of the lane products,
-// then each lane applies its exclusive neighbour product (~7.5 products per tuple instead of
-// the 17 of a 256-lane Hillis-Steele pair). Output as before: inclusive pre / suf within
-// the 256-tuple block, tot[b] = the block product (padding lanes contribute 1).
-__global__ __launch_bounds__(64) void p256_sinv_prep_kernel(const uint8_t* __restrict__ ss, uint32_t n,
-                                                            sinv_ws ws) {
-    __shared__ u32 buf[8][64];
+// s^-1 groups of SBFT_SINV_GROUP tuples (1,024): each group gets inclusive pre / suf
+// products and a total tot[g]; the totals kernel turns the totals into kb[g] = 1 / tot[g].
+// One 128-lane workgroup per group, eight consecutive tuples per lane: serial prefix /
+// suffix over the lane's eight, a 128-lane scan of the lane products, then each lane
+// applies its exclusive neighbour product (~5.9 products per tuple; padding tuples are 1).
+#define SBFT_SINV_GROUP_LOG2 10
+#define SBFT_SINV_GROUP (1u << SBFT_SINV_GROUP_LOG2)
+__global__ __launch_bounds__(128) void p256_sinv_prep_kernel(const uint8_t* __restrict__ ss, uint32_t n,
+                                                             sinv_ws ws) {
+    constexpr int L = 128, T = SBFT_SINV_GROUP / L;
+    __shared__ u32 buf[8][L];
     const int lane = threadIdx.x;
-    SBFT_CHECK(blockDim.x == 64, "prep geometry", blockDim.x, 64);
-    const uint32_t g0 = blockIdx.x * 256 + lane * 4;
+    SBFT_CHECK(blockDim.x == L, "prep geometry", blockDim.x, L);
+    const uint32_t g0 = blockIdx.x * SBFT_SINV_GROUP + lane * T;
     const fe one = fe_const(C_ONEN);
-    fe x[4];
+    fe x[T];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < T; ++j) {
         x[j] = one;
         if (g0 + j < n) {
             const fe s = load_be32(ss + 32ull * (g0 + j));
             if (!fe_is_zero_raw(s) && fe_lt(s, P256_N)) fn_mul(x[j], s, fe_const(C_R2N));
         }
     }
-    // prefix: p_j = x_0..x_j inside the lane, scanned across lanes
-    fe p[4];
-    p[0] = x[0];
+    {
+        // prefix: p_j = x_0..x_j inside the lane, scanned across lanes
+        fe p[T];
+        p[0] = x[0];
 #pragma unroll
-    for (int j = 1; j < 4; ++j) fn_mul(p[j], p[j - 1], x[j]);
-    fe c = p[3];
-    block_scan_mul_n(c, buf, lane, false);  // inclusive over lanes; buf holds every lane's value
-    if (lane == 63) st_fe(ws.tot + 2ull * blockIdx.x, c);
-    if (lane > 0) {
-        fe e;
+        for (int j = 1; j < T; ++j) fn_mul(p[j], p[j - 1], x[j]);
+        fe c = p[T - 1];
+        block_scan_mul_n(c, buf, lane, false);  // inclusive over lanes; buf holds every lane's value
+        if (lane == L - 1) st_fe(ws.tot + 2ull * blockIdx.x, c);
+        if (lane > 0) {
+            fe e;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) e.v[k] = buf[k][lane - 1];
+            for (int k = 0; k < 8; ++k) e.v[k] = buf[k][lane - 1];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fn_mul(p[j], p[j], e);
+            for (int j = 0; j < T; ++j) fn_mul(p[j], p[j], e);
+        }
+#pragma unroll
+        for (int j = 0; j < T; ++j)
+            if (g0 + j < n) st_fe(ws.pre + 2ull * (g0 + j), p[j]);
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        if (g0 + j < n) st_fe(ws.pre + 2ull * (g0 + j), p[j]);
     __syncthreads();  // buf is reused by the suffix scan
-    // suffix: q_j = x_j..x_3 inside the lane, scanned across lanes from lane 63 down
-    fe q[4];
-    q[3] = x[3];
+    // suffix: q_j = x_j..x_{T-1} inside the lane, scanned across lanes from the last lane down
+    fe q[T];
+    q[T - 1] = x[T - 1];
 #pragma unroll
-    for (int j = 2; j >= 0; --j) fn_mul(q[j], x[j], q[j + 1]);
-    c = q[0];
+    for (int j = T - 2; j >= 0; --j) fn_mul(q[j], x[j], q[j + 1]);
+    fe c = q[0];
     block_scan_mul_n(c, buf, lane, true);
-    if (lane < 63) {
+    if (lane < L - 1) {
         fe e;
 #pragma unroll
         for (int k = 0; k < 8; ++k) e.v[k] = buf[k][lane + 1];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fn_mul(q[j], q[j], e);
+        for (int j = 0; j < T; ++j) fn_mul(q[j], q[j], e);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < T; ++j)
         if (g0 + j < n) st_fe(ws.suf + 2ull * (g0 + j), q[j]);
 }
 
@@ -627,17 +632,17 @@ SBFT_DEV void build_q_table_pair(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& q
     }
 }
 
-// 2-3. w = s^-1 of tuple t from the launch-wide Montgomery trick (p256_sinv_* kernels: 256
-// tuples per scan block), then u1 = e w, u2 = r w, recoded for the signed-odd ladders: an even
+// 2-3. w = s^-1 of tuple t from the launch-wide Montgomery trick (p256_sinv_* kernels: 1,024
+// tuples per scan group), then u1 = e w, u2 = r w, recoded for the signed-odd ladders: an even
 // u becomes n - u with the base negated ((n-u)(-P) = uP); u == 0 becomes n, whose ladder
 // cancels to infinity. Invalid lanes get u1 = u2 = 1.
 SBFT_DEV fe sinv_from_ws(const sinv_ws& ws, uint32_t t, uint32_t n, bool active) {
     fe w;
-    const uint32_t pos = t & 255u;
-    const fe kb = ld_fe(ws.kb + 2ull * (t >> 8));
+    const uint32_t pos = t & (SBFT_SINV_GROUP - 1);
+    const fe kb = ld_fe(ws.kb + 2ull * (t >> SBFT_SINV_GROUP_LOG2));
     const fe one = fe_const(C_ONEN);
     const fe pre = (pos > 0 && active) ? ld_fe(ws.pre + 2ull * (t - 1)) : one;
-    const fe suf = (pos < 255 && active && t + 1 < n) ? ld_fe(ws.suf + 2ull * (t + 1)) : one;
+    const fe suf = (pos < SBFT_SINV_GROUP - 1 && active && t + 1 < n) ? ld_fe(ws.suf + 2ull * (t + 1)) : one;
     fn_mul(w, kb, pre);
     fn_mul(w, w, suf);  // s^-1 * R (garbage for lanes whose s is invalid: masked by `valid`)
     return w;
@@ -1116,9 +1121,10 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
     if (hipMemsetAsync(d_work, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     SBFT_STEP("memset");
     if (lanes < 2) {  // the small-batch kernels invert s themselves
-        hipLaunchKernelGGL(sbft::p256_sinv_prep_kernel, dim3(blocks), dim3(64), 0, stream, d_s, n, ws);
+        const unsigned groups = (n + SBFT_SINV_GROUP - 1) / SBFT_SINV_GROUP;  // <= blocks: fits tot / kb
+        hipLaunchKernelGGL(sbft::p256_sinv_prep_kernel, dim3(groups), dim3(128), 0, stream, d_s, n, ws);
         SBFT_STEP("prep");
-        hipLaunchKernelGGL(sbft::p256_sinv_totals_kernel, dim3(1), dim3(threads), 0, stream, (uint32_t)blocks,
+        hipLaunchKernelGGL(sbft::p256_sinv_totals_kernel, dim3(1), dim3(threads), 0, stream, (uint32_t)groups,
                            ws);
         SBFT_STEP("totals");
     }
