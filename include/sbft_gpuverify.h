@@ -68,6 +68,13 @@ typedef struct sbft_gv_opts {
 int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out);
 void sbft_gv_destroy(sbft_gv_ctx* ctx);
 int sbft_gv_device_count(const sbft_gv_ctx* ctx);
+/* The host-side batch split every host-buffer call uses (no GPU; pure arithmetic, exported so
+ * the split is testable without devices): a batch of n >= min_split (0 = 65536) tuples on
+ * n_devices devices is cut into contiguous shares [begin[i], begin[i] + count[i]) that differ
+ * by at most one tuple, one per device in device order; a smaller batch stays whole on one
+ * device. begin / count hold n_devices entries; returns the number of shares. There is no
+ * collective: every tuple is independent. */
+size_t sbft_gv_plan_split(size_t n, size_t n_devices, size_t min_split, size_t* begin, size_t* count);
 const char* sbft_gv_strerror(int code);
 
 /* Batched P-256 ECDSA verify, host buffers, synchronous. Split over the context's devices

@@ -8,7 +8,9 @@
  * Formats (the reference defines none):
  *  signed request  "SBR1" | u16 len | client_id | u16 len | req_id | u32 len | payload |
  *                  65-byte SEC1 uncompressed public key | 64-byte r||s
- *                  signature over SHA-256(every byte before r||s); integers little-endian
+ *                  signature over SHA-256(every byte before r||s); integers little-endian;
+ *                  client_id and req_id hold no NUL byte (else the request is malformed,
+ *                  SBFT_V_EFORMAT: RequestInfos are returned as NUL-terminated records)
  *  proposal payload u32 count | count x (u32 len | signed request)
  *  consenter Msg   "SBC1" | u16 len | proposal digest (hex, Proposal.Digest()) | u32 len | aux
  *                  Signature.Value = r||s over SHA-256(Msg) by consenter ID's registered key

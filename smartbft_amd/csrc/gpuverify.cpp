@@ -201,6 +201,58 @@ struct Slot {
         return SBFT_GV_OK;
     }
 
+    // double-buffered staging of the streamed hash + verify (sbft_gv_sha256_verify_p256_stream):
+    // per window slot a device buffer, a pinned input and a pinned output buffer, and the
+    // events that order them (H2D done on the copy stream, outputs landed on the main stream)
+    struct StreamStage {
+        uint8_t* dev = nullptr;
+        size_t dev_cap = 0;
+        uint8_t* pin_in = nullptr;
+        size_t in_cap = 0;
+        uint8_t* pin_out = nullptr;
+        size_t out_cap = 0;
+        hipEvent_t h2d_done = nullptr, out_done = nullptr;
+    } stage[2];
+    int reserve_stage(int b, size_t dev_bytes, size_t in_bytes, size_t out_bytes) {
+        StreamStage& st = stage[b];
+        if (!st.h2d_done && hipEventCreateWithFlags(&st.h2d_done, hipEventDisableTiming) != hipSuccess) {
+            st.h2d_done = nullptr;
+            return SBFT_GV_EDEVICE;
+        }
+        if (!st.out_done && hipEventCreateWithFlags(&st.out_done, hipEventDisableTiming) != hipSuccess) {
+            st.out_done = nullptr;
+            return SBFT_GV_EDEVICE;
+        }
+        auto grow = [](uint8_t*& p, size_t& cap, size_t want, bool pinned) -> int {
+            if (want <= cap) return SBFT_GV_OK;
+            if (p) (void)(pinned ? hipHostFree(p) : hipFree(p));
+            p = nullptr;
+            cap = 0;
+            want = ((want + ((size_t)1 << 20) - 1) >> 20) << 20;
+            const hipError_t e = pinned ? hipHostMalloc((void**)&p, want, hipHostMallocDefault) : hipMalloc(&p, want);
+            if (e != hipSuccess) {
+                p = nullptr;
+                return SBFT_GV_ENOMEM;
+            }
+            cap = want;
+            return SBFT_GV_OK;
+        };
+        int rc = grow(st.dev, st.dev_cap, dev_bytes, false);
+        if (!rc) rc = grow(st.pin_in, st.in_cap, in_bytes, true);
+        if (!rc) rc = grow(st.pin_out, st.out_cap, out_bytes, true);
+        return rc;
+    }
+    void free_stage() {
+        for (StreamStage& st : stage) {
+            if (st.dev) (void)hipFree(st.dev);
+            if (st.pin_in) (void)hipHostFree(st.pin_in);
+            if (st.pin_out) (void)hipHostFree(st.pin_out);
+            if (st.h2d_done) (void)hipEventDestroy(st.h2d_done);
+            if (st.out_done) (void)hipEventDestroy(st.out_done);
+            st = StreamStage();
+        }
+    }
+
     int reserve(size_t bytes) {
         if (bytes <= dcap) return SBFT_GV_OK;
         if (dbuf) (void)hipFree(dbuf);
@@ -330,6 +382,7 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
             if (kv.second.ptr) (void)hipFree(kv.second.ptr);
         }
         for (hipEvent_t e : s->sub_ev) (void)hipEventDestroy(e);
+        s->free_stage();
         for (hipStream_t st : {s->copy_stream, s->stream2}) {
             if (!st) continue;
             (void)hipStreamSynchronize(st);
@@ -390,6 +443,26 @@ int sbft_gv_kernel_time(sbft_gv_ctx* ctx, uint64_t* launches, double* ms) {
 }
 
 int sbft_gv_device_count(const sbft_gv_ctx* ctx) { return ctx ? (int)ctx->slots.size() : 0; }
+
+size_t sbft_gv_plan_split(size_t n, size_t n_devices, size_t min_split, size_t* begin, size_t* count) {
+    if (n_devices == 0 || !begin || !count) return 0;
+    if (n < (min_split ? min_split : 65536) || n_devices == 1) {
+        begin[0] = 0;
+        count[0] = n;
+        return 1;
+    }
+    // contiguous shares that differ by at most one tuple; a device with none is left out
+    size_t parts = 0;
+    for (size_t d = 0; d < n_devices; ++d) {
+        const size_t b = n * d / n_devices, e = n * (d + 1) / n_devices;
+        if (e > b) {
+            begin[parts] = b;
+            count[parts] = e - b;
+            ++parts;
+        }
+    }
+    return parts;
+}
 
 void sbft_gv_normalize_hash(const uint8_t* hash, size_t len, uint8_t out32[32]) {
     // Go hashToNat (crypto/internal/fips140/ecdsa): the leftmost N.Size() = 32 bytes; a
@@ -504,16 +577,34 @@ struct Chunk {
 std::vector<Chunk> plan(sbft_gv_ctx* ctx, size_t n) {
     std::vector<Chunk> out;
     const size_t nd = ctx->slots.size();
-    if (n < ctx->min_split || nd == 1) {
+    std::vector<size_t> begin(nd), count(nd);
+    const size_t parts = sbft_gv_plan_split(n, nd, ctx->min_split, begin.data(), count.data());
+    if (parts == 1) {
+        // one device: round-robin, so concurrent small calls spread over the GPUs
         const uint32_t k = ctx->rr.fetch_add(1) % nd;
         out.push_back({ctx->slots[k], 0, n, 0, ctx->lanes_for(n)});
         return out;
     }
-    for (size_t d = 0; d < nd; ++d) {
-        const size_t b = n * d / nd, e = n * (d + 1) / nd;
-        if (e > b) out.push_back({ctx->slots[d], b, e - b, 0, ctx->lanes_for(e - b)});
-    }
+    for (size_t d = 0; d < parts; ++d)
+        out.push_back({ctx->slots[d], begin[d], count[d], 0, ctx->lanes_for(count[d])});
     return out;
+}
+
+// Run f(i) for i in [0, m): i = 0 on the calling thread, the others on threads of their own
+// (one per device chunk), so each device's pageable H2D copies and its synchronisation are
+// driven independently instead of one device after another. Returns the first non-zero rc.
+template <class F>
+int for_each_device(size_t m, F&& f) {
+    if (m == 1) return f((size_t)0);
+    std::vector<int> rc(m, SBFT_GV_OK);
+    std::vector<std::thread> th;
+    th.reserve(m - 1);
+    for (size_t i = 1; i < m; ++i) th.emplace_back([&, i] { rc[i] = f(i); });
+    rc[0] = f((size_t)0);
+    for (auto& t : th) t.join();
+    for (int r : rc)
+        if (r) return r;
+    return SBFT_GV_OK;
 }
 
 #define HIPCHK(x)                                   \
@@ -591,29 +682,40 @@ int enqueue_verify_piped(const Chunk& c, const uint8_t* digest, const uint8_t* r
     // the copy stream and the second compute stream start after earlier work on the slot's
     // stream (which may still read dbuf)
     HIPCHK(hipEventRecord(ev_start, sl->stream));
-    HIPCHK(hipStreamWaitEvent(sl->copy_stream, ev_start, 0));
-    HIPCHK(hipStreamWaitEvent(sl->stream2, ev_start, 0));
-    for (size_t i = 0; i < subs; ++i) {
-        const size_t b = cut[i], m = cut[i + 1] - b;
-        for (int k = 0; k < 5; ++k)
-            HIPCHK(hipMemcpyAsync(base + k * f + 32 * b, src[k] + 32 * (c.begin + b), 32 * m,
-                                  hipMemcpyHostToDevice, sl->copy_stream));
-        HIPCHK(hipEventRecord(sl->sub_ev[i], sl->copy_stream));
+    // From here on work may be queued on the copy stream and stream2, which the caller does not
+    // synchronise (run_chunks waits on sl->stream only): a failure drains both before it
+    // returns, so no copy or kernel is still writing dbuf when the next call reallocates it.
+    auto body = [&]() -> int {
+        HIPCHK(hipStreamWaitEvent(sl->copy_stream, ev_start, 0));
+        HIPCHK(hipStreamWaitEvent(sl->stream2, ev_start, 0));
+        for (size_t i = 0; i < subs; ++i) {
+            const size_t b = cut[i], m = cut[i + 1] - b;
+            for (int k = 0; k < 5; ++k)
+                HIPCHK(hipMemcpyAsync(base + k * f + 32 * b, src[k] + 32 * (c.begin + b), 32 * m,
+                                      hipMemcpyHostToDevice, sl->copy_stream));
+            HIPCHK(hipEventRecord(sl->sub_ev[i], sl->copy_stream));
+        }
+        for (size_t i = 0; i < subs; ++i) {
+            const size_t b = cut[i], m = cut[i + 1] - b;
+            hipStream_t st = cs[i & 1];
+            uint32_t* work = (uint32_t*)(base + 5 * f + fo + (i & 1) * wb);
+            HIPCHK(hipStreamWaitEvent(st, sl->sub_ev[i], 0));
+            if (sbft_launch_p256_verify(base + 32 * b, base + f + 32 * b, base + 2 * f + 32 * b,
+                                        base + 3 * f + 32 * b, base + 4 * f + 32 * b, base + 5 * f + b,
+                                        (uint32_t)m, work, gcomb, st, nullptr, nullptr, 1))
+                return SBFT_GV_ELAUNCH;
+        }
+        HIPCHK(hipEventRecord(ev_join, sl->stream2));
+        HIPCHK(hipStreamWaitEvent(sl->stream, ev_join, 0));
+        HIPCHK(hipMemcpyAsync(ok_out + c.begin, base + 5 * f, c.count, hipMemcpyDeviceToHost, sl->stream));
+        return SBFT_GV_OK;
+    };
+    rc = body();
+    if (rc) {
+        (void)hipStreamSynchronize(sl->copy_stream);
+        (void)hipStreamSynchronize(sl->stream2);
     }
-    for (size_t i = 0; i < subs; ++i) {
-        const size_t b = cut[i], m = cut[i + 1] - b;
-        hipStream_t st = cs[i & 1];
-        uint32_t* work = (uint32_t*)(base + 5 * f + fo + (i & 1) * wb);
-        HIPCHK(hipStreamWaitEvent(st, sl->sub_ev[i], 0));
-        if (sbft_launch_p256_verify(base + 32 * b, base + f + 32 * b, base + 2 * f + 32 * b,
-                                    base + 3 * f + 32 * b, base + 4 * f + 32 * b, base + 5 * f + b,
-                                    (uint32_t)m, work, gcomb, st, nullptr, nullptr, 1))
-            return SBFT_GV_ELAUNCH;
-    }
-    HIPCHK(hipEventRecord(ev_join, sl->stream2));
-    HIPCHK(hipStreamWaitEvent(sl->stream, ev_join, 0));
-    HIPCHK(hipMemcpyAsync(ok_out + c.begin, base + 5 * f, c.count, hipMemcpyDeviceToHost, sl->stream));
-    return SBFT_GV_OK;
+    return rc;
 }
 
 // Hash (and optionally verify) messages [c.begin, +c.count). Offsets are rebased to the
@@ -734,19 +836,19 @@ int enqueue_selftest(const Chunk& c, int op, const uint8_t* a, const uint8_t* b,
     return SBFT_GV_OK;
 }
 
+// Each device chunk is enqueued and synchronised by its own host thread (for_each_device);
+// a chunk's slot is locked by the thread that drives it.
 template <class F>
 int run_chunks(sbft_gv_ctx* ctx, size_t n, F&& enqueue) {
     std::vector<Chunk> chunks = plan(ctx, n);
-    std::vector<std::unique_lock<std::mutex>> locks;
-    locks.reserve(chunks.size());
-    for (auto& c : chunks) locks.emplace_back(c.slot->mu);
-    int rc = SBFT_GV_OK;
-    for (size_t i = 0; i < chunks.size() && rc == SBFT_GV_OK; ++i) rc = enqueue(chunks[i], i);
-    for (auto& c : chunks) {
+    return for_each_device(chunks.size(), [&](size_t i) {
+        const Chunk& c = chunks[i];
+        std::lock_guard<std::mutex> lk(c.slot->mu);
+        int rc = enqueue(c, i);
         (void)hipSetDevice(c.slot->device);
         if (hipStreamSynchronize(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
-    }
-    return rc;
+        return rc;
+    });
 }
 
 }  // namespace
@@ -903,6 +1005,184 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     return SBFT_GV_OK;
 }
 
+// ---------------------------------------------------------------- streamed hash + verify
+namespace {
+
+constexpr size_t kStreamWindowDefault = (size_t)256 << 20;  // payload bytes per window
+constexpr size_t kStreamWindowMsgs = 65536;                 // messages per window, at most
+constexpr unsigned kStageThreads = 4;                       // host threads gathering a window
+
+// Copy n items with f(i) on up to kStageThreads threads (contiguous index ranges).
+template <class F>
+void parallel_ranges(size_t n, size_t bytes, F&& f) {
+    const unsigned t = bytes >= ((size_t)8 << 20) ? kStageThreads : 1;
+    if (t == 1 || n < 2 * t) {
+        f((size_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned k = 1; k < t; ++k) th.emplace_back([&, k] { f(n * k / t, n * (k + 1) / t); });
+    f((size_t)0, n / t);
+    for (auto& x : th) x.join();
+}
+
+struct StreamArgs {
+    const uint8_t* blob;
+    size_t blob_len;
+    const uint64_t* off;
+    const uint32_t* len;
+    const uint8_t *r, *s, *qx, *qy;
+    uint8_t* ok_out;
+    uint8_t* dig_out;
+    size_t window_bytes;
+    bool blob_pinned;
+};
+
+// One device's share [c.begin, c.begin + c.count), streamed in windows through the slot's two
+// stage buffers. Window w (stage b = w & 1):
+//   host    : wait for window w-2's outputs on stage b (out_done), hand them to the caller;
+//             gather window w's messages (compacted), rebased offsets, lengths and tuple
+//             fields into the pinned input of stage b (the messages themselves are DMA'd
+//             straight from the caller's blob when it is page-locked and the window's span is
+//             dense)
+//   copy    : H2D of the stage -> device buffer b; record h2d_done
+//   compute : wait h2d_done; SHA-256 -> verify (digests stay on the device) -> D2H of the
+//             verdicts (+ digests) into the stage's pinned output; record out_done
+// so the host gathers window w+1 while the device copies and computes window w.
+int stream_chunk(sbft_gv_ctx* ctx, const Chunk& c, const StreamArgs& a) {
+    Slot* sl = c.slot;
+    HIPCHK(hipSetDevice(sl->device));
+    int rc = sl->reserve_pipe(0);  // the copy stream
+    if (rc) return rc;
+    const void* gcomb = sl->gcomb_table();
+    if (!gcomb) return SBFT_GV_ENOMEM;
+    // window boundaries (message index ranges)
+    std::vector<size_t> cut{c.begin};
+    {
+        size_t bytes = 0, msgs = 0;
+        for (size_t k = c.begin; k < c.begin + c.count; ++k) {
+            if (a.off[k] + a.len[k] > a.blob_len || a.off[k] + a.len[k] < a.off[k]) return SBFT_GV_EINVAL;
+            if (msgs && (bytes + a.len[k] > a.window_bytes || msgs == kStreamWindowMsgs)) {
+                cut.push_back(k);
+                bytes = msgs = 0;
+            }
+            bytes += a.len[k];
+            ++msgs;
+        }
+        cut.push_back(c.begin + c.count);
+    }
+    const size_t W = cut.size() - 1;
+    // per window: payload bytes, span [lo, hi) in the caller's blob, and whether the span is
+    // DMA'd in place (page-locked blob, messages laid out densely) or gathered on the host
+    std::vector<uint64_t> lo(W, UINT64_MAX), hi(W, 0), bytes(W, 0);
+    std::vector<uint8_t> direct(W);
+    size_t m = 0, dev_blob = 0, pin_blob = 0;
+    for (size_t w = 0; w < W; ++w) {
+        for (size_t k = cut[w]; k < cut[w + 1]; ++k) {
+            lo[w] = std::min(lo[w], a.off[k]);
+            hi[w] = std::max(hi[w], a.off[k] + a.len[k]);
+            bytes[w] += a.len[k];
+        }
+        const uint64_t span = hi[w] - lo[w];
+        direct[w] = a.blob_pinned && span <= bytes[w] + bytes[w] / 8 + 4096;
+        m = std::max(m, cut[w + 1] - cut[w]);
+        dev_blob = std::max<size_t>(dev_blob, direct[w] ? span : bytes[w]);
+        if (!direct[w]) pin_blob = std::max<size_t>(pin_blob, bytes[w]);
+    }
+    // stage layouts (256-B aligned regions; m = the largest window's message count):
+    //   pinned in : blob gather area (pb) | off (8 m) | len (4 m) | r | s | qx | qy (32 m each)
+    //   device    : blob (fb)             | off | len | r | s | qx | qy | hash counter (256) |
+    //               digests (32 m) | ok (m) | verify workspace
+    //   pinned out: ok (m) | digests (32 m)
+    // The hash kernel reads up to 128 B past a message: the device blob region has 256 spare.
+    const size_t fb = align_up(dev_blob + 256, 256), pb = pin_blob ? align_up(pin_blob, 256) : 0;
+    const size_t fo = align_up(8 * m, 256), fl = align_up(4 * m, 256), fd = align_up(32 * m, 256),
+                 fk = align_up(m, 256);
+    const size_t meta = fo + fl + 4 * fd;
+    const size_t dev_bytes = fb + meta + 256 + fd + fk + align_up(sbft_verify_work_bytes(m), 256);
+    for (int b = 0; b < 2; ++b)
+        if ((rc = sl->reserve_stage(b, dev_bytes, pb + meta, fk + fd))) return rc;
+    auto collect = [&](size_t w) -> int {  // outputs of window w (stage w & 1) -> caller
+        Slot::StreamStage& st = sl->stage[w & 1];
+        HIPCHK(hipEventSynchronize(st.out_done));
+        const size_t b = cut[w], mw = cut[w + 1] - b;
+        std::memcpy(a.ok_out + b, st.pin_out, mw);
+        if (a.dig_out) std::memcpy(a.dig_out + 32 * b, st.pin_out + fk, 32 * mw);
+        return SBFT_GV_OK;
+    };
+    for (size_t w = 0; w < W; ++w) {
+        Slot::StreamStage& st = sl->stage[w & 1];
+        if (w >= 2 && (rc = collect(w - 2))) return rc;
+        const size_t b = cut[w], mw = cut[w + 1] - b;
+        uint8_t* in = st.pin_in;
+        uint64_t* off_h = (uint64_t*)(in + pb);
+        uint32_t* len_h = (uint32_t*)(in + pb + fo);
+        uint8_t* tup = in + pb + fo + fl;
+        if (direct[w]) {
+            for (size_t k = 0; k < mw; ++k) off_h[k] = a.off[b + k] - lo[w];
+        } else {
+            uint64_t at = 0;
+            for (size_t k = 0; k < mw; ++k) {
+                off_h[k] = at;
+                at += a.len[b + k];
+            }
+            parallel_ranges(mw, bytes[w], [&](size_t k0, size_t k1) {
+                for (size_t k = k0; k < k1; ++k)
+                    if (a.len[b + k]) std::memcpy(in + off_h[k], a.blob + a.off[b + k], a.len[b + k]);
+            });
+        }
+        std::memcpy(len_h, a.len + b, 4 * mw);
+        const uint8_t* src4[4] = {a.r, a.s, a.qx, a.qy};
+        for (int f = 0; f < 4; ++f) std::memcpy(tup + f * fd, src4[f] + 32 * b, 32 * mw);
+        uint8_t* d = st.dev;
+        if (direct[w])
+            HIPCHK(hipMemcpyAsync(d, a.blob + lo[w], hi[w] - lo[w], hipMemcpyHostToDevice, sl->copy_stream));
+        else if (bytes[w])
+            HIPCHK(hipMemcpyAsync(d, in, bytes[w], hipMemcpyHostToDevice, sl->copy_stream));
+        HIPCHK(hipMemcpyAsync(d + fb, in + pb, meta, hipMemcpyHostToDevice, sl->copy_stream));
+        HIPCHK(hipEventRecord(st.h2d_done, sl->copy_stream));
+        HIPCHK(hipStreamWaitEvent(sl->stream, st.h2d_done, 0));
+        uint8_t* d_tup = d + fb + fo + fl;
+        uint8_t* d_ctr = d + fb + meta;
+        uint8_t* d_dig = d_ctr + 256;
+        uint8_t* d_ok = d_dig + fd;
+        uint32_t* work = (uint32_t*)(d_ok + fk);
+        if (sbft_launch_sha256(d, (const uint64_t*)(d + fb), (const uint32_t*)(d + fb + fo), nullptr, d_dig,
+                               (uint32_t)mw, (uint32_t*)d_ctr, sl->stream) ||
+            sbft_launch_p256_verify(d_dig, d_tup, d_tup + fd, d_tup + 2 * fd, d_tup + 3 * fd, d_ok, (uint32_t)mw,
+                                    work, gcomb, sl->stream, nullptr, nullptr, ctx->lanes_for(mw)))
+            return SBFT_GV_ELAUNCH;
+        HIPCHK(hipMemcpyAsync(st.pin_out, d_ok, mw, hipMemcpyDeviceToHost, sl->stream));
+        if (a.dig_out) HIPCHK(hipMemcpyAsync(st.pin_out + fk, d_dig, 32 * mw, hipMemcpyDeviceToHost, sl->stream));
+        HIPCHK(hipEventRecord(st.out_done, sl->stream));
+    }
+    for (size_t w = W >= 2 ? W - 2 : 0; w < W; ++w)
+        if ((rc = collect(w))) return rc;
+    return SBFT_GV_OK;
+}
+
+}  // namespace
+
+extern "C" int sbft_gv_sha256_verify_p256_stream(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len,
+                                                 const uint64_t* off, const uint32_t* len, const uint8_t* r,
+                                                 const uint8_t* s, const uint8_t* qx, const uint8_t* qy, size_t n,
+                                                 size_t window_bytes, uint8_t* ok_out, uint8_t* dig_out) {
+    if (!ctx) return SBFT_GV_EINVAL;
+    if (n == 0) return SBFT_GV_OK;
+    if ((!blob && blob_len) || !off || !len || !r || !s || !qx || !qy || !ok_out || n > 0xffffffffu)
+        return SBFT_GV_EINVAL;
+    StreamArgs a{blob, blob_len, off, len, r, s, qx, qy, ok_out, dig_out,
+                 window_bytes ? window_bytes : kStreamWindowDefault, blob && is_pinned(blob)};
+    // a message longer than the window gets a window of its own
+    return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
+        const int rc = stream_chunk(ctx, c, a);
+        if (rc) {  // drain the copy stream too (run_chunks waits on the main stream only)
+            (void)hipStreamSynchronize(c.slot->copy_stream);
+        }
+        return rc;
+    });
+}
+
 // ---------------------------------------------------------------- registered keys
 namespace {
 
@@ -1025,22 +1305,17 @@ int run_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* blob, size
     }
     const uint32_t nkeys = (uint32_t)keys.size();
     std::vector<Chunk> chunks = plan(ctx, n);
-    std::vector<std::unique_lock<std::mutex>> locks;
-    locks.reserve(chunks.size());
-    for (auto& c : chunks) locks.emplace_back(c.slot->mu);
-    int rc = SBFT_GV_OK;
-    for (size_t i = 0; i < chunks.size() && rc == SBFT_GV_OK; ++i) {
-        rc = build_tables(chunks[i].slot, keys, nkeys, nullptr);
-        if (rc == SBFT_GV_OK)
-            rc = enqueue_keyed(chunks[i], digest, blob, blob_len, off, len, r, s, key, nkeys);
-    }
-    for (auto& c : chunks) {
+    return for_each_device(chunks.size(), [&](size_t i) {
+        Chunk& c = chunks[i];
+        std::lock_guard<std::mutex> lk(c.slot->mu);
+        int rc = build_tables(c.slot, keys, nkeys, nullptr);
+        if (rc == SBFT_GV_OK) rc = enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys);
         (void)hipSetDevice(c.slot->device);
         if (hipStreamSynchronize(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
-    }
-    if (rc == SBFT_GV_OK)
-        for (auto& c : chunks) std::memcpy(ok_out + c.begin, c.slot->pin + c.out_off, c.count);
-    return rc;
+        // the verdicts sit in the slot's pinned staging, which the lock still protects
+        if (rc == SBFT_GV_OK) std::memcpy(ok_out + c.begin, c.slot->pin + c.out_off, c.count);
+        return rc;
+    });
 }
 
 // Small signing batches on one device: one H2D of d | k | digest through pinned staging, the

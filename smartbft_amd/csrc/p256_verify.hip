@@ -3,7 +3,8 @@
 // One verify per lane. Per lane (Go 1.24.1 crypto/ecdsa.Verify semantics, restated in
 // oracle/p256_oracle.c, which the parity tests hold this kernel to bit for bit):
 //   1. range checks r, s in [1, n-1]; Qx, Qy < p; Q on y^2 = x^3 - 3x + b
-//   2. e = digest mod n; w = s^-1 mod n (Fermat, Montgomery mod n)
+//   2. e = digest mod n; w = s^-1 mod n (batched over the launch: Montgomery's trick in
+//      1,024-tuple groups, one safegcd inversion of the product of the group totals)
 //   3. u1 = e*w, u2 = r*w
 //   4. R = u2*Q + u1*G. u2*Q: 256 doublings with radix-16 regular signed-odd digits (never
 //      zero, so every addition is live and select-free) over [1,3,..,15]Q, built per lane with
@@ -219,13 +220,13 @@ __global__ __launch_bounds__(256) void p256_verify_fixup_kernel(const uint8_t* _
 }
 
 // ------------------------------------------------------------ batched s^-1
-// Montgomery's trick over the whole launch: s_i^-1 = G^-1 * E_b * F_b * pre_{i-1} * suf_{i+1},
-// with G the product of all s, E_b / F_b the products of the block totals before / after
-// block b, and pre / suf the inclusive products inside block b. One Fermat inversion per
-// launch replaces one per lane (~11% of the per-verify instructions).
-//   prep kernel   : per block, prefix/suffix scans of s*R (LDS) -> pre, suf, tot[b]
-//   totals kernel : one workgroup: scans of tot, G^-1, K_b = G^-1 E_b F_b -> kb[b]
-//   main kernel   : w_i = K_b * pre_{i-1} * suf_{i+1}
+// Montgomery's trick over the whole launch: s_i^-1 = G^-1 * E_g * F_g * pre_{i-1} * suf_{i+1},
+// with G the product of all s, E_g / F_g the products of the group totals before / after
+// group g (groups of SBFT_SINV_GROUP = 1,024 tuples), and pre / suf the inclusive products
+// inside group g. One safegcd inversion (p256_inv.hpp) per launch replaces one per lane.
+//   prep kernel   : per group, prefix/suffix scans of s*R -> pre, suf, tot[g]
+//   totals kernel : one workgroup: scans of tot, G^-1, K_g = G^-1 E_g F_g -> kb[g]
+//   main kernel   : w_i = K_g * pre_{i-1} * suf_{i+1}
 // Lanes with s outside [1, n-1] (or past n) contribute 1, so every product is invertible.
 struct sinv_ws {
     uint4* pre;  // n x 32 B (Montgomery limbs, little-endian)
@@ -800,7 +801,7 @@ SBFT_DEV bool verify_final(const jp29& acc, const fe& rv, bool& exc) {
     return accept;
 }
 
-// Throughput kernel: one verify per lane, 256-thread workgroups (one s^-1 scan block each).
+// Throughput kernel: one verify per lane, 256-thread workgroups (four per 1,024-tuple s^-1 group).
 __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(const uint8_t* __restrict__ digest,
                                                           const uint8_t* __restrict__ rr,
                                                           const uint8_t* __restrict__ ss,

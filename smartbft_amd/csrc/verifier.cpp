@@ -318,9 +318,11 @@ bool parse_request(const uint8_t* d, size_t len, size_t base, Req& out) {
     const uint8_t* q;
     uint32_t a, b, c;
     if (!r.take(4, q) || std::memcmp(q, REQ_MAGIC, 4)) return false;
-    if (!r.u16(a) || !r.take(a, q)) return false;
+    // ids are returned as NUL-terminated "client_id\0id\0" records (write_info): an id holding
+    // a NUL would shift every later record, so such a request is malformed
+    if (!r.u16(a) || !r.take(a, q) || (a && std::memchr(q, 0, a))) return false;
     out.client_id = {(const char*)q, (int)a};
-    if (!r.u16(b) || !r.take(b, q)) return false;
+    if (!r.u16(b) || !r.take(b, q) || (b && std::memchr(q, 0, b))) return false;
     out.req_id = {(const char*)q, (int)b};
     if (!r.u32(c) || !r.take(c, q)) return false;
     if (!r.take(65, out.pub)) return false;

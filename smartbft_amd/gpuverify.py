@@ -23,6 +23,7 @@ EXPORTS = [
     "sbft_gv_register_key", "sbft_gv_verify_p256_keyed", "sbft_gv_sha256_verify_p256_keyed",
     "sbft_gv_kernel_timing", "sbft_gv_kernel_time", "sbft_gv_register_keys",
     "sbft_gv_sha256_verify_p256_framed", "sbft_gv_host_alloc", "sbft_gv_host_free",
+    "sbft_gv_plan_split",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -92,6 +93,9 @@ def load_library():
     L.sbft_gv_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(_vp)]
     L.sbft_gv_host_free.argtypes = [_vp]
     L.sbft_gv_host_free.restype = None
+    _szp = ctypes.POINTER(ctypes.c_size_t)
+    L.sbft_gv_plan_split.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, _szp, _szp]
+    L.sbft_gv_plan_split.restype = ctypes.c_size_t
     _LIB = L
     return L
 
@@ -134,6 +138,48 @@ def _soa(a, n: int) -> np.ndarray:
     if a.shape != (n, 32):
         raise ValueError(f"expected ({n}, 32) uint8, got {a.shape}")
     return a
+
+
+def _msgs(blob, off, ln):
+    """Host-side message batch: contiguous uint8 blob, uint64 offsets and uint32 lengths of
+    one length n each (the C side reads len[k] / off[k] for every k < n)."""
+    blob = np.ascontiguousarray(blob, dtype=np.uint8).reshape(-1)
+    off = np.ascontiguousarray(off, dtype=np.uint64).reshape(-1)
+    ln = np.ascontiguousarray(ln, dtype=np.uint32).reshape(-1)
+    if ln.shape != off.shape:
+        raise ValueError(f"offsets {off.shape} and lengths {ln.shape} differ")
+    return blob, off, ln, off.shape[0]
+
+
+def _key_ids(key_ids, n: int) -> np.ndarray:
+    kid = np.ascontiguousarray(key_ids, dtype=np.uint32).reshape(-1)
+    if kid.shape != (n,):
+        raise ValueError(f"expected {n} key ids, got {kid.shape}")
+    return kid
+
+
+def _dev(t, numel: int, what: str, dtype=None):
+    """A device tensor the C side reads or writes numel elements of, densely."""
+    import torch
+    if not t.is_cuda:
+        raise ValueError(f"{what}: expected a HIP device tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: tensor must be contiguous")
+    if t.numel() != numel:
+        raise ValueError(f"{what}: expected {numel} elements, got {t.numel()}")
+    if t.dtype != (dtype or torch.uint8):
+        raise ValueError(f"{what}: expected {dtype or torch.uint8}, got {t.dtype}")
+    return t.data_ptr()
+
+
+def plan_split(n: int, n_devices: int, min_split: int = 0) -> list[tuple[int, int]]:
+    """The library's host-side batch split (sbft_gv_plan_split, no GPU): [(begin, count)], one
+    contiguous share per device."""
+    L = load_library()
+    b = (ctypes.c_size_t * max(1, n_devices))()
+    c = (ctypes.c_size_t * max(1, n_devices))()
+    m = L.sbft_gv_plan_split(n, n_devices, min_split, b, c)
+    return [(b[i], c[i]) for i in range(m)]
 
 
 def normalize_hash(h: bytes) -> bytes:
@@ -218,7 +264,7 @@ class GpuVerifier:
     def verify_keyed(self, digest, r, s, key_ids) -> np.ndarray:
         n = len(digest)
         arrs = [_soa(a, n) for a in (digest, r, s)]
-        kid = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        kid = _key_ids(key_ids, n)
         ok = np.zeros(n, dtype=np.uint8)
         self._check(self.L.sbft_gv_verify_p256_keyed(
             self.ctx, *[_p(a) for a in arrs], kid.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n, _p(ok)),
@@ -226,12 +272,9 @@ class GpuVerifier:
         return ok
 
     def sha256_verify_keyed(self, blob, off, ln, r, s, key_ids) -> np.ndarray:
-        blob = np.ascontiguousarray(blob, dtype=np.uint8)
-        off = np.ascontiguousarray(off, dtype=np.uint64)
-        ln = np.ascontiguousarray(ln, dtype=np.uint32)
-        n = off.shape[0]
+        blob, off, ln, n = _msgs(blob, off, ln)
         arrs = [_soa(a, n) for a in (r, s)]
-        kid = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        kid = _key_ids(key_ids, n)
         ok = np.zeros(n, dtype=np.uint8)
         self._check(self.L.sbft_gv_sha256_verify_p256_keyed(
             self.ctx, _p(blob) if blob.size else None, blob.size,
@@ -260,16 +303,14 @@ class GpuVerifier:
 
     def sign_dev(self, d_d, d_k, d_e, d_qx, d_qy, d_r, d_s, d_status, stream=None):
         n = d_status.numel()
+        p = [_dev(t, 32 * n, w) for t, w in ((d_d, "d"), (d_k, "k"), (d_e, "digest"), (d_qx, "qx"),
+                                             (d_qy, "qy"), (d_r, "r"), (d_s, "s"))]
         self._check(self.L.sbft_gv_sign_p256_dev(
-            self.ctx, d_status.device.index, d_d.data_ptr(), d_k.data_ptr(), d_e.data_ptr(), n,
-            d_qx.data_ptr(), d_qy.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), d_status.data_ptr(),
-            self._stream(stream)), "sbft_gv_sign_p256_dev")
+            self.ctx, d_status.device.index, p[0], p[1], p[2], n, p[3], p[4], p[5], p[6],
+            _dev(d_status, n, "status"), self._stream(stream)), "sbft_gv_sign_p256_dev")
 
     def sha256(self, blob: np.ndarray, off: np.ndarray, ln: np.ndarray) -> np.ndarray:
-        blob = np.ascontiguousarray(blob, dtype=np.uint8)
-        off = np.ascontiguousarray(off, dtype=np.uint64)
-        ln = np.ascontiguousarray(ln, dtype=np.uint32)
-        n = off.shape[0]
+        blob, off, ln, n = _msgs(blob, off, ln)
         dig = np.zeros((n, 32), dtype=np.uint8)
         self._check(self.L.sbft_gv_sha256(self.ctx, _p(blob) if blob.size else None, blob.size,
                                           off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
@@ -278,10 +319,7 @@ class GpuVerifier:
         return dig
 
     def sha256_verify(self, blob, off, ln, r, s, qx, qy, want_digests=False):
-        blob = np.ascontiguousarray(blob, dtype=np.uint8)
-        off = np.ascontiguousarray(off, dtype=np.uint64)
-        ln = np.ascontiguousarray(ln, dtype=np.uint32)
-        n = off.shape[0]
+        blob, off, ln, n = _msgs(blob, off, ln)
         arrs = [_soa(a, n) for a in (r, s, qx, qy)]
         ok = np.zeros(n, dtype=np.uint8)
         dig = np.zeros((n, 32), dtype=np.uint8) if want_digests else None
@@ -295,10 +333,7 @@ class GpuVerifier:
     def sha256_verify_framed(self, blob, off, ln, sig_rel: int, pub_rel: int) -> np.ndarray:
         """Hash + verify of messages whose r || s and x || y sit in the blob at message end
         + sig_rel / + pub_rel (sbft_gv_sha256_verify_p256_framed)."""
-        blob = np.ascontiguousarray(blob, dtype=np.uint8)
-        off = np.ascontiguousarray(off, dtype=np.uint64)
-        ln = np.ascontiguousarray(ln, dtype=np.uint32)
-        n = off.shape[0]
+        blob, off, ln, n = _msgs(blob, off, ln)
         ok = np.zeros(n, dtype=np.uint8)
         self._check(self.L.sbft_gv_sha256_verify_p256_framed(
             self.ctx, _p(blob) if blob.size else None, blob.size,
@@ -317,9 +352,10 @@ class GpuVerifier:
     def verify_dev(self, d_digest, d_r, d_s, d_qx, d_qy, d_ok, stream=None):
         n = d_ok.numel()
         dev = d_ok.device.index
+        p = [_dev(t, 32 * n, w) for t, w in ((d_digest, "digest"), (d_r, "r"), (d_s, "s"), (d_qx, "qx"),
+                                             (d_qy, "qy"))]
         self._check(self.L.sbft_gv_verify_p256_dev(
-            self.ctx, dev, d_digest.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), d_qx.data_ptr(),
-            d_qy.data_ptr(), n, d_ok.data_ptr(), self._stream(stream)), "sbft_gv_verify_p256_dev")
+            self.ctx, dev, *p, n, _dev(d_ok, n, "ok"), self._stream(stream)), "sbft_gv_verify_p256_dev")
 
     def kernel_timing(self, enable: bool):
         """Record HIP events around each device-resident verify's main kernel."""
@@ -332,9 +368,18 @@ class GpuVerifier:
         return n.value, ms.value
 
     def sha256_dev(self, d_blob, d_off, d_len, d_dig, stream=None, d_order=None):
+        """d_off int64/uint64 offsets, d_len int32 lengths, d_order (optional) int32 permutation;
+        the blob must be readable 128 bytes past its last message (the hash kernel's over-read)."""
+        import torch
         n = d_off.numel()
-        self._check(self.L.sbft_gv_sha256_dev(self.ctx, d_dig.device.index, d_blob.data_ptr(),
-                                              d_off.data_ptr(), d_len.data_ptr(),
-                                              d_order.data_ptr() if d_order is not None else None,
-                                              n, d_dig.data_ptr(), self._stream(stream)),
+        if d_blob.dtype != torch.uint8 or not d_blob.is_contiguous() or not d_blob.is_cuda:
+            raise ValueError("blob: expected a contiguous uint8 device tensor")
+        if d_off.dtype not in (torch.int64, torch.uint64):
+            raise ValueError(f"offsets: expected 64-bit integers, got {d_off.dtype}")
+        p_off = _dev(d_off, n, "offsets", d_off.dtype)
+        p_len = _dev(d_len, n, "lengths", d_len.dtype if d_len.dtype in (torch.int32, torch.uint32) else torch.int32)
+        p_ord = _dev(d_order, n, "order", d_order.dtype if d_order.dtype in (torch.int32, torch.uint32)
+                     else torch.int32) if d_order is not None else None
+        self._check(self.L.sbft_gv_sha256_dev(self.ctx, d_dig.device.index, d_blob.data_ptr(), p_off, p_len,
+                                              p_ord, n, _dev(d_dig, 32 * n, "digests"), self._stream(stream)),
                     "sbft_gv_sha256_dev")

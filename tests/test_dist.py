@@ -46,3 +46,33 @@ def test_shard_range_single():
     assert shard_range(0, 1, 7) == (0, 7)
     with pytest.raises(AssertionError):
         shard_range(2, 2, 7)
+
+
+@pytest.mark.parametrize("nd", [2, 4, 8])
+@pytest.mark.parametrize("n", [0, 1, 7, 65535, 65536, 65537, 1_000_000, 8_000_003, 10_000])
+def test_library_plan_split(nd, n):
+    """The engine's in-process multi-GPU split (sbft_gv_plan_split, used by every host-buffer
+    call: one contiguous share per device, each driven by its own host thread and stream).
+    Shares tile [0, n) in device order and differ by at most one tuple; batches below
+    min_split (65,536 by default) stay whole on one device."""
+    from smartbft_amd.gpuverify import plan_split
+    parts = plan_split(n, nd)
+    if n < 65536:
+        assert parts == [(0, n)]
+        return
+    assert len(parts) == nd
+    assert parts[0][0] == 0 and sum(c for _, c in parts) == n
+    for (b0, c0), (b1, _) in zip(parts, parts[1:]):
+        assert b0 + c0 == b1
+    counts = [c for _, c in parts]
+    assert max(counts) - min(counts) <= 1
+
+
+def test_library_plan_split_min_split_and_tiny_shares():
+    from smartbft_amd.gpuverify import plan_split
+    assert plan_split(100, 8, min_split=1) == [(0, 12), (12, 13), (25, 12), (37, 13), (50, 12), (62, 13),
+                                               (75, 12), (87, 13)]
+    # fewer tuples than devices: empty shares are left out
+    assert plan_split(3, 8, min_split=1) == [(0, 1), (1, 1), (2, 1)]
+    assert plan_split(10, 1, min_split=1) == [(0, 10)]
+    assert plan_split(10, 0) == []

@@ -1,0 +1,213 @@
+"""GPU parity tests at the workloads of BASELINE.json configs 3 and 5, through the C ABI,
+against the oracle (oracle/p256_oracle.c, the C restatement of Go crypto/ecdsa.Verify) and
+hashlib-independent SHA-256 (the oracle's).
+
+Config 3: VerifyProposal (view.go:555) over a 10,000-request proposal, a distinct client key
+per request, corrupted requests at the first, middle and last index: the whole proposal is
+rejected (view.go:386-393) and the reported index is the first request the oracle rejects.
+Both the generic launch and the registered-client (keyed) launch.
+
+Config 5: hash + verify of payloads uniform in [1 KiB, 64 KiB] with corrupted signatures and
+tampered payloads, fused (tuples passed in) and framed (tuples gathered on the device from the
+signed-request layout), on the one-lane throughput kernel and the two-lane latency kernel."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+KERNEL_OPTS = {"lane": dict(pair_max=-1, quad_max=-1), "pair": dict(pair_max=1 << 30, quad_max=-1)}
+
+
+# ---------------------------------------------------------------- config 3
+@pytest.fixture(scope="module")
+def requests_10k(gpu):
+    from smartbft_amd.workload import make_signed_requests
+    return make_signed_requests(gpu, 10_000, start=31337)
+
+
+def _tuples(reqs):
+    """The (digest, r, s, qx, qy) each request's signature check verifies (signed-request
+    format of include/sbft_verifier.h: the body ends with the 65-byte SEC1 key, r || s follows)."""
+    n = len(reqs)
+    out = [np.zeros((n, 32), dtype=np.uint8) for _ in range(5)]
+    for i, q in enumerate(reqs):
+        body, sig = q[:-64], q[-64:]
+        pub = body[-65:]
+        for k, b in enumerate((hashlib.sha256(body).digest(), sig[:32], sig[32:], pub[1:33], pub[33:])):
+            out[k][i] = np.frombuffer(b, dtype=np.uint8)
+    return out
+
+
+def _corrupt(reqs, where, kind):
+    out = list(reqs)
+    for i in where:
+        q = bytearray(out[i])
+        if kind == "sig":
+            q[-40] ^= 0x10                       # a bit of s
+        elif kind == "payload":
+            q[-64 - 65 - 10] ^= 0x01             # inside the payload (signed body)
+        elif kind == "key":
+            q[-64 - 1] ^= 0x01                   # qy's last byte: off the curve
+        out[i] = bytes(q)
+    return out
+
+
+CASES = [([0], "sig"), ([5000], "sig"), ([9999], "sig"), ([9999, 5000, 0], "payload"), ([4321], "key"),
+         ([7777, 9998], "sig")]
+
+
+def _check_proposal(v, reqs, where, kind):
+    from smartbft_amd import plugin
+    bad = _corrupt(reqs, where, kind)
+    want = oracle.verify_batch(*_tuples(bad))
+    first = int(np.nonzero(want == 0)[0][0])
+    assert first == min(where) and int((want == 0).sum()) == len(set(where))
+    p = plugin.Proposal(plugin.encode_payload(bad), b"header", b"metadata", 1)
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(p)
+    assert ei.value.code == plugin.EVERIFY and ei.value.index == first
+    assert f"request {first} (client{31337 + first}:tx{31337 + first}) has an invalid signature" in str(ei.value)
+
+
+def test_config3_verify_proposal_10k_generic(gpu, requests_10k):
+    from smartbft_amd import plugin
+    reqs = requests_10k
+    assert len({q[-129:-64] for q in reqs}) == 10_000  # a distinct client key per request
+    assert oracle.verify_batch(*_tuples(reqs)).all()
+    v = plugin.Verifier(gpu, 1)
+    p = plugin.Proposal(plugin.encode_payload(reqs), b"header", b"metadata", 1)
+    infos = v.VerifyProposal(p)
+    assert [(i.ClientID, i.ID) for i in infos] == [(f"client{31337 + i}", f"tx{31337 + i}") for i in range(10_000)]
+    assert v.RequestsFromProposal(p) == infos
+    for where, kind in CASES:
+        _check_proposal(v, reqs, where, kind)
+    v.close()
+
+
+def test_config3_verify_proposal_10k_registered_clients(gpu, requests_10k):
+    """The same proposals with every client key registered (keyed comb-table launch), then with
+    half of them registered (the proposal is split over the keyed and the generic launch)."""
+    from smartbft_amd import plugin
+    reqs = requests_10k
+    p = plugin.Proposal(plugin.encode_payload(reqs), b"header", b"metadata", 1)
+    half = plugin.Verifier(gpu, 1)
+    half.add_clients([q[-129:-64] for q in reqs[::2]])
+    want = [(f"client{31337 + i}", f"tx{31337 + i}") for i in range(10_000)]
+    assert [(i.ClientID, i.ID) for i in half.VerifyProposal(p)] == want
+    for where, kind in CASES:
+        _check_proposal(half, reqs, where, kind)
+    half.close()
+    full = plugin.Verifier(gpu, 1)
+    full.add_clients([q[-129:-64] for q in reqs])
+    assert [(i.ClientID, i.ID) for i in full.VerifyProposal(p)] == want
+    for where, kind in CASES:
+        _check_proposal(full, reqs, where, kind)
+    full.close()
+
+
+# ---------------------------------------------------------------- config 5
+def _config5_batch(n, seed, sign_with_gpu=None):
+    """n messages, lengths uniform in [1 KiB, 64 KiB], each signed under its own key; ~1/5 with
+    a corrupted signature, ~1/7 with the payload tampered after signing, a few with s = 0 / r >= n.
+    Returns blob, off, len, (r, s, qx, qy), and the oracle's verdicts over SHA-256 of the
+    messages as they are in the blob."""
+    rng = np.random.default_rng(seed)
+    ln = rng.integers(1024, 65537, size=n).astype(np.uint32)
+    gaps = rng.integers(0, 4, size=n)  # unaligned message starts
+    off = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(gaps[i])
+        off[i] = pos
+        pos += int(ln[i])
+    blob = rng.integers(0, 256, size=pos, dtype=np.uint8)
+    dig = oracle.sha256_batch(blob, off, ln)
+    d = [int.from_bytes(rng.bytes(32), "big") % oracle.N or 1 for _ in range(n)]
+    k = [int.from_bytes(rng.bytes(32), "big") % oracle.N or 1 for _ in range(n)]
+    b32 = lambda xs: np.frombuffer(b"".join(x.to_bytes(32, "big") for x in xs), dtype=np.uint8).reshape(-1, 32)
+    if sign_with_gpu is not None:
+        qx, qy, r, s, st = sign_with_gpu.sign(b32(d), b32(k), dig)
+        assert st.all()
+    else:
+        qx, qy, r, s = (np.zeros((n, 32), dtype=np.uint8) for _ in range(4))
+        for i in range(n):
+            x, y = oracle.pubkey(d[i])
+            rr, ss = oracle.sign(d[i], k[i], bytes(dig[i]))
+            qx[i], qy[i], r[i], s[i] = (np.frombuffer(b, dtype=np.uint8) for b in (x, y, rr, ss))
+    for i in range(n):
+        if i % 5 == 1:
+            r[i, int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
+        elif i % 7 == 2:
+            blob[int(off[i]) + int(rng.integers(0, int(ln[i])))] ^= 0x40  # tampered after signing
+        elif i % 97 == 3:
+            s[i] = 0
+        elif i % 89 == 4:
+            r[i] = np.frombuffer(oracle.N.to_bytes(32, "big"), dtype=np.uint8)
+    dig = oracle.sha256_batch(blob, off, ln)
+    want = oracle.verify_batch(dig, r, s, qx, qy)
+    return blob, off, ln, (r, s, qx, qy), dig, want
+
+
+@pytest.mark.parametrize("mode", list(KERNEL_OPTS))
+def test_config5_fused_hash_verify_1_to_64_kib(mode):
+    import torch
+    from smartbft_amd import GpuVerifier
+    assert torch.cuda.is_available()
+    gv = GpuVerifier(**KERNEL_OPTS[mode])
+    blob, off, ln, cols, dig, want = _config5_batch(700, seed=55)
+    assert 0.5 < want.mean() < 0.8
+    ok, got_dig = gv.sha256_verify(blob, off, ln, *cols, want_digests=True)
+    assert np.array_equal(got_dig, dig)
+    assert np.array_equal(ok, want)
+    gv.close()
+
+
+@pytest.mark.parametrize("mode", list(KERNEL_OPTS))
+def test_config5_framed_hash_verify_1_to_64_kib(mode):
+    """The same payload sizes in the signed-request layout: each message is payload || qx || qy
+    (the key closes the signed body) followed by r || s; the device gathers the tuple."""
+    import torch
+    from smartbft_amd import GpuVerifier
+    assert torch.cuda.is_available()
+    gv = GpuVerifier(**KERNEL_OPTS[mode])
+    rng = np.random.default_rng(56)
+    n = 400
+    parts, off, lens, exp = [], [], [], []
+    pos = 1
+    for i in range(n):
+        d = int.from_bytes(rng.bytes(32), "big") % oracle.N or 1
+        k = int.from_bytes(rng.bytes(32), "big") % oracle.N or 1
+        qx, qy = oracle.pubkey(d)
+        body = rng.bytes(int(rng.integers(1024, 65537))) + qx + qy
+        r, s = oracle.sign(d, k, hashlib.sha256(body).digest())
+        sig = r + s
+        if i % 6 == 1:
+            sig = sig[:40] + bytes([sig[40] ^ 4]) + sig[41:]
+        if i % 9 == 2:
+            body = body[:100] + bytes([body[100] ^ 1]) + body[101:]
+        cols = (hashlib.sha256(body).digest(), sig[:32], sig[32:], body[-64:-32], body[-32:])
+        exp.append(oracle.verify_batch(*[np.frombuffer(x, dtype=np.uint8).reshape(1, 32) for x in cols])[0])
+        off.append(pos)
+        lens.append(len(body))
+        parts.append(body + sig)
+        pos += len(body) + 64
+    exp = np.array(exp, dtype=np.uint8)
+    blob = np.frombuffer(b"\0" + b"".join(parts), dtype=np.uint8)
+    got = gv.sha256_verify_framed(blob, np.array(off), np.array(lens), 0, -64)
+    assert np.array_equal(got, exp)
+    assert 0 < exp.sum() < n
+    gv.close()
+
+
+def test_config5_large_batch_throughput_kernel(gpu):
+    """40,000 messages of 1-64 KiB (~1.3 GB): above the latency kernel's 32,768-tuple limit, so
+    the one-lane kernel with its launch-wide s^-1 batching runs; signed by the engine's signer
+    (itself pinned to the oracle byte for byte in test_gpu_verify.py), verdicts vs the oracle."""
+    blob, off, ln, cols, dig, want = _config5_batch(40_000, seed=57, sign_with_gpu=gpu)
+    ok, got_dig = gpu.sha256_verify(blob, off, ln, *cols, want_digests=True)
+    assert np.array_equal(got_dig, dig)
+    assert np.array_equal(ok, want)

@@ -258,11 +258,35 @@ def test_kernels_golden_vectors(gpu_kernel, p256_vectors):
     assert len(bad) == 0, {names[c]: int((cat[bad] == c).sum()) for c in np.unique(cat[bad])}
 
 
-@pytest.mark.parametrize("n", [1, 2, 31, 32, 33, 255, 256, 257, 4097])
+# 1023/1024/1025/2049: the edges of the one-lane kernel's 1,024-tuple s^-1 groups
+# (p256_verify.hip sinv_prep/sinv_totals)
+@pytest.mark.parametrize("n", [1, 2, 31, 32, 33, 255, 256, 257, 1023, 1024, 1025, 2049, 4097])
 def test_kernels_ragged_sizes(gpu_kernel, p256_vectors, n):
     f, exp, cat, names = p256_vectors
     idx = np.arange(n) * 5 % len(exp)
     assert np.array_equal(gpu_kernel.verify(*split_fields(f[idx])), exp[idx])
+
+
+@pytest.fixture(scope="module")
+def valid_2100():
+    return _rand_tuples(2100, seed=77, corrupt_frac=0.0)
+
+
+@pytest.mark.parametrize("n", [1024, 1025, 2048, 2049, 2100])
+def test_kernels_invalid_s_at_group_edges(gpu_kernel, valid_2100, n):
+    """s = 0 and s >= n contribute 1 to the launch-wide batched s^-1 products; placed on both
+    sides of every 1,024-tuple group boundary they must neither be accepted nor poison their
+    neighbours' inverses (the whole group would then mis-verify)."""
+    f = valid_2100[:n].copy()
+    N = oracle.N.to_bytes(32, "big")
+    specials = {0: bytes(32), 1023: bytes(32), 1024: N, 1022: (oracle.N + 1).to_bytes(32, "big"),
+                2047: b"\xff" * 32, 2048: bytes(32), n - 1: N}
+    for i, val in specials.items():
+        if i < n:
+            f[i, 64:96] = np.frombuffer(val, dtype=np.uint8)
+    exp = oracle.verify_batch(*split_fields(f))
+    assert exp.sum() == n - len([i for i in specials if i < n])
+    assert np.array_equal(gpu_kernel.verify(*split_fields(f)), exp)
 
 
 def test_kernels_random_batch(gpu_kernel):

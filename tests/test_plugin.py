@@ -101,6 +101,25 @@ def test_requests_from_proposal_parse_only():
         v.VerifyProposal(p)
 
 
+@pytest.mark.parametrize("cid,rid", [("cl\0ient", "r1"), ("client", "r\0"), ("\0", "x")])
+def test_nul_inside_an_id_is_malformed(cid, rid):
+    """RequestInfos leave the C ABI as NUL-terminated "client_id\\0id\\0" records: an id holding a
+    NUL would shift every later record (wrong ClientID/ID pairs for the pool). Such a request is
+    malformed on every path: VerifyRequest, the batch form, and the proposal parse."""
+    v = plugin.Verifier(None)
+    bad = _fake_request(cid, rid, b"p")
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyRequest(bad)
+    assert ei.value.code == plugin.EFORMAT
+    assert v.VerifyRequests([bad]) == [plugin.EFORMAT]
+    good = [_fake_request(f"c{i}", f"r{i}", b"") for i in range(3)]
+    assert len(v.RequestsFromProposal(plugin.Proposal(plugin.encode_payload(good)))) == 3
+    assert v.RequestsFromProposal(plugin.Proposal(plugin.encode_payload(good[:1] + [bad] + good[1:]))) == []
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(plugin.Proposal(plugin.encode_payload(good[:1] + [bad] + good[1:])))
+    assert ei.value.code == plugin.EFORMAT
+
+
 def test_auxiliary_data():
     aux = b"prepares-from"
     msg = b"SBC1" + (64).to_bytes(2, "little") + b"a" * 64 + len(aux).to_bytes(4, "little") + aux
