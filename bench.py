@@ -43,7 +43,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1_000_000, help="tuples per GPU")
     ap.add_argument("--cpu-sample", type=int, default=131072)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads for the CPU baselines (0 = every core this job may use: "
+                         "sched_getaffinity capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip configs 3/4 latency")
     ap.add_argument("--latency-calls", type=int, default=200)
@@ -53,6 +55,62 @@ def parse():
                     help="config 5: 16M requests over 8 GPUs = 2M per GPU (~68 GB of payload in HBM)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_verify_latest.json"))
     return ap.parse_args()
+
+
+def host_cores() -> dict:
+    """The host cores this job may use: the affinity mask, capped by the cgroup CPU quota
+    (cgroup v2 cpu.max or v1 cfs_quota_us / cfs_period_us) when one is set."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    used = aff if quota is None else max(1, min(aff, int(quota)))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"affinity": aff, "cgroup_quota_cores": quota, "cores_available": used, "cpu": model}
+
+
+def _openssl_rate(tuples: np.ndarray, threads: int, seconds: float):
+    exe = os.path.join(ROOT, "oracle", "openssl_bench")
+    if not os.path.exists(exe):
+        return None
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as tf:
+        tf.write(tuples.tobytes())
+        path = tf.name
+    try:
+        out = subprocess.run([exe, path, str(threads), str(seconds)], capture_output=True, text=True, timeout=300)
+        if out.returncode != 0:
+            return None
+        return json.loads(out.stdout.strip().splitlines()[-1])
+    finally:
+        os.unlink(path)
+
+
+def _harness(*args, timeout=600):
+    """tools/latency_harness (per-call latency of configs 3 and 4, GPU and CPU); None if absent."""
+    exe = os.path.join(ROOT, "tools", "latency_harness")
+    if not os.path.exists(exe):
+        return None
+    out = subprocess.run([exe, *[str(a) for a in args]], capture_output=True, text=True, timeout=timeout)
+    if out.returncode != 0:
+        raise RuntimeError(f"latency_harness {args}: rc={out.returncode} {out.stderr[-500:]}")
+    return json.loads(out.stdout.strip().splitlines()[-1])
 
 
 def cpu_baseline(wl, sample: int, threads: int):
@@ -68,51 +126,42 @@ def cpu_baseline(wl, sample: int, threads: int):
     port = {"value": round(sample / dt, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
             "sample": f"first {sample} tuples of the bench workload, oracle/p256_oracle.c "
                       f"(C restatement of Go crypto/ecdsa.Verify), {threads} pthreads, {dt:.2f} s"}
+    # OpenSSL ECDSA_do_verify (ecp_nistz256 assembly): the stand-in for Go's assembly P-256,
+    # on one core and on every core this job may use (openssl_bench times only tuples whose
+    # key decodes: a Go plugin rejects an undecodable key before any arithmetic)
     go_proxy = None
-    exe = os.path.join(ROOT, "oracle", "openssl_bench")
-    if os.path.exists(exe):
-        with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as tf:
-            tf.write(np.concatenate(f, axis=1).tobytes())
-            path = tf.name
-        try:
-            out = subprocess.run([exe, path, str(threads), "10"], capture_output=True, text=True,
-                                 timeout=120)
-            if out.returncode == 0:
-                j = json.loads(out.stdout.strip().splitlines()[-1])
-                go_proxy = {"value": j["verifies_per_s"], "unit": "verifies/s", "cores": threads,
-                            "kind": "fallback: OpenSSL 3.0.2 ECDSA_do_verify, not Go (Go absent)",
-                            "sample": f"{sample} workload tuples cycled for {j['seconds']:.1f} s"}
-        finally:
-            os.unlink(path)
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    port["cpu"] = cpu_model
-    if go_proxy:
-        go_proxy["cpu"] = cpu_model
+    tuples = np.concatenate(f, axis=1)
+    one = _openssl_rate(tuples, 1, 4)
+    allc = _openssl_rate(tuples, threads, 8)
+    hc = host_cores()
+    port["cpu"] = hc["cpu"]
+    port["cores_available"] = hc["cores_available"]
+    if allc:
+        go_proxy = {"value": allc["verifies_per_s"], "unit": "verifies/s", "cores": threads,
+                    "kind": "fallback: OpenSSL 3.0.2 ECDSA_do_verify, not Go (Go absent)",
+                    "sample": f"{sample} workload tuples cycled for {allc['seconds']:.1f} s on {threads} threads",
+                    "single_core": one["verifies_per_s"] if one else None,
+                    "cpu": hc["cpu"], "cores_available": hc["cores_available"], "host": hc}
     return port, go_proxy, ok_cpu
 
 
-def host_path(gv, wl, dev, reps: int = 3):
+def host_path(gv, wls, dev, reps: int = 3):
     """PCIe-inclusive rate of the host-buffer C ABI (sbft_gv_verify_p256: the call a cgo
     plugin makes with Go-heap tuples): H2D of 160 B/tuple + verify pipeline + D2H of verdicts,
-    on the same 1M tuples. Reported beside `value`, never as it."""
-    f = [np.ascontiguousarray(a) for a in wl.host_fields(0, wl.n)]
+    on the same tuples (every device's; one call, split over the context's devices, each
+    device's share on a host thread of its own). Reported beside `value`, never as it."""
+    f = [np.ascontiguousarray(np.concatenate(parts)) for parts in zip(*[w.host_fields(0, w.n) for w in wls])]
+    n = len(f[0])
     ok = gv.verify(*f)  # warm-up (workspace growth)
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
         ok = gv.verify(*f)
         ts.append(time.perf_counter() - t0)
-    want = (~wl.corrupted).to(torch.uint8).cpu().numpy()
+    want = np.concatenate([(~w.corrupted).to(torch.uint8).cpu().numpy() for w in wls])
     best = min(ts)
-    out = {"value": round(wl.n / best, 1), "unit": "verifies/s", "ms": round(best * 1e3, 3),
-           "mismatches": int((ok != want).sum()),
+    out = {"value": round(n / best, 1), "unit": "verifies/s", "ms": round(best * 1e3, 3),
+           "mismatches": int((ok != want).sum()), "devices": gv.device_count,
            "path": "sbft_gv_verify_p256, pageable host buffers, H2D + kernels + D2H"}
     # the same call with the inputs in sbft_gv_host_alloc memory: H2D of later sub-batches
     # overlaps the kernels of earlier ones (gpuverify.cpp enqueue_verify_piped)
@@ -129,7 +178,7 @@ def host_path(gv, wl, dev, reps: int = 3):
             okp = gv.verify(*pa)
             tp.append(time.perf_counter() - t0)
         bp = min(tp)
-        out["pinned"] = {"value": round(wl.n / bp, 1), "unit": "verifies/s", "ms": round(bp * 1e3, 3),
+        out["pinned"] = {"value": round(n / bp, 1), "unit": "verifies/s", "ms": round(bp * 1e3, 3),
                          "mismatches": int((okp != want).sum()),
                          "path": "sbft_gv_verify_p256, inputs in sbft_gv_host_alloc memory, "
                                  "copy stream overlapped with sub-batch verify launches on two compute streams"}
@@ -229,72 +278,103 @@ def latency_configs(gv, calls: int):
     out["commit_quorum_n100"] = {"p50_ms": p50, "p99_ms": p99, "calls": calls, "signatures": q,
                                  "python_wrapper_p50_ms": _pcts(tp)[0],
                                  "path": "sbft_verifier_verify_consenter_sigs (C ABI), host buffers"}
+    # the unmodified library: 66 goroutines (view.go:537-541), one VerifyConsenterSig each
+    # (:834), released together per decision (tools/latency_harness quorum-gpu); stock = one
+    # launch per call, coalesced = sbft_verifier_coalesce_consenter_sigs(66, 50 us)
+    stock = _harness("quorum-gpu", 66, calls, 0, 0)
+    coal = _harness("quorum-gpu", 66, calls, 66, 50)
+    if stock and coal:
+        assert stock["wrong_verdicts"] == 0 and coal["wrong_verdicts"] == 0
+        out["commit_quorum_n100_concurrent_singles"] = {
+            "stock": stock, "coalesced": coal,
+            "path": "66 threads, one sbft_verifier_verify_consenter_sig each per decision; every 10th "
+                    "decision has one bad vote, whose caller must get its own EVERIFY"}
     return out
 
 
-def sha_config5(gv, dev, n_msgs: int, uniform_len: int = 0):
-    """BASELINE config 5's hashing stage on one GPU: payload lengths uniform in [1 KiB, 64 KiB]
-    (seeded), device-resident, SHA-256 kernel only (kernel-time GB/s of payload bytes). A sample of
-    digests is checked against hashlib."""
+def sha_config5(gv, dev, n_msgs: int, e2e_msgs: int = 65536):
+    """BASELINE config 5 on one GPU: requests with payload lengths uniform in [1 KiB, 64 KiB]
+    (seeded; 2M per GPU = the 16M of config 5 over 8 GPUs), each signed under its own key,
+    ~10% corrupted (smartbft_amd/workload.py make_config5).
+      - hash only: the SHA-256 kernel on the HBM-resident payloads (kernel time);
+      - hash + verify: sbft_gv_sha256_verify_p256_dev, digests never leave the GPU (kernel
+        time of the SHA + verify launches); parity: verdict == not corrupted, every request;
+      - streamed end to end from host memory: sbft_gv_sha256_verify_p256_stream on the first
+        e2e_msgs requests (~2 GB), from pageable and from page-locked memory (PCIe included);
+        verdicts equal the device-resident ones."""
     import hashlib
-    rng = np.random.default_rng(5)
-    ln = rng.integers(1024, 65537, size=n_msgs).astype(np.uint32)
-    if uniform_len:  # diagnostics: every message the same length
-        ln[:] = uniform_len
-    off = np.concatenate([[0], np.cumsum(ln.astype(np.uint64))[:-1]]).astype(np.uint64)
-    total = int(ln.astype(np.uint64).sum())
-    g = torch.Generator(device=dev)
-    g.manual_seed(5)
-    blob = torch.randint(0, 256, (total + 128,), dtype=torch.uint8, device=dev, generator=g)
-    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
-    d_len = torch.from_numpy(ln.astype(np.int32)).to(dev)
-    dig = torch.empty((n_msgs, 32), dtype=torch.uint8, device=dev)
+    from smartbft_amd import PinnedArray
+    from smartbft_amd.workload import make_config5
+    c5 = make_config5(gv, n_msgs, device=dev.index)
+    n = c5.n
     stream = torch.cuda.current_stream(dev)
-    gv.sha256_dev(blob, d_off, d_len, dig, stream)
+    dig = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    gv.sha256_dev(c5.blob, c5.d_off, c5.d_len, dig, stream)
     torch.cuda.synchronize(dev)
-    for i in (0, n_msgs // 2, n_msgs - 1):
-        m = blob[int(off[i]):int(off[i]) + int(ln[i])].cpu().numpy().tobytes()
+    for i in (0, n // 2, n - 1):
+        m = c5.blob[int(c5.off[i]):int(c5.off[i]) + int(c5.ln[i])].cpu().numpy().tobytes()
         assert dig[i].cpu().numpy().tobytes() == hashlib.sha256(m).digest(), i
     # the d_order path (messages taken in a permuted sequence) must give the same digests
-    order = torch.flip(torch.arange(n_msgs, device=dev, dtype=torch.int32), [0])
+    order = torch.flip(torch.arange(n, device=dev, dtype=torch.int32), [0])
     dig2 = torch.empty_like(dig)
-    gv.sha256_dev(blob, d_off, d_len, dig2, stream, d_order=order)
+    gv.sha256_dev(c5.blob, c5.d_off, c5.d_len, dig2, stream, d_order=order)
     torch.cuda.synchronize(dev)
     assert torch.equal(dig, dig2), "permuted-order SHA-256 differs from index order"
+    del dig2, order
 
-    def timed(o):
+    def timed(fn, reps=3):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 3
+        fn()
         e0.record(stream)
         for _ in range(reps):
-            gv.sha256_dev(blob, d_off, d_len, dig, stream, d_order=o)
+            fn()
         e1.record(stream)
         torch.cuda.synchronize(dev)
         return e0.elapsed_time(e1) / 1e3 / reps
 
-    sec = timed(None)  # index order: the load-balanced kernel needs no length sort
-    gbs = (total + 32 * n_msgs) / sec / 1e9
-    # end to end from host memory (the host-buffer C ABI: pageable H2D + kernel + D2H) on a
-    # bounded sample of the same messages: 65,536 messages, ~2.1 GB
-    k = min(n_msgs, 65536)
-    hb = blob[:int(off[k - 1]) + int(ln[k - 1])].cpu().numpy()
-    gv.sha256(hb, off[:k], ln[:k])  # warm-up (staging growth)
+    nbytes = c5.total + 32 * n
+    sec_h = timed(lambda: gv.sha256_dev(c5.blob, c5.d_off, c5.d_len, dig, stream))
+    hv = lambda: gv.sha256_verify_dev(c5.blob, c5.d_off, c5.d_len, c5.r, c5.s, c5.qx, c5.qy, ok, dig, stream)
+    sec_hv = timed(hv)
+    want = (~c5.corrupted).to(torch.uint8)
+    mism = int((ok != want).sum())
+    # streamed from host memory, bounded sample of the same requests
+    k = min(n, e2e_msgs)
+    span = int(c5.off[k - 1]) + int(c5.ln[k - 1])
+    hb = c5.blob[:span].cpu().numpy()
+    cols = [t[:k].cpu().numpy() for t in (c5.r, c5.s, c5.qx, c5.qy)]
+    want_k = ok[:k].cpu().numpy()
+    gv.sha256_verify_stream(hb, c5.off[:k], c5.ln[:k], *cols)  # warm-up (staging growth)
     t0 = time.perf_counter()
-    hd = gv.sha256(hb, off[:k], ln[:k])
+    ok_e = gv.sha256_verify_stream(hb, c5.off[:k], c5.ln[:k], *cols)
     e2e = time.perf_counter() - t0
-    assert hd[k - 1].tobytes() == dig[k - 1].cpu().numpy().tobytes()
-    e2e_gbs = (hb.size + 32 * k) / e2e / 1e9
-    del blob, hb
-    return {"value": round(gbs, 1), "unit": "GB/s (payload + digest bytes, kernel time)",
-            "messages": n_msgs, "payload_bytes": total, "avg_kernel_ms": round(sec * 1e3, 3),
-            "end_to_end": {"value": round(e2e_gbs, 1), "unit": "GB/s", "messages": k,
-                           "path": "sbft_gv_sha256 from pageable host memory (H2D + kernel + D2H)"},
-            "roofline": {"bound": "valu", "hbm_peak_GBs": 8000, "frac_of_hbm": round(gbs / 8000, 4),
-                         "valu_ceiling_GBs": 1840,
-                         "frac_of_valu_ceiling": round(gbs / 1840, 4),
-                         "note": "one lane per message; 1,421 VALU instructions per 64-B block (22.2/B) "
-                                 "cap SHA-256 at ~1.84 TB/s on MI355X (tools/sha_ceiling.hip, "
-                                 "register-resident blocks), below HBM"}}
+    pin = PinnedArray(hb.shape)
+    try:
+        pin.array[:] = hb
+        gv.sha256_verify_stream(pin.array, c5.off[:k], c5.ln[:k], *cols)
+        t0 = time.perf_counter()
+        ok_p = gv.sha256_verify_stream(pin.array, c5.off[:k], c5.ln[:k], *cols)
+        e2e_p = time.perf_counter() - t0
+    finally:
+        pin.close()
+    e2e_bytes = span + 32 * k
+    del hb
+    gbs_h, gbs_hv = nbytes / sec_h / 1e9, nbytes / sec_hv / 1e9
+    return {"value": round(gbs_h, 1), "unit": "GB/s (payload + digest bytes, kernel time)",
+            "messages": n, "payload_bytes": c5.total, "avg_kernel_ms": round(sec_h * 1e3, 3),
+            "roofline": {"bound": "valu", "hbm_peak_GBs": 8000, "frac_of_hbm": round(gbs_h / 8000, 4)},
+            "hash_verify": {"value": round(gbs_hv, 1), "unit": "GB/s (payload + digest bytes, kernel time)",
+                            "verifies_per_s": round(n / sec_hv, 1), "ms": round(sec_hv * 1e3, 3),
+                            "mismatches": mism, "expected_accepts": int(want.sum()),
+                            "path": "sbft_gv_sha256_verify_p256_dev: SHA-256 -> verify, digests stay in HBM"},
+            "streamed": {"pageable": {"value": round(e2e_bytes / e2e / 1e9, 1), "unit": "GB/s",
+                                      "mismatches": int((ok_e != want_k).sum())},
+                         "pinned": {"value": round(e2e_bytes / e2e_p / 1e9, 1), "unit": "GB/s",
+                                    "mismatches": int((ok_p != want_k).sum())},
+                         "messages": k, "bytes": e2e_bytes,
+                         "path": "sbft_gv_sha256_verify_p256_stream: 64 MiB windows, double-buffered "
+                                 "staging (H2D of window w+1 || SHA -> verify of window w), PCIe included"}}
 
 
 def main():
@@ -314,22 +394,41 @@ def main():
 
     from smartbft_amd.dist import reduce_timing, shard_range
 
-    gv = GpuVerifier(device_mask=1 << local)
+    # devices this process drives: one under torchrun (one process per GPU), or all --gpus of
+    # them in one process (the library's in-process multi-device path: one context over N
+    # devices, each device's launch enqueued on its own stream, no collective)
+    if world > 1:
+        assert world == args.gpus, f"WORLD_SIZE={world} but --gpus {args.gpus}"
+        devs = [local]
+    else:
+        avail = torch.cuda.device_count()
+        assert args.gpus <= avail, f"--gpus {args.gpus} but {avail} visible devices"
+        devs = list(range(args.gpus))
+    gv = GpuVerifier(device_mask=sum(1 << d for d in devs))
+    assert gv.device_count == len(devs)
     n = args.n
-    lo, _ = shard_range(rank, world, n)
-    wl = make_workload(gv, n, start=lo, device=local)
-    ok = torch.empty(n, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    wls, oks, streams = [], [], []
+    for j, d in enumerate(devs):
+        lo, _ = shard_range(rank * len(devs) + j, world * len(devs), n)
+        wls.append(make_workload(gv, n, start=lo, device=d))
+        oks.append(torch.empty(n, dtype=torch.uint8, device=f"cuda:{d}"))
+        streams.append(torch.cuda.current_stream(torch.device(f"cuda:{d}")))
+    wl, ok, stream = wls[0], oks[0], streams[0]
 
     def step():
-        gv.verify_dev(wl.digest, wl.r, wl.s, wl.qx, wl.qy, ok, stream)
+        for w, o, st in zip(wls, oks, streams):  # asynchronous: every device runs concurrently
+            gv.verify_dev(w.digest, w.r, w.s, w.qx, w.qy, o, st)
+
+    def sync_all():
+        for d in devs:
+            torch.cuda.synchronize(d)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync_all()
     # parity property at full size: verdict == not corrupted, for every tuple
     expect = (~wl.corrupted).to(torch.uint8)
-    mismatches = int((ok != expect).sum())
+    mismatches = sum(int((o != (~w.corrupted).to(torch.uint8)).sum()) for w, o in zip(wls, oks))
 
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -339,13 +438,13 @@ def main():
     gv.kernel_time()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync_all()
     t0 = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
         step()
         ends[i].record(stream)
-    torch.cuda.synchronize(dev)
+    sync_all()
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
@@ -354,11 +453,12 @@ def main():
     avg_step_gpu_ms = sum(step_ms) / len(step_ms)
     launches, kern_total_ms = gv.kernel_time()
     gv.kernel_timing(False)
-    assert launches == args.steps, (launches, args.steps)
+    assert launches == args.steps * len(devs), (launches, args.steps)
     avg_kern_s = kern_total_ms / launches / 1e3
+    n_gpus = world * len(devs)
 
     if rank == 0:
-        total = n * world * args.steps
+        total = n * n_gpus * args.steps
         value = total / elapsed
         achieved_t = n * PRODUCTS_PER_VERIFY / avg_kern_s / 1e12
         traffic = None
@@ -375,7 +475,7 @@ def main():
             "metric": "P-256 ECDSA verifies/sec",
             "value": round(value, 1),
             "unit": "verifies/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -386,10 +486,17 @@ def main():
             "data": "synthetic (on-GPU seeded keys/signatures, ~10% corrupted; smartbft_amd/workload.py)",
             "config": {"workload": "BASELINE config 2: synthetic P-256 verifies, 32-byte SHA-256 digests, "
                                    "distinct key per tuple, 10% corrupted, device-resident",
-                       "tuples_per_gpu": n, "parallelism": f"batch split x{world} (no collective)"},
+                       "tuples_per_gpu": n,
+                       "parallelism": (f"one process per GPU x{world}" if world > 1 else
+                                       f"in-process multi-device x{len(devs)}") + " (no collective)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_t, 3), "peak": MAD_PEAK_T,
                          "unit": "T 32x32->64 products/s (v_mad_i64_i32 issue rate)",
                          "frac": round(achieved_t / MAD_PEAK_T, 4), "traffic": traffic,
+                         # rocprofv3 cannot run inside this process: traffic (FETCH_SIZE +
+                         # WRITE_SIZE per launch) and valu_issue come from the committed PMC passes
+                         # of the same kernel (tools/pmc_summary.py -> --traffic-file), not this run
+                         "traffic_source": (os.path.relpath(args.traffic_file, ROOT) +
+                                            " (committed rocprofv3 --pmc passes, not this run)") if traffic else None,
                          "kernel": "p256_verify_kernel", "avg_kernel_ms": round(avg_kern_s * 1e3, 4),
                          "kernel_timing": "HIP events around p256_verify_kernel on its launch stream",
                          "step_gpu_ms": round(avg_step_gpu_ms, 4),
@@ -404,10 +511,11 @@ def main():
                 "peak_T": VALU_ISSUE_PEAK_T, "frac": round(instr_per_verify * n / avg_kern_s / 1e12 / VALU_ISSUE_PEAK_T, 3),
                 "frac_at_2_05GHz": round(instr_per_verify * n / avg_kern_s / 1e12 / (VALU_ISSUE_PEAK_T * 2.05 / 2.4), 3)},
             "parity": {"full_size_mismatches": mismatches,
-                       "expected_accepts": int(expect.sum()) * world},
+                       "expected_accepts": int(expect.sum()) * n_gpus},
         }
-        if world == 1 and not args.no_cpu_baseline:
-            port, go_proxy, ok_cpu = cpu_baseline(wl, args.cpu_sample, args.cpu_threads)
+        if n_gpus == 1 and not args.no_cpu_baseline:
+            cpu_threads = args.cpu_threads or host_cores()["cores_available"]
+            port, go_proxy, ok_cpu = cpu_baseline(wl, args.cpu_sample, cpu_threads)
             rec["cpu_baseline"] = port
             if go_proxy:
                 rec["cpu_baseline_go_proxy"] = go_proxy
@@ -417,15 +525,27 @@ def main():
             if go_proxy:
                 rec["speedup_vs_go_proxy"] = round(value / go_proxy["value"], 1)
         if world == 1 and not args.no_host_path:
-            rec["host_buffer_path"] = host_path(gv, wl, dev)
-        if world == 1 and not args.no_sha:
+            rec["host_buffer_path"] = host_path(gv, wls, dev)
+        if n_gpus == 1 and not args.no_sha:
             rec["sha256_config5"] = sha_config5(gv, dev, args.sha_messages)
-        if world == 1 and not args.no_latency:
+        if n_gpus == 1 and not args.no_latency:
             lat = latency_configs(gv, args.latency_calls)
-            if "cpu_baseline_go_proxy" in rec:
-                thr = rec["cpu_baseline_go_proxy"]["value"]
-                lat["verify_proposal_10k"]["cpu_go_proxy_ms_estimate"] = round(10_000 / thr * 1e3, 3)
-                lat["commit_quorum_n100"]["cpu_go_proxy_ms_estimate"] = round(67 / thr * 1e3, 3)
+            if not args.no_cpu_baseline:
+                # measured CPU latencies of the same calls (tools/latency_harness, OpenSSL):
+                # VerifyProposal's 10k verifies over every core this job may use, and the
+                # commit quorum's 66 votes with one thread per vote (view.go:537-541), capped
+                # at the cores available
+                cores = args.cpu_threads or host_cores()["cores_available"]
+                pc = _harness("proposal-cpu", 10_000, 20, cores)
+                qc = _harness("quorum-cpu", 66, 200, min(66, cores))
+                if pc:
+                    lat["verify_proposal_10k"]["cpu_openssl"] = pc
+                    lat["verify_proposal_10k"]["speedup_p50_vs_cpu"] = round(
+                        pc["p50_ms"] / lat["verify_proposal_10k"]["p50_ms"], 1)
+                if qc and "commit_quorum_n100_concurrent_singles" in lat:
+                    lat["commit_quorum_n100_concurrent_singles"]["cpu_openssl"] = qc
+                    lat["commit_quorum_n100_concurrent_singles"]["speedup_p50_vs_cpu"] = round(
+                        qc["p50_ms"] / lat["commit_quorum_n100_concurrent_singles"]["coalesced"]["p50_ms"], 1)
             rec["latency"] = lat
         print(json.dumps(rec), flush=True)
     if world > 1:

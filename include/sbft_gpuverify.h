@@ -114,6 +114,23 @@ int sbft_gv_sha256_verify_p256_framed(sbft_gv_ctx* ctx, const uint8_t* blob, siz
                                       const uint64_t* off, const uint32_t* len, size_t n, int32_t sig_rel,
                                       int32_t pub_rel, uint8_t* ok_out);
 
+/* Streamed hash + verify of a batch far larger than one launch (BASELINE config 5: requests
+ * with 1-64 KiB payloads, hashed on the GPU, then verified). Same inputs and outputs as
+ * sbft_gv_sha256_verify_p256 (dig_out may be NULL). Each device takes a contiguous share of the
+ * messages (sbft_gv_plan_split) on a host thread of its own and streams it in windows of about
+ * window_bytes of payload (0 = 64 MiB) through two staging buffers: while the device hashes
+ * and verifies window w, the host thread stages and copies window w+1. Windows whose messages
+ * lie densely in the blob are DMA'd in place (at the full PCIe rate when the blob is in
+ * page-locked memory, sbft_gv_host_alloc); scattered ones are gathered on the host first.
+ * Digests never leave the device unless dig_out is given.
+ * Replaces: per-request crypto/sha256 + crypto/ecdsa.Verify in an api.Verifier's
+ * VerifyRequest for requests of up to RequestMaxBytes (pkg/types/config.go:111) arriving
+ * through Controller.HandleRequest (internal/bft/controller.go:233-246). */
+int sbft_gv_sha256_verify_p256_stream(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len,
+                                      const uint64_t* off, const uint32_t* len, const uint8_t* r,
+                                      const uint8_t* s, const uint8_t* qx, const uint8_t* qy, size_t n,
+                                      size_t window_bytes, uint8_t* ok_out, uint8_t* dig_out);
+
 /* Bytes of device workspace the verify pipeline uses for a batch of n tuples (fixup list +
  * batched-inversion arrays, ~65 B per tuple). The device-resident entry points keep one such
  * workspace per caller stream inside the context. */

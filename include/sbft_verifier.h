@@ -96,6 +96,16 @@ int sbft_verifier_verify_request(sbft_verifier* v, const uint8_t* req, size_t le
 int sbft_verifier_verify_consenter_sig(sbft_verifier* v, const sbft_signature* s, const sbft_proposal* p,
                                        uint8_t* aux, size_t aux_cap, size_t* aux_len, char* err,
                                        size_t err_cap);
+/* Coalescing of concurrent VerifyConsenterSig calls, for the unmodified library: view.go
+ * verifies a decision's q-1 commit votes from q-1 goroutines at once (view.go:537-541 ->
+ * voteVerifier.verifyVote :834), each with a single call. With coalescing on (max_batch > 1),
+ * concurrent calls join one batch that launches when it holds max_batch calls or max_wait_us
+ * after its first call, so a quorum costs one or two launches instead of q-1 serialised ones.
+ * Every caller still gets exactly its own result (status, error text, aux). max_batch <= 1
+ * turns it off (the default). The calls may check different proposals. */
+int sbft_verifier_coalesce_consenter_sigs(sbft_verifier* v, size_t max_batch, uint32_t max_wait_us);
+/* VerifyConsenterSig launches and calls served so far (observability). */
+void sbft_verifier_consenter_stats(const sbft_verifier* v, uint64_t* launches, uint64_t* calls);
 /* Batching hook (new): n consenter signatures over one proposal in one GPU
  * launch. status[i] = 0 ok, else the per-signature error code; auxes are not returned (use
  * sbft_verifier_auxiliary_data on the accepted messages). Returns 0 if the call ran. */

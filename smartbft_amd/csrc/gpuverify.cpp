@@ -1008,7 +1008,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
 // ---------------------------------------------------------------- streamed hash + verify
 namespace {
 
-constexpr size_t kStreamWindowDefault = (size_t)256 << 20;  // payload bytes per window
+constexpr size_t kStreamWindowDefault = (size_t)64 << 20;   // payload bytes per window
 constexpr size_t kStreamWindowMsgs = 65536;                 // messages per window, at most
 constexpr unsigned kStageThreads = 4;                       // host threads gathering a window
 
@@ -1041,10 +1041,10 @@ struct StreamArgs {
 // One device's share [c.begin, c.begin + c.count), streamed in windows through the slot's two
 // stage buffers. Window w (stage b = w & 1):
 //   host    : wait for window w-2's outputs on stage b (out_done), hand them to the caller;
-//             gather window w's messages (compacted), rebased offsets, lengths and tuple
-//             fields into the pinned input of stage b (the messages themselves are DMA'd
-//             straight from the caller's blob when it is page-locked and the window's span is
-//             dense)
+//             write window w's rebased offsets, lengths and tuple fields into the pinned
+//             input of stage b; the messages are DMA'd straight from the caller's blob when
+//             the window's span is dense (from pageable memory the runtime stages the copy
+//             and this thread waits for it), else gathered into the stage first
 //   copy    : H2D of the stage -> device buffer b; record h2d_done
 //   compute : wait h2d_done; SHA-256 -> verify (digests stay on the device) -> D2H of the
 //             verdicts (+ digests) into the stage's pinned output; record out_done
@@ -1084,7 +1084,10 @@ int stream_chunk(sbft_gv_ctx* ctx, const Chunk& c, const StreamArgs& a) {
             bytes[w] += a.len[k];
         }
         const uint64_t span = hi[w] - lo[w];
-        direct[w] = a.blob_pinned && span <= bytes[w] + bytes[w] / 8 + 4096;
+        // dense: DMA'd in place (from pageable memory through the runtime's own staging,
+        // which runs at the PCIe rate; a host gather into our staging is the fallback for
+        // windows whose messages are scattered over the blob)
+        direct[w] = span <= bytes[w] + bytes[w] / 8 + 4096;
         m = std::max(m, cut[w + 1] - cut[w]);
         dev_blob = std::max<size_t>(dev_blob, direct[w] ? span : bytes[w]);
         if (!direct[w]) pin_blob = std::max<size_t>(pin_blob, bytes[w]);

@@ -480,6 +480,28 @@ struct sbft_verifier {
     } memo[4];
     int memo_next = 0;
 
+    // VerifyConsenterSig coalescer (sbft_verifier_coalesce_consenter_sigs). The library verifies
+    // a decision's q-1 commit votes from q-1 goroutines at once (view.go:537-541 -> :834), each
+    // with a single VerifyConsenterSig call; concurrent calls join one batch and share one
+    // launch. A batch closes when it holds cs_max calls or cs_wait after its first call.
+    struct CsEntry {
+        const sbft_signature* sig;
+        const sbft_proposal* p;
+        int32_t status = 0;
+        std::string why;
+    };
+    struct CsBatch {
+        std::vector<CsEntry*> entries;
+        bool closed = false, done = false;
+        int rc = 0;
+        std::condition_variable cv;
+    };
+    std::mutex cs_mu;
+    std::shared_ptr<CsBatch> cs_open;
+    size_t cs_max = 0;  // 0 = off: every call is its own launch
+    std::chrono::microseconds cs_wait{0};
+    std::atomic<uint64_t> cs_launches{0}, cs_calls{0};
+
     void digest_of(const sbft_proposal* p, char out[65]) {
         auto same = [](const std::vector<uint8_t>& v, const uint8_t* q, size_t n) {
             return v.size() == n && (n == 0 || std::memcmp(v.data(), q, n) == 0);
@@ -650,8 +672,15 @@ struct sbft_verifier {
     // reasons[i] gets the error text.
     int consenter_batch(const sbft_signature* sigs, size_t n, const sbft_proposal* p, int32_t* status,
                         std::vector<std::string>* reasons) {
+        std::vector<const sbft_proposal*> props(n, p);
+        return consenter_batch(sigs, n, props.data(), status, reasons);
+    }
+    // The same with a proposal per signature (the consenter-signature coalescer batches calls
+    // from concurrent callers, which may check different proposals): one launch for all.
+    int consenter_batch(const sbft_signature* sigs, size_t n, const sbft_proposal* const* props, int32_t* status,
+                        std::vector<std::string>* reasons) {
         char digest[65];
-        digest_of(p, digest);
+        const sbft_proposal* last = nullptr;
         std::vector<const uint8_t*> msgs, sv, kv, kmsgs, ksv;
         std::vector<size_t> lens, which, klens, kwhich;
         std::vector<uint32_t> kids;
@@ -660,6 +689,10 @@ struct sbft_verifier {
         for (size_t i = 0; i < n; ++i) {
             Msg m;
             status[i] = 0;
+            if (props[i] != last) {  // digest_of is memoised; consecutive equal proposals skip it
+                digest_of(props[i], digest);
+                last = props[i];
+            }
             if (!parse_msg(sigs[i].msg, sigs[i].msg_len, m)) {
                 status[i] = SBFT_V_EFORMAT;
                 if (reasons) (*reasons)[i] = "malformed signature message";
@@ -950,18 +983,107 @@ int sbft_verifier_verify_request(sbft_verifier* v, const uint8_t* req, size_t le
     return 0;
 }
 
+// One VerifyConsenterSig through the coalescer: join the open batch (or open one and lead
+// it), and return this call's own status and reason. The leader waits until the batch is full
+// or its deadline passes, closes it, runs ONE consenter_batch over every joined call (their
+// proposals may differ) and wakes the others. No background thread.
+static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const sbft_proposal* p, int32_t& st,
+                               std::string& why) {
+    using Batch = sbft_verifier::CsBatch;
+    sbft_verifier::CsEntry me{s, p};
+    std::shared_ptr<Batch> batch;
+    bool leader = false;
+    {
+        std::unique_lock<std::mutex> g(v->cs_mu);
+        if (!v->cs_open) {
+            v->cs_open = std::make_shared<Batch>();
+            leader = true;
+        }
+        batch = v->cs_open;
+        batch->entries.push_back(&me);
+        if (batch->entries.size() >= v->cs_max) {
+            batch->closed = true;
+            v->cs_open.reset();
+            batch->cv.notify_all();  // wakes the leader early
+        }
+        if (leader) {
+            batch->cv.wait_until(g, std::chrono::steady_clock::now() + v->cs_wait, [&] { return batch->closed; });
+            if (!batch->closed) {
+                batch->closed = true;
+                v->cs_open.reset();
+            }
+        } else {
+            batch->cv.wait(g, [&] { return batch->done; });
+        }
+    }
+    if (leader) {
+        // closed: nobody else touches the entries until done is published
+        const size_t n = batch->entries.size();
+        std::vector<sbft_signature> sigs(n);
+        std::vector<const sbft_proposal*> props(n);
+        for (size_t i = 0; i < n; ++i) {
+            sigs[i] = *batch->entries[i]->sig;
+            props[i] = batch->entries[i]->p;
+        }
+        std::vector<int32_t> sts(n);
+        std::vector<std::string> whys;
+        const int rc = v->consenter_batch(sigs.data(), n, props.data(), sts.data(), &whys);
+        v->cs_launches++;
+        v->cs_calls += n;
+        std::lock_guard<std::mutex> g(v->cs_mu);
+        for (size_t i = 0; i < n; ++i) {
+            batch->entries[i]->status = rc ? 0 : sts[i];
+            if (!rc) batch->entries[i]->why = std::move(whys[i]);
+        }
+        batch->rc = rc;
+        batch->done = true;
+        batch->cv.notify_all();
+    }
+    st = me.status;
+    why = std::move(me.why);
+    return batch->rc;
+}
+
+int sbft_verifier_coalesce_consenter_sigs(sbft_verifier* v, size_t max_batch, uint32_t max_wait_us) {
+    if (!v) return SBFT_GV_EINVAL;
+    std::lock_guard<std::mutex> g(v->cs_mu);
+    v->cs_max = max_batch;
+    v->cs_wait = std::chrono::microseconds(max_wait_us);
+    return 0;
+}
+
+void sbft_verifier_consenter_stats(const sbft_verifier* v, uint64_t* launches, uint64_t* calls) {
+    if (!v) return;
+    if (launches) *launches = v->cs_launches.load();
+    if (calls) *calls = v->cs_calls.load();
+}
+
 int sbft_verifier_verify_consenter_sig(sbft_verifier* v, const sbft_signature* s, const sbft_proposal* p,
                                        uint8_t* aux, size_t aux_cap, size_t* aux_len, char* err, size_t err_cap) {
     if (!v || !s || !p) return SBFT_GV_EINVAL;
     int32_t st = 0;
-    std::vector<std::string> why;
-    const int rc = v->consenter_batch(s, 1, p, &st, &why);
+    int rc;
+    std::string reason;
+    size_t coalesce;
+    {
+        std::lock_guard<std::mutex> g(v->cs_mu);
+        coalesce = v->cs_max;
+    }
+    if (coalesce > 1) {
+        rc = consenter_coalesced(v, s, p, st, reason);
+    } else {
+        std::vector<std::string> why;
+        rc = v->consenter_batch(s, 1, p, &st, &why);
+        v->cs_launches++;
+        v->cs_calls++;
+        if (!rc) reason = why[0];
+    }
     if (rc) {
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
         return rc;
     }
     if (st) {
-        put_err(err, err_cap, "%s", why[0].c_str());
+        put_err(err, err_cap, "%s", reason.c_str());
         return st;
     }
     Msg m;

@@ -23,7 +23,7 @@ EXPORTS = [
     "sbft_gv_register_key", "sbft_gv_verify_p256_keyed", "sbft_gv_sha256_verify_p256_keyed",
     "sbft_gv_kernel_timing", "sbft_gv_kernel_time", "sbft_gv_register_keys",
     "sbft_gv_sha256_verify_p256_framed", "sbft_gv_host_alloc", "sbft_gv_host_free",
-    "sbft_gv_plan_split",
+    "sbft_gv_plan_split", "sbft_gv_sha256_verify_p256_stream",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -93,6 +93,10 @@ def load_library():
     L.sbft_gv_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(_vp)]
     L.sbft_gv_host_free.argtypes = [_vp]
     L.sbft_gv_host_free.restype = None
+    L.sbft_gv_sha256_verify_p256_stream.argtypes = [_vp, _u8p, ctypes.c_size_t,
+                                                    ctypes.POINTER(ctypes.c_uint64),
+                                                    ctypes.POINTER(ctypes.c_uint32)] + [_u8p] * 4 + \
+                                                   [ctypes.c_size_t, ctypes.c_size_t, _u8p, _u8p]
     _szp = ctypes.POINTER(ctypes.c_size_t)
     L.sbft_gv_plan_split.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, _szp, _szp]
     L.sbft_gv_plan_split.restype = ctypes.c_size_t
@@ -330,6 +334,24 @@ class GpuVerifier:
             _p(dig) if dig is not None else None), "sbft_gv_sha256_verify_p256")
         return (ok, dig) if want_digests else ok
 
+    def sha256_verify_stream(self, blob, off, ln, r, s, qx, qy, window_bytes: int = 0, want_digests=False):
+        """Streamed hash + verify (sbft_gv_sha256_verify_p256_stream): windows of about
+        window_bytes of payload through double-buffered pinned staging, one host thread per
+        device. blob may be a PinnedArray's array (then dense windows are DMA'd in place)."""
+        if not (isinstance(blob, np.ndarray) and blob.dtype == np.uint8 and blob.flags.c_contiguous):
+            blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        blob = blob.reshape(-1)
+        _, off, ln, n = _msgs(blob[:0], off, ln)
+        arrs = [_soa(a, n) for a in (r, s, qx, qy)]
+        ok = np.zeros(n, dtype=np.uint8)
+        dig = np.zeros((n, 32), dtype=np.uint8) if want_digests else None
+        self._check(self.L.sbft_gv_sha256_verify_p256_stream(
+            self.ctx, _p(blob) if blob.size else None, blob.size,
+            off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+            ln.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), *[_p(a) for a in arrs], n, window_bytes,
+            _p(ok), _p(dig) if dig is not None else None), "sbft_gv_sha256_verify_p256_stream")
+        return (ok, dig) if want_digests else ok
+
     def sha256_verify_framed(self, blob, off, ln, sig_rel: int, pub_rel: int) -> np.ndarray:
         """Hash + verify of messages whose r || s and x || y sit in the blob at message end
         + sig_rel / + pub_rel (sbft_gv_sha256_verify_p256_framed)."""
@@ -356,6 +378,19 @@ class GpuVerifier:
                                              (d_qy, "qy"))]
         self._check(self.L.sbft_gv_verify_p256_dev(
             self.ctx, dev, *p, n, _dev(d_ok, n, "ok"), self._stream(stream)), "sbft_gv_verify_p256_dev")
+
+    def sha256_verify_dev(self, d_blob, d_off, d_len, d_r, d_s, d_qx, d_qy, d_ok, d_dig, stream=None):
+        """Device-resident hash + verify (sbft_gv_sha256_verify_p256_dev): digests of the
+        messages land in d_dig and feed the verify of the same tuples on the same stream."""
+        import torch
+        n = d_ok.numel()
+        if d_off.dtype not in (torch.int64, torch.uint64) or d_len.dtype not in (torch.int32, torch.uint32):
+            raise ValueError("offsets must be 64-bit and lengths 32-bit integers")
+        p = [_dev(t, 32 * n, w) for t, w in ((d_r, "r"), (d_s, "s"), (d_qx, "qx"), (d_qy, "qy"))]
+        self._check(self.L.sbft_gv_sha256_verify_p256_dev(
+            self.ctx, d_ok.device.index, d_blob.data_ptr(), _dev(d_off, n, "offsets", d_off.dtype),
+            _dev(d_len, n, "lengths", d_len.dtype), None, *p, n, _dev(d_ok, n, "ok"),
+            _dev(d_dig, 32 * n, "digests"), self._stream(stream)), "sbft_gv_sha256_verify_p256_dev")
 
     def kernel_timing(self, enable: bool):
         """Record HIP events around each device-resident verify's main kernel."""

@@ -128,6 +128,9 @@ def _lib():
                                                ctypes.c_char_p, ctypes.c_size_t]
     L.sbft_verifier_verify_consenter_sig.argtypes = [_vp, S, P, _u8p, ctypes.c_size_t, sz, ctypes.c_char_p,
                                                      ctypes.c_size_t]
+    L.sbft_verifier_coalesce_consenter_sigs.argtypes = [_vp, ctypes.c_size_t, ctypes.c_uint32]
+    L.sbft_verifier_consenter_stats.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    L.sbft_verifier_consenter_stats.restype = None
     L.sbft_verifier_verify_consenter_sigs.argtypes = [_vp, S, ctypes.c_size_t, P, ctypes.POINTER(ctypes.c_int32)]
     L.sbft_verifier_verify_signature.argtypes = [_vp, S, ctypes.c_char_p, ctypes.c_size_t]
     L.sbft_verifier_auxiliary_data.restype = ctypes.c_int64
@@ -282,6 +285,15 @@ class Verifier:
         if rc:
             raise VerifyError(rc, err.value.decode())
         return bytes(aux[:alen.value])
+
+    def coalesce_consenter_sigs(self, max_batch: int, max_wait_us: int):
+        """Concurrent VerifyConsenterSig calls share launches (max_batch <= 1: off)."""
+        assert self.L.sbft_verifier_coalesce_consenter_sigs(self.h, max_batch, max_wait_us) == 0
+
+    def consenter_stats(self) -> tuple[int, int]:
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self.L.sbft_verifier_consenter_stats(self.h, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
 
     def VerifyConsenterSigs(self, sigs: list[Signature], p: Proposal) -> list[int]:
         keep = []

@@ -155,3 +155,56 @@ def make_signed_requests(gv, n: int, start: int = 0, device: int = 0) -> list[by
         raise RuntimeError("signer rejected a synthetic request key")
     rh, sh = r.cpu().numpy(), s.cpu().numpy()
     return [bodies[i] + rh[i].tobytes() + sh[i].tobytes() for i in range(n)]
+
+
+class Config5:
+    """BASELINE config 5 on one device: n requests with payload lengths uniform in
+    [1 KiB, 64 KiB] (seeded), resident in HBM, each signed over SHA-256 of its payload under a
+    key of its own; ~10% corrupted after signing (by kind = i mod 3: an r bit, an s bit, one
+    payload byte)."""
+
+    def __init__(self, blob, off, ln, d_off, d_len, r, s, qx, qy, corrupted, total):
+        self.blob, self.off, self.ln, self.d_off, self.d_len = blob, off, ln, d_off, d_len
+        self.r, self.s, self.qx, self.qy, self.corrupted, self.total = r, s, qx, qy, corrupted, total
+
+    @property
+    def n(self) -> int:
+        return len(self.off)
+
+
+def make_config5(gv, n: int, device: int = 0, seed: int = 5) -> Config5:
+    dev = torch.device(f"cuda:{device}")
+    rng = np.random.default_rng(seed)
+    ln = rng.integers(1024, 65537, size=n).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(ln.astype(np.uint64))[:-1]]).astype(np.uint64)
+    total = int(ln.astype(np.uint64).sum())
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    blob = torch.randint(0, 256, (total + 256,), dtype=torch.uint8, device=dev, generator=g)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(ln.astype(np.int32)).to(dev)
+    dig = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    gv.sha256_dev(blob, d_off, d_len, dig)
+    d = _reduce_mod_n(_gpu_sha(gv, *_tag_messages(b"c5key", 0, n), dev))
+    k = _reduce_mod_n(_gpu_sha(gv, *_tag_messages(b"c5k", 0, n), dev))
+    qx, qy, r, s = (torch.empty((n, 32), dtype=torch.uint8, device=dev) for _ in range(4))
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    gv.sign_dev(d, k, dig, qx, qy, r, s, st)
+    torch.cuda.synchronize(dev)
+    if not bool((st == 1).all()):
+        raise RuntimeError("signer rejected a synthetic config-5 key")
+    del d, k, dig
+    c = _gpu_sha(gv, *_tag_messages(b"c5c", 0, n), dev)
+    corrupted = c[:, 0] < 26
+    idx = torch.nonzero(corrupted).flatten()
+    kind = idx % 3
+    byte = (c[idx, 1] % 32).long()
+    bit = (1 << (c[idx, 2] % 8).to(torch.int32)).to(torch.uint8)
+    for kk, t in ((0, r), (1, s)):
+        sel = idx[kind == kk]
+        t[sel, byte[kind == kk]] ^= bit[kind == kk]
+    sel = idx[kind == 2]
+    pos = d_off[sel] + (c[sel, 3].long() * 256 + c[sel, 4].long()) % d_len[sel].long()
+    blob[pos] ^= bit[kind == 2]
+    torch.cuda.synchronize(dev)
+    return Config5(blob, off, ln, d_off, d_len, r, s, qx, qy, corrupted, total)

@@ -211,3 +211,48 @@ def test_config5_large_batch_throughput_kernel(gpu):
     ok, got_dig = gpu.sha256_verify(blob, off, ln, *cols, want_digests=True)
     assert np.array_equal(got_dig, dig)
     assert np.array_equal(ok, want)
+
+
+# ---------------------------------------------------------------- config 5, streamed
+@pytest.fixture(scope="module")
+def config5_batch():
+    return _config5_batch(600, seed=58)
+
+
+@pytest.mark.parametrize("window", [0, 1 << 20, 300_000, 16_384])
+def test_config5_streamed_pageable(gpu, config5_batch, window):
+    """sbft_gv_sha256_verify_p256_stream from pageable memory: windows gathered on the host
+    into double-buffered pinned staging. Small windows force many windows, windows of one
+    message, and messages longer than the window (16 KiB < 64 KiB)."""
+    blob, off, ln, cols, dig, want = config5_batch
+    ok, got = gpu.sha256_verify_stream(blob, off, ln, *cols, window_bytes=window, want_digests=True)
+    assert np.array_equal(got, dig)
+    assert np.array_equal(ok, want)
+    assert np.array_equal(gpu.sha256_verify_stream(blob, off, ln, *cols, window_bytes=window), want)
+
+
+def test_config5_streamed_pinned_blob(gpu, config5_batch):
+    """A page-locked blob with dense windows is DMA'd in place; with the messages listed in a
+    permuted order the windows are sparse and gathered on the host instead. Same verdicts."""
+    from smartbft_amd import PinnedArray
+    blob, off, ln, cols, dig, want = config5_batch
+    pin = PinnedArray(blob.shape)
+    try:
+        pin.array[:] = blob
+        ok, got = gpu.sha256_verify_stream(pin.array, off, ln, *cols, window_bytes=2 << 20, want_digests=True)
+        assert np.array_equal(got, dig) and np.array_equal(ok, want)
+        perm = np.random.default_rng(1).permutation(len(off))
+        ok2 = gpu.sha256_verify_stream(pin.array, off[perm], ln[perm], *[c[perm] for c in cols],
+                                       window_bytes=2 << 20)
+        assert np.array_equal(ok2, want[perm])
+    finally:
+        pin.close()
+
+
+def test_config5_streamed_edges(gpu, config5_batch):
+    blob, off, ln, cols, dig, want = config5_batch
+    assert np.array_equal(gpu.sha256_verify_stream(blob, off[:1], ln[:1], *[c[:1] for c in cols]), want[:1])
+    z = np.zeros((0, 32), dtype=np.uint8)
+    assert gpu.sha256_verify_stream(blob, off[:0], ln[:0], z, z, z, z).shape == (0,)
+    with pytest.raises(Exception):  # a message past the blob's end is rejected, not read
+        gpu.sha256_verify_stream(blob[:100], off[:2], ln[:2], *[c[:2] for c in cols])

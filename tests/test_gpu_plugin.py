@@ -333,3 +333,54 @@ def test_verify_proposal_format_errors_and_concurrent_callers(net):
         t.join()
     assert not errors, errors
     assert len(results) == 4
+
+
+# ---- config 4 as the stock library drives it: concurrent single VerifyConsenterSig calls ----
+def test_consenter_sig_coalescer_concurrent_callers(gpu):
+    """view.go:537-541 spawns one goroutine per commit vote, each calling VerifyConsenterSig
+    (:834). With coalescing on, 66 concurrent single calls share few launches; every caller
+    still gets its own verdict, aux, and error text (view.go:840 logs "Couldn't verify %d's
+    signature: %v" with it)."""
+    import threading
+    q, f = plugin.compute_quorum(100)
+    nodes = [plugin.Signer(gpu, i, _priv(("co", i))) for i in range(1, q + 1)]
+    v = plugin.Verifier(gpu, 1)
+    for s in nodes:
+        v.add_consenter(s.id, s.public_key())
+    blocks = [plugin.Proposal(b"blk-%d" % k * 50, b"h", b"m", 1) for k in range(2)]
+    votes = [nodes[i].SignProposal(blocks[i % 2], b"aux-%d" % i) for i in range(1, q)]  # two proposals mixed
+    bad = 17
+    votes[bad] = plugin.Signature(votes[bad].ID, votes[bad - 2].Value, votes[bad].Msg)
+    v.coalesce_consenter_sigs(max_batch=q - 1, max_wait_us=20000)
+    l0, c0 = v.consenter_stats()
+    out = [None] * len(votes)
+    start = threading.Barrier(len(votes))
+
+    def call(i):
+        start.wait()
+        try:
+            out[i] = v.VerifyConsenterSig(votes[i], blocks[(i + 1) % 2])
+        except plugin.VerifyError as e:
+            out[i] = e
+
+    th = [threading.Thread(target=call, args=(i,)) for i in range(len(votes))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    for i, o in enumerate(out):
+        if i == bad:
+            assert isinstance(o, plugin.VerifyError) and o.code == plugin.EVERIFY
+            assert f"Couldn't verify {votes[i].ID}'s signature: {o}" == \
+                f"Couldn't verify {votes[i].ID}'s signature: invalid signature"
+        else:
+            assert o == b"aux-%d" % (i + 1), (i, o)
+    l1, c1 = v.consenter_stats()
+    assert c1 - c0 == len(votes) and l1 - l0 <= 8, (l1 - l0, c1 - c0)
+    # a lone call after its deadline, and coalescing off again: one launch per call
+    assert v.VerifyConsenterSig(votes[0], blocks[1]) == b"aux-1"
+    v.coalesce_consenter_sigs(0, 0)
+    with pytest.raises(plugin.VerifyError, match="does not bind"):
+        v.VerifyConsenterSig(votes[0], blocks[0])
+    assert v.consenter_stats() == (l1 + 2, c1 + 2)
+    v.close()

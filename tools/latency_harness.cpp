@@ -1,0 +1,286 @@
+// latency_harness.cpp — per-call latency of BASELINE configs 3 and 4 as the library drives them,
+// on the GPU path (through the C ABI of libsbft_gpuverify.so) and on a CPU baseline (OpenSSL
+// libcrypto ECDSA_do_verify; Go is absent on both machines, so OpenSSL's ecp_nistz256 assembly
+// is the stand-in for Go's crypto/ecdsa). Measurement tooling for bench.py, not product code.
+//
+//   quorum-gpu  CALLERS DECISIONS COALESCE_MAX COALESCE_WAIT_US
+//       view.go:537-541: one goroutine per commit vote, each calling VerifyConsenterSig
+//       (:834). CALLERS threads of a persistent pool are released at once per decision; each
+//       makes ONE sbft_verifier_verify_consenter_sig call on its own vote. Latency = release ->
+//       the last call returned. COALESCE_MAX <= 1 is the stock behaviour (a launch per call).
+//       Every 10th decision carries one bad signature (vote 7): its caller must get
+//       SBFT_V_EVERIFY with the reference's text, everyone else 0.
+//   quorum-cpu  CALLERS DECISIONS THREADS
+//       the same fan-out with the verify on the CPU: CALLERS votes verified by THREADS
+//       workers (one thread per vote when THREADS >= CALLERS), SHA-256(Msg) + ECDSA_do_verify
+//       each, keys pre-materialised.
+//   proposal-cpu REQUESTS DECISIONS THREADS
+//       VerifyProposal (view.go:555) on the CPU: REQUESTS signed requests (distinct keys,
+//       64-256 B bodies) verified by THREADS workers pulling indices from an atomic counter:
+//       SHA-256(body) + ECDSA_do_verify each, keys pre-materialised (favours the CPU: a real
+//       plugin also decodes each request's key).
+// Prints one JSON object.
+#include <openssl/bn.h>
+#include <openssl/ec.h>
+#include <openssl/ecdsa.h>
+#include <openssl/obj_mac.h>
+#include <openssl/sha.h>
+#include <pthread.h>
+#include <sched.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../include/sbft_verifier.h"
+
+using Clock = std::chrono::steady_clock;
+
+static double pct(std::vector<double> v, double p) {
+    std::sort(v.begin(), v.end());
+    if (v.empty()) return 0;
+    size_t i = (size_t)(p / 100.0 * (v.size() - 1) + 0.5);
+    return v[std::min(i, v.size() - 1)];
+}
+
+// A pool of `n` threads released together once per round; run(i) is thread i's work.
+// Returns per-round wall times (release -> last thread done), microseconds.
+static std::vector<double> fan_out(size_t n, int rounds, const std::function<void(size_t, int)>& run) {
+    std::mutex mu;
+    std::condition_variable cv_go, cv_done;
+    int gen = -1;
+    size_t remaining = 0;
+    bool stop = false;
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < n; ++i)
+        th.emplace_back([&, i] {
+            int seen = -1;
+            for (;;) {
+                int g;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv_go.wait(lk, [&] { return stop || gen != seen; });
+                    if (stop) return;
+                    g = seen = gen;
+                }
+                run(i, g);
+                std::lock_guard<std::mutex> lk(mu);
+                if (--remaining == 0) cv_done.notify_one();
+            }
+        });
+    std::vector<double> out;
+    for (int r = 0; r < rounds; ++r) {
+        Clock::time_point t0;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            remaining = n;
+            t0 = Clock::now();
+            gen = r;
+            cv_go.notify_all();
+            cv_done.wait(lk, [&] { return remaining == 0; });
+        }
+        out.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = true;
+    }
+    cv_go.notify_all();
+    for (auto& t : th) t.join();
+    return out;
+}
+
+static void priv_of(uint64_t tag, uint8_t out[32]) {
+    // deterministic private keys in [1, n-1]: SHA-256(tag) with the top bit cleared
+    uint8_t in[16] = "sbft-harness";
+    std::memcpy(in + 8, &tag, 8);
+    SHA256_CTX c;
+    SHA256_Init(&c);
+    SHA256_Update(&c, in, sizeof in);
+    SHA256_Final(out, &c);
+    out[0] &= 0x7f;
+    out[31] |= 1;
+}
+
+static int quorum_gpu(int callers, int decisions, int cmax, int cwait) {
+    sbft_gv_ctx* ctx = nullptr;
+    if (sbft_gv_init(nullptr, &ctx)) {
+        std::fprintf(stderr, "no GPU\n");
+        return 1;
+    }
+    sbft_verifier* v = sbft_verifier_new(ctx, 1);
+    const int voters = callers + 1;  // the node's own signature is not verified (view.go:851-858)
+    std::vector<sbft_signer*> signers;
+    for (int i = 1; i <= voters; ++i) {
+        uint8_t d[32], pub[65];
+        priv_of(1000 + i, d);
+        signers.push_back(sbft_signer_new(ctx, i, d));
+        sbft_signer_public_key(signers.back(), pub);
+        sbft_verifier_add_consenter(v, i, pub);
+    }
+    // 8 blocks in rotation: every decision checks a proposal the digest memo does not hold
+    const int NB = 8;
+    std::vector<std::string> payloads(NB);
+    std::vector<sbft_proposal> props(NB);
+    std::vector<std::vector<std::vector<uint8_t>>> msgs(NB), vals(NB);
+    for (int b = 0; b < NB; ++b) {
+        payloads[b] = std::string(1300, 'a' + b);
+        props[b] = sbft_proposal{(const uint8_t*)payloads[b].data(), payloads[b].size(), (const uint8_t*)"h", 1,
+                                 (const uint8_t*)"m", 1, 1};
+        for (int i = 0; i < callers; ++i) {
+            std::vector<uint8_t> m(256), sig(64);
+            size_t ml = 0;
+            sbft_signer_sign_proposal(signers[i + 1], &props[b], nullptr, 0, m.data(), m.size(), &ml, sig.data());
+            m.resize(ml);
+            msgs[b].push_back(m);
+            vals[b].push_back(sig);
+        }
+    }
+    if (cmax > 1) sbft_verifier_coalesce_consenter_sigs(v, cmax, cwait);
+    std::atomic<int> wrong{0};
+    auto run = [&](size_t i, int g) {
+        const int b = g % NB;
+        std::vector<uint8_t> val = vals[b][i];
+        const bool bad = g % 10 == 9 && i == 7;
+        if (bad) val[40] ^= 1;
+        sbft_signature s{(uint64_t)(i + 2), val.data(), val.size(), msgs[b][i].data(), msgs[b][i].size()};
+        uint8_t aux[64];
+        size_t alen = 0;
+        char err[256] = {0};
+        const int rc = sbft_verifier_verify_consenter_sig(v, &s, &props[b], aux, sizeof aux, &alen, err, sizeof err);
+        if (bad ? (rc != SBFT_V_EVERIFY || !std::strstr(err, "invalid signature")) : rc != 0) wrong++;
+    };
+    fan_out(callers, 5, run);  // warm-up: tables, staging, memo
+    uint64_t l0, c0, l1, c1;
+    sbft_verifier_consenter_stats(v, &l0, &c0);
+    auto t = fan_out(callers, decisions, run);
+    sbft_verifier_consenter_stats(v, &l1, &c1);
+    std::printf("{\"mode\": \"quorum-gpu\", \"callers\": %d, \"decisions\": %d, \"coalesce_max\": %d, "
+                "\"coalesce_wait_us\": %d, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"launches_per_decision\": %.2f, "
+                "\"wrong_verdicts\": %d}\n",
+                callers, decisions, cmax, cwait, pct(t, 50) / 1e3, pct(t, 99) / 1e3,
+                (double)(l1 - l0) / decisions, wrong.load());
+    for (auto* s : signers) sbft_signer_free(s);
+    sbft_verifier_free(v);
+    sbft_gv_destroy(ctx);
+    return wrong.load() ? 2 : 0;
+}
+
+// SHA-256 through the low-level interface: OpenSSL 3's one-shot SHA256() fetches the digest
+// from the library context on every call, which serialises threads on its lock
+static void sha256_ll(const uint8_t* m, size_t n, uint8_t h[32]) {
+    SHA256_CTX c;
+    SHA256_Init(&c);
+    SHA256_Update(&c, m, n);
+    SHA256_Final(h, &c);
+}
+
+struct CpuTuple {
+    std::vector<uint8_t> msg;
+    EC_KEY* key;
+    ECDSA_SIG* sig;
+};
+
+static std::vector<CpuTuple> cpu_tuples(int n, int min_len, int max_len) {
+    std::vector<CpuTuple> out(n);
+    EC_GROUP* grp = EC_GROUP_new_by_curve_name(NID_X9_62_prime256v1);
+    uint32_t x = 12345;
+    for (int i = 0; i < n; ++i) {
+        x = x * 1103515245u + 12345u;
+        const int len = min_len + (int)(x % (uint32_t)(max_len - min_len + 1));
+        out[i].msg.resize(len);
+        for (int j = 0; j < len; ++j) out[i].msg[j] = (uint8_t)(i * 31 + j * 7);
+        EC_KEY* k = EC_KEY_new();
+        EC_KEY_set_group(k, grp);
+        EC_KEY_generate_key(k);
+        uint8_t h[32];
+        sha256_ll(out[i].msg.data(), len, h);
+        {
+            // r, s re-imported as plain BIGNUMs (a signer's BIGNUMs carry flags such as
+            // constant-time that would slow the verify down)
+            ECDSA_SIG* sg = ECDSA_do_sign(h, 32, k);
+            uint8_t rb[32], sb[32];
+            BN_bn2binpad(ECDSA_SIG_get0_r(sg), rb, 32);
+            BN_bn2binpad(ECDSA_SIG_get0_s(sg), sb, 32);
+            ECDSA_SIG_free(sg);
+            out[i].sig = ECDSA_SIG_new();
+            ECDSA_SIG_set0(out[i].sig, BN_bin2bn(rb, 32, nullptr), BN_bin2bn(sb, 32, nullptr));
+        }
+        // the verifier's key is decoded from its SEC1 bytes (affine, public only), as a
+        // plugin holds it; a generated key object carries a projective point that every
+        // verify would convert again
+        uint8_t oct[65];
+        EC_POINT_point2oct(grp, EC_KEY_get0_public_key(k), POINT_CONVERSION_UNCOMPRESSED, oct, 65, nullptr);
+        EC_KEY* pk = EC_KEY_new();
+        EC_KEY_set_group(pk, grp);
+        EC_KEY_oct2key(pk, oct, 65, nullptr);
+        EC_KEY_free(k);
+        out[i].key = pk;
+    }
+    EC_GROUP_free(grp);
+    return out;
+}
+
+static bool cpu_verify(const CpuTuple& t) {
+    uint8_t h[32];
+    sha256_ll(t.msg.data(), t.msg.size(), h);
+    return ECDSA_do_verify(h, 32, t.sig, t.key) == 1;
+}
+
+static int quorum_cpu(int callers, int decisions, int threads) {
+    auto tup = cpu_tuples(callers, 128, 128);
+    std::atomic<int> bad{0};
+    const int nt = std::max(1, std::min(threads, callers));
+    auto t = fan_out(nt, decisions, [&](size_t i, int) {
+        for (int k = (int)i; k < callers; k += nt)
+            if (!cpu_verify(tup[k])) bad++;
+    });
+    std::printf("{\"mode\": \"quorum-cpu\", \"callers\": %d, \"decisions\": %d, \"threads\": %d, \"p50_ms\": %.4f, "
+                "\"p99_ms\": %.4f, \"rejected\": %d}\n",
+                callers, decisions, nt, pct(t, 50) / 1e3, pct(t, 99) / 1e3, bad.load());
+    return 0;
+}
+
+static int proposal_cpu(int requests, int decisions, int threads) {
+    auto tup = cpu_tuples(requests, 64 + 150, 256 + 150);  // body = ids + payload + key
+    std::atomic<int> bad{0};
+    const int nt = std::max(1, threads);
+    // one pool; per decision the workers pull request indices from that decision's counter
+    std::unique_ptr<std::atomic<int>[]> next(new std::atomic<int>[decisions]);
+    for (int g = 0; g < decisions; ++g) next[g] = 0;
+    auto t = fan_out(nt, decisions, [&](size_t, int g) {
+        for (;;) {
+            const int k = next[g].fetch_add(1);
+            if (k >= requests) break;
+            if (!cpu_verify(tup[k])) bad++;
+        }
+    });
+    std::printf("{\"mode\": \"proposal-cpu\", \"requests\": %d, \"decisions\": %d, \"threads\": %d, "
+                "\"p50_ms\": %.4f, \"p99_ms\": %.4f, \"rejected\": %d}\n",
+                requests, decisions, nt, pct(t, 50) / 1e3, pct(t, 99) / 1e3, bad.load());
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-cpu|proposal-cpu ...\n", argv[0]);
+        return 1;
+    }
+    const std::string mode = argv[1];
+    auto arg = [&](int i, int def) { return argc > i ? std::atoi(argv[i]) : def; };
+    if (mode == "quorum-gpu") return quorum_gpu(arg(2, 66), arg(3, 200), arg(4, 0), arg(5, 0));
+    if (mode == "quorum-cpu") return quorum_cpu(arg(2, 66), arg(3, 200), arg(4, 66));
+    if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
+    std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
+    return 1;
+}
