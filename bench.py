@@ -373,8 +373,8 @@ def sha_config5(gv, dev, n_msgs: int, e2e_msgs: int = 65536):
                          "pinned": {"value": round(e2e_bytes / e2e_p / 1e9, 1), "unit": "GB/s",
                                     "mismatches": int((ok_p != want_k).sum())},
                          "messages": k, "bytes": e2e_bytes,
-                         "path": "sbft_gv_sha256_verify_p256_stream: 64 MiB windows, double-buffered "
-                                 "staging (H2D of window w+1 || SHA -> verify of window w), PCIe included"}}
+                         "path": "sbft_gv_sha256_verify_p256_stream: 256 MiB windows, 6 in flight per device "
+                                 "(H2D of one window || SHA -> verify of earlier ones), PCIe included"}}
 
 
 def main():

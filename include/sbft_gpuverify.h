@@ -60,6 +60,10 @@ typedef struct sbft_gv_opts {
 } sbft_gv_opts;
 
 #define SBFT_GV_PAIR_MAX_DEFAULT 32768u
+/* The device-resident hash entry points (sbft_gv_sha256_dev, sbft_gv_sha256_verify_p256_dev)
+ * read up to this many bytes past the end of a message (the hash kernel moves whole 16-B
+ * pieces of whole steps into LDS): the blob must stay readable that far past its last message. */
+#define SBFT_GV_SHA_BLOB_PAD 256u
 #define SBFT_GV_QUAD_MAX_DEFAULT 0u
 
 /* Create a context (per-device stream + device/pinned staging grown on demand).
@@ -118,8 +122,10 @@ int sbft_gv_sha256_verify_p256_framed(sbft_gv_ctx* ctx, const uint8_t* blob, siz
  * with 1-64 KiB payloads, hashed on the GPU, then verified). Same inputs and outputs as
  * sbft_gv_sha256_verify_p256 (dig_out may be NULL). Each device takes a contiguous share of the
  * messages (sbft_gv_plan_split) on a host thread of its own and streams it in windows of about
- * window_bytes of payload (0 = 64 MiB) through two staging buffers: while the device hashes
- * and verifies window w, the host thread stages and copies window w+1. Windows whose messages
+ * window_bytes of payload (0 = 256 MiB) through six staging buffers: up to six windows hash
+ * and verify concurrently (each on a stream of its own: hashing is serial within a message, so
+ * one window alone leaves most CUs idle) while the host thread stages and copies the next.
+ * Windows whose messages
  * lie densely in the blob are DMA'd in place (at the full PCIe rate when the blob is in
  * page-locked memory, sbft_gv_host_alloc); scattered ones are gathered on the host first.
  * Digests never leave the device unless dig_out is given.

@@ -13,6 +13,8 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -212,9 +214,16 @@ struct Slot {
         uint8_t* pin_out = nullptr;
         size_t out_cap = 0;
         hipEvent_t h2d_done = nullptr, out_done = nullptr;
-    } stage[2];
-    int reserve_stage(int b, size_t dev_bytes, size_t in_bytes, size_t out_bytes) {
+        hipStream_t cs = nullptr;  // the stage's compute stream
+    };
+    std::vector<StreamStage> stage;
+    int reserve_stage(size_t b, size_t dev_bytes, size_t in_bytes, size_t out_bytes) {
+        if (stage.size() <= b) stage.resize(b + 1);
         StreamStage& st = stage[b];
+        if (!st.cs && hipStreamCreateWithFlags(&st.cs, hipStreamNonBlocking) != hipSuccess) {
+            st.cs = nullptr;
+            return SBFT_GV_EDEVICE;
+        }
         if (!st.h2d_done && hipEventCreateWithFlags(&st.h2d_done, hipEventDisableTiming) != hipSuccess) {
             st.h2d_done = nullptr;
             return SBFT_GV_EDEVICE;
@@ -244,13 +253,18 @@ struct Slot {
     }
     void free_stage() {
         for (StreamStage& st : stage) {
+            if (st.cs) (void)hipStreamSynchronize(st.cs);
             if (st.dev) (void)hipFree(st.dev);
             if (st.pin_in) (void)hipHostFree(st.pin_in);
             if (st.pin_out) (void)hipHostFree(st.pin_out);
             if (st.h2d_done) (void)hipEventDestroy(st.h2d_done);
             if (st.out_done) (void)hipEventDestroy(st.out_done);
-            st = StreamStage();
+            if (st.cs) {
+                (void)hipStreamSynchronize(st.cs);
+                (void)hipStreamDestroy(st.cs);
+            }
         }
+        stage.clear();
     }
 
     int reserve(size_t bytes) {
@@ -750,7 +764,7 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
     rebased.resize(c.count);
     for (size_t k = 0; k < c.count; ++k) rebased[k] = off[c.begin + k] - lo;
     const size_t span = hi - lo;
-    const size_t fb = align_up(span + 128, 256);  // funnel over-read padding
+    const size_t fb = align_up(span + SBFT_GV_SHA_BLOB_PAD, 256);  // the hash kernel's over-read
     const size_t fo = align_up(8 * c.count, 256), fl = align_up(4 * c.count, 256);
     const size_t fd = align_up(32 * c.count, 256);
     const bool verify = ok_out != nullptr;
@@ -951,7 +965,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     Slot* sl = ctx->slots[ctx->rr.fetch_add(1) % ctx->slots.size()];
     std::unique_lock<std::mutex> lk(sl->mu);
     HIPCHK(hipSetDevice(sl->device));
-    int rc = sl->reserve_blob(blob_len + 256);  // + the hash kernel's funnel over-read
+    int rc = sl->reserve_blob(blob_len + SBFT_GV_SHA_BLOB_PAD);  // + the hash kernel's over-read
     if (rc) return rc;
     // the parse runs on the helper while this thread stages the payload for the DMA
     int prc = 0;
@@ -1008,7 +1022,11 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
 // ---------------------------------------------------------------- streamed hash + verify
 namespace {
 
-constexpr size_t kStreamWindowDefault = (size_t)64 << 20;   // payload bytes per window
+constexpr size_t kStreamWindowDefault = (size_t)256 << 20;  // payload bytes per window
+// windows in flight per device. Hashing is serial within a message (a 64 KiB message is 1,024
+// dependent compressions), so one window of a few hundred long messages occupies a few CUs for
+// milliseconds: several windows run concurrently, each on its stage's compute stream.
+constexpr size_t kStreamStages = 6;
 constexpr size_t kStreamWindowMsgs = 65536;                 // messages per window, at most
 constexpr unsigned kStageThreads = 4;                       // host threads gathering a window
 
@@ -1038,17 +1056,18 @@ struct StreamArgs {
     bool blob_pinned;
 };
 
-// One device's share [c.begin, c.begin + c.count), streamed in windows through the slot's two
-// stage buffers. Window w (stage b = w & 1):
-//   host    : wait for window w-2's outputs on stage b (out_done), hand them to the caller;
+// One device's share [c.begin, c.begin + c.count), streamed in windows through the slot's K
+// stage buffers (kStreamStages). Window w (stage b = w mod K):
+//   host    : wait for window w-K's outputs on stage b (out_done), hand them to the caller;
 //             write window w's rebased offsets, lengths and tuple fields into the pinned
 //             input of stage b; the messages are DMA'd straight from the caller's blob when
 //             the window's span is dense (from pageable memory the runtime stages the copy
 //             and this thread waits for it), else gathered into the stage first
 //   copy    : H2D of the stage -> device buffer b; record h2d_done
-//   compute : wait h2d_done; SHA-256 -> verify (digests stay on the device) -> D2H of the
-//             verdicts (+ digests) into the stage's pinned output; record out_done
-// so the host gathers window w+1 while the device copies and computes window w.
+//   compute : on the stage's own stream: wait h2d_done; SHA-256 -> verify (digests stay on
+//             the device) -> D2H of the verdicts (+ digests) into the stage's pinned output;
+//             record out_done
+// so up to K windows hash and verify concurrently while the copy stream moves the next.
 int stream_chunk(sbft_gv_ctx* ctx, const Chunk& c, const StreamArgs& a) {
     Slot* sl = c.slot;
     HIPCHK(hipSetDevice(sl->device));
@@ -1097,25 +1116,37 @@ int stream_chunk(sbft_gv_ctx* ctx, const Chunk& c, const StreamArgs& a) {
     //   device    : blob (fb)             | off | len | r | s | qx | qy | hash counter (256) |
     //               digests (32 m) | ok (m) | verify workspace
     //   pinned out: ok (m) | digests (32 m)
-    // The hash kernel reads up to 128 B past a message: the device blob region has 256 spare.
-    const size_t fb = align_up(dev_blob + 256, 256), pb = pin_blob ? align_up(pin_blob, 256) : 0;
+    // The hash kernel reads up to SBFT_GV_SHA_BLOB_PAD B past a message: the device blob region has that spare.
+    const size_t fb = align_up(dev_blob + SBFT_GV_SHA_BLOB_PAD, 256), pb = pin_blob ? align_up(pin_blob, 256) : 0;
     const size_t fo = align_up(8 * m, 256), fl = align_up(4 * m, 256), fd = align_up(32 * m, 256),
                  fk = align_up(m, 256);
     const size_t meta = fo + fl + 4 * fd;
     const size_t dev_bytes = fb + meta + 256 + fd + fk + align_up(sbft_verify_work_bytes(m), 256);
-    for (int b = 0; b < 2; ++b)
+    const size_t K = std::min(kStreamStages, W);
+    for (size_t b = 0; b < K; ++b)
         if ((rc = sl->reserve_stage(b, dev_bytes, pb + meta, fk + fd))) return rc;
-    auto collect = [&](size_t w) -> int {  // outputs of window w (stage w & 1) -> caller
-        Slot::StreamStage& st = sl->stage[w & 1];
-        HIPCHK(hipEventSynchronize(st.out_done));
+    auto collect = [&](size_t w) -> int {  // outputs of window w (stage w % K) -> caller
+        Slot::StreamStage& st = sl->stage[w % K];
+        // poll: a blocking event wait can sleep past the event by a scheduler tick or more,
+        // once per window
+        hipError_t q;
+        while ((q = hipEventQuery(st.out_done)) == hipErrorNotReady) std::this_thread::yield();
+        if (q != hipSuccess) return SBFT_GV_EDEVICE;
         const size_t b = cut[w], mw = cut[w + 1] - b;
         std::memcpy(a.ok_out + b, st.pin_out, mw);
         if (a.dig_out) std::memcpy(a.dig_out + 32 * b, st.pin_out + fk, 32 * mw);
         return SBFT_GV_OK;
     };
+    static const bool trace = getenv("SBFT_STREAM_TRACE") != nullptr;  // diagnostics
+    const auto t_start = std::chrono::steady_clock::now();
+    auto us = [&] {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_start).count();
+    };
     for (size_t w = 0; w < W; ++w) {
-        Slot::StreamStage& st = sl->stage[w & 1];
-        if (w >= 2 && (rc = collect(w - 2))) return rc;
+        Slot::StreamStage& st = sl->stage[w % K];
+        const double t0 = trace ? us() : 0;
+        if (w >= K && (rc = collect(w - K))) return rc;
+        const double t1 = trace ? us() : 0;
         const size_t b = cut[w], mw = cut[w + 1] - b;
         uint8_t* in = st.pin_in;
         uint64_t* off_h = (uint64_t*)(in + pb);
@@ -1144,22 +1175,25 @@ int stream_chunk(sbft_gv_ctx* ctx, const Chunk& c, const StreamArgs& a) {
             HIPCHK(hipMemcpyAsync(d, in, bytes[w], hipMemcpyHostToDevice, sl->copy_stream));
         HIPCHK(hipMemcpyAsync(d + fb, in + pb, meta, hipMemcpyHostToDevice, sl->copy_stream));
         HIPCHK(hipEventRecord(st.h2d_done, sl->copy_stream));
-        HIPCHK(hipStreamWaitEvent(sl->stream, st.h2d_done, 0));
+        HIPCHK(hipStreamWaitEvent(st.cs, st.h2d_done, 0));
         uint8_t* d_tup = d + fb + fo + fl;
         uint8_t* d_ctr = d + fb + meta;
         uint8_t* d_dig = d_ctr + 256;
         uint8_t* d_ok = d_dig + fd;
         uint32_t* work = (uint32_t*)(d_ok + fk);
         if (sbft_launch_sha256(d, (const uint64_t*)(d + fb), (const uint32_t*)(d + fb + fo), nullptr, d_dig,
-                               (uint32_t)mw, (uint32_t*)d_ctr, sl->stream) ||
+                               (uint32_t)mw, (uint32_t*)d_ctr, st.cs) ||
             sbft_launch_p256_verify(d_dig, d_tup, d_tup + fd, d_tup + 2 * fd, d_tup + 3 * fd, d_ok, (uint32_t)mw,
-                                    work, gcomb, sl->stream, nullptr, nullptr, ctx->lanes_for(mw)))
+                                    work, gcomb, st.cs, nullptr, nullptr, ctx->lanes_for(mw)))
             return SBFT_GV_ELAUNCH;
-        HIPCHK(hipMemcpyAsync(st.pin_out, d_ok, mw, hipMemcpyDeviceToHost, sl->stream));
-        if (a.dig_out) HIPCHK(hipMemcpyAsync(st.pin_out + fk, d_dig, 32 * mw, hipMemcpyDeviceToHost, sl->stream));
-        HIPCHK(hipEventRecord(st.out_done, sl->stream));
+        HIPCHK(hipMemcpyAsync(st.pin_out, d_ok, mw, hipMemcpyDeviceToHost, st.cs));
+        if (a.dig_out) HIPCHK(hipMemcpyAsync(st.pin_out + fk, d_dig, 32 * mw, hipMemcpyDeviceToHost, st.cs));
+        HIPCHK(hipEventRecord(st.out_done, st.cs));
+        if (trace)
+            fprintf(stderr, "stream dev %d window %zu: msgs %zu bytes %llu direct %d | collect %.0f us, stage+enqueue %.0f us\n",
+                    sl->device, w, mw, (unsigned long long)bytes[w], (int)direct[w], t1 - t0, us() - t1);
     }
-    for (size_t w = W >= 2 ? W - 2 : 0; w < W; ++w)
+    for (size_t w = W >= K ? W - K : 0; w < W; ++w)
         if ((rc = collect(w))) return rc;
     return SBFT_GV_OK;
 }
@@ -1179,8 +1213,10 @@ extern "C" int sbft_gv_sha256_verify_p256_stream(sbft_gv_ctx* ctx, const uint8_t
     // a message longer than the window gets a window of its own
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
         const int rc = stream_chunk(ctx, c, a);
-        if (rc) {  // drain the copy stream too (run_chunks waits on the main stream only)
+        if (rc) {  // drain the copy and stage streams too (run_chunks waits on the main stream only)
             (void)hipStreamSynchronize(c.slot->copy_stream);
+            for (auto& st : c.slot->stage)
+                if (st.cs) (void)hipStreamSynchronize(st.cs);
         }
         return rc;
     });

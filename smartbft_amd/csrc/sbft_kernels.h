@@ -30,8 +30,8 @@ int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const u
                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int lanes = 1);
 size_t sbft_gcomb_table_bytes(void);
 int sbft_launch_gcomb_build(void* d_table, hipStream_t stream);
-// SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable >= 68 bytes
-// past its last message (funnel over-read). Digests are 32-byte big-endian. d_order (may be
+// SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable
+// SBFT_GV_SHA_BLOB_PAD (256) bytes past its last message (whole-step LDS-DMA over-read). Digests are 32-byte big-endian. d_order (may be
 // NULL): the messages are taken in the order d_order[0], d_order[1], ... (load-balanced;
 // NULL = index order, which keeps each wavefront's streams adjacent in memory). d_ctr: one
 // device u32 of scratch private to the stream (zeroed by the launch).

@@ -35,7 +35,7 @@ def _tag_messages(tag: bytes, start: int, n: int) -> tuple[np.ndarray, np.ndarra
 
 
 def _gpu_sha(gv, blob: np.ndarray, off: np.ndarray, ln: np.ndarray, dev) -> torch.Tensor:
-    pad = np.zeros(blob.size + 128, dtype=np.uint8)
+    pad = np.zeros(blob.size + 256, dtype=np.uint8)  # SBFT_GV_SHA_BLOB_PAD
     pad[:blob.size] = blob
     d_blob = torch.from_numpy(pad).to(dev)
     d_off = torch.from_numpy(off.astype(np.int64)).to(dev)

@@ -140,7 +140,7 @@ def test_sha256_dev_explicit_order(gpu):
     n = 1500
     lens = rng.integers(0, 5000, size=n).astype(np.uint32)
     off = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
-    blob = rng.integers(0, 256, size=int(lens.sum()) + 128, dtype=np.uint8)
+    blob = rng.integers(0, 256, size=int(lens.sum()) + 256, dtype=np.uint8)  # SBFT_GV_SHA_BLOB_PAD
     exp = oracle.sha256_batch(blob, off, lens)
     dev = torch.device("cuda:0")
     d_blob = torch.from_numpy(blob).to(dev)
