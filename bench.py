@@ -377,6 +377,39 @@ def sha_config5(gv, dev, n_msgs: int, e2e_msgs: int = 65536):
                                  "(H2D of one window || SHA -> verify of earlier ones), PCIe included"}}
 
 
+def adversarial(gv, dev):
+    """Worst case a client can force: every tuple of a batch exceptional inside the lean Shamir
+    ladder (crafted R = infinity, P + P / P + (-P) additions; the request format lets the client
+    choose Q), so the whole batch is re-verified by the case-split fix-up kernel. Tiled from
+    the golden categories r_infinity and shamir_exceptional (tests/golden, data only); verdicts
+    checked against the fixtures. A bad proposal triggers complain + sync in the library
+    (view.go:386-393), so the cost of rejecting one matters."""
+    import json as _json
+    raw = np.fromfile(os.path.join(ROOT, "tests", "golden", "p256_vectors.bin"), dtype=np.uint8).reshape(-1, 162)
+    cats = _json.load(open(os.path.join(ROOT, "tests", "golden", "p256_categories.json")))["categories"]
+    sel = np.isin(raw[:, 161], [cats.index("r_infinity"), cats.index("shamir_exceptional")])
+    base = raw[sel]
+    out = {"base_vectors": int(len(base)), "base_accepts": int(base[:, 160].sum())}
+    stream = torch.cuda.current_stream(dev)
+    for n in (10_000, 1_000_000):
+        t = np.resize(base, (n, 162))
+        f = [torch.from_numpy(np.ascontiguousarray(t[:, 32 * k:32 * k + 32])).to(dev) for k in range(5)]
+        ok = torch.empty(n, dtype=torch.uint8, device=dev)
+        run = lambda: gv.verify_dev(*f, ok, stream)
+        run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 3
+        e0.record(stream)
+        for _ in range(reps):
+            run()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        out[f"all_exceptional_{n}"] = {"ms": round(ms, 3), "verifies_per_s": round(n / ms * 1e3, 1),
+                                       "mismatches": int((ok.cpu().numpy() != t[:, 160]).sum())}
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -529,6 +562,7 @@ def main():
         if n_gpus == 1 and not args.no_sha:
             rec["sha256_config5"] = sha_config5(gv, dev, args.sha_messages)
         if n_gpus == 1 and not args.no_latency:
+            rec["adversarial"] = adversarial(gv, dev)
             lat = latency_configs(gv, args.latency_calls)
             if not args.no_cpu_baseline:
                 # measured CPU latencies of the same calls (tools/latency_harness, OpenSSL):

@@ -206,9 +206,10 @@ __global__ __launch_bounds__(256) void p256_verify_fixup_kernel(const uint8_t* _
                                                                 uint8_t* __restrict__ ok,
                                                                 const uint32_t* __restrict__ work) {
     __shared__ u32 gtab[2 * 8 * P256_GTAB4_ENTRIES];
+    const uint32_t count = work[0];
+    if (blockIdx.x * blockDim.x >= count) return;  // block-uniform: the grid is sized for the worst case
     for (int i = threadIdx.x; i < 2 * 8 * P256_GTAB4_ENTRIES; i += blockDim.x) gtab[i] = C_GTAB[i];
     __syncthreads();
-    const uint32_t count = work[0];
     const uint32_t* list = work + 1;
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
         const uint32_t idx = list[j];
@@ -1144,7 +1145,18 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
     }
     if (ev1 && hipEventRecord(ev1, stream) != hipSuccess) return -1;
     SBFT_STEP("verify");
-    const unsigned fix_blocks = blocks < 64 ? blocks : 64;
+    // The flagged count is known only on the device: size the grid for the worst case (every
+    // tuple exceptional, e.g. a batch of crafted R = infinity signatures), capped at one
+    // resident round of the chip; blocks past the count exit at once.
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    const unsigned fix_cap = 8u * (unsigned)cus;
+    const unsigned fix_blocks = blocks < fix_cap ? blocks : fix_cap;
     hipLaunchKernelGGL(sbft::p256_verify_fixup_kernel, dim3(fix_blocks), dim3(threads), 0, stream,
                        d_digest, d_r, d_s, d_qx, d_qy, d_ok, (const uint32_t*)d_work);
     SBFT_STEP("fixup");

@@ -117,11 +117,12 @@ __global__ __launch_bounds__(256) void sha256_stream_kernel(const uint8_t* __res
 //
 // The DMA reads up to 16 P + 64 bytes past a message's end (it fetches whole steps; the
 // padding blocks are built in registers): callers pad the blob by SBFT_SHA_BLOB_PAD bytes.
-template <int C, bool DB>
+template <int C, int M, bool DB>
 struct ShaLds {
     static constexpr int P = 4 * C + 1;       // 16-B pieces per slot row
     static constexpr int ROW = 16 * P;        // bytes per slot row
-    static constexpr int BUF = 64 * ROW;      // one wavefront's step buffer
+    static constexpr int SLOTS = 64 * M;      // a wavefront's messages in flight (M per lane)
+    static constexpr int BUF = SLOTS * ROW;   // one wavefront's step buffer
     static constexpr int NBUF = DB ? 2 : 1;   // double-buffered: step t+1's DMA overlaps step t
     static constexpr int WAVES = 4;           // wavefronts per workgroup
     static constexpr int LDS = WAVES * NBUF * BUF;
@@ -157,151 +158,232 @@ struct ShaQueue {
     }
 };
 
-template <int C>
-__device__ __forceinline__ void sha_lds_fetch(uint8_t* buf, uint64_t chunk, uint32_t lane) {
+// One step's DMA: slot s = m * 64 + lane fetches its P pieces from chunk[m] of its owner lane.
+template <int C, int M>
+__device__ __forceinline__ void sha_lds_fetch(uint8_t* buf, const uint64_t (&chunk)[M], uint32_t lane) {
     typedef __attribute__((address_space(3))) void* lptr;
     typedef __attribute__((address_space(1))) void* gptr;
     constexpr int P = 4 * C + 1;
-    const uint64_t a = chunk & ~(uint64_t)15;
-    const uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32);
+    uint32_t alo[M], ahi[M];
 #pragma unroll
-    for (int i = 0; i < P; ++i) {
+    for (int m = 0; m < M; ++m) {
+        const uint64_t a = chunk[m] & ~(uint64_t)15;
+        alo[m] = (uint32_t)a;
+        ahi[m] = (uint32_t)(a >> 32);
+    }
+#pragma unroll
+    for (int i = 0; i < M * P; ++i) {
         const uint32_t g = (uint32_t)i * 64u + lane;
         const uint32_t slot = g / (uint32_t)P, piece = g - slot * (uint32_t)P;
-        const uint32_t lo = (uint32_t)__shfl((int)alo, (int)slot, 64), hi = (uint32_t)__shfl((int)ahi, (int)slot, 64);
+        const uint32_t owner = slot & 63u, m = slot >> 6;
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {  // the slot's sub-index m is per lane: fetch each, keep one
+            const uint32_t l = (uint32_t)__shfl((int)alo[k], (int)owner, 64), h = (uint32_t)__shfl((int)ahi[k], (int)owner, 64);
+            if (M == 1 || m == (uint32_t)k) {
+                lo = l;
+                hi = h;
+            }
+        }
         const uint64_t src = (((uint64_t)hi << 32) | lo) + 16u * piece;
         __builtin_amdgcn_global_load_lds((gptr)(uintptr_t)src, (lptr)(buf + i * 1024), 16, 0, 0);
     }
 }
 
-template <int C, bool DB>
+// M independent compressions interleaved round by round: the M dependency chains give the
+// scheduler M x the instruction-level parallelism of one (SHA-256's rounds are a serial chain).
+// live[m] false: the state of message m is left unchanged.
+template <int M>
+__device__ __forceinline__ void compress_multi(uint32_t (&h)[M][8], uint32_t (&w)[M][16], const bool (&live)[M]) {
+    uint32_t a[M], b[M], c[M], d[M], e[M], f[M], g[M], hh[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        a[m] = h[m][0]; b[m] = h[m][1]; c[m] = h[m][2]; d[m] = h[m][3];
+        e[m] = h[m][4]; f[m] = h[m][5]; g[m] = h[m][6]; hh[m] = h[m][7];
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            uint32_t wi;
+            if (i < 16) {
+                wi = w[m][i];
+            } else {
+                const uint32_t w15 = w[m][(i + 1) & 15], w2 = w[m][(i + 14) & 15];
+                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                wi = w[m][i & 15] + s0 + w[m][(i + 9) & 15] + s1;
+                w[m][i & 15] = wi;
+            }
+            const uint32_t S1 = xor3(rotr(e[m], 6), rotr(e[m], 11), rotr(e[m], 25));
+            const uint32_t ch = __builtin_amdgcn_bitop3_b32(e[m], f[m], g[m], 0xCA);
+            const uint32_t t1 = hh[m] + S1 + ch + K256[i] + wi;
+            const uint32_t S0 = xor3(rotr(a[m], 2), rotr(a[m], 13), rotr(a[m], 22));
+            const uint32_t maj = __builtin_amdgcn_bitop3_b32(a[m], b[m], c[m], 0xE8);
+            hh[m] = g[m];
+            g[m] = f[m];
+            f[m] = e[m];
+            e[m] = d[m] + t1;
+            d[m] = c[m];
+            c[m] = b[m];
+            b[m] = a[m];
+            a[m] = t1 + S0 + maj;
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        if (live[m]) {
+            h[m][0] += a[m]; h[m][1] += b[m]; h[m][2] += c[m]; h[m][3] += d[m];
+            h[m][4] += e[m]; h[m][5] += f[m]; h[m][6] += g[m]; h[m][7] += hh[m];
+        }
+    }
+}
+
+__device__ __forceinline__ void sha_init(uint32_t (&h)[8]) {
+    h[0] = 0x6a09e667;
+    h[1] = 0xbb67ae85;
+    h[2] = 0x3c6ef372;
+    h[3] = 0xa54ff53a;
+    h[4] = 0x510e527f;
+    h[5] = 0x9b05688c;
+    h[6] = 0x1f83d9ab;
+    h[7] = 0x5be0cd19;
+}
+
+template <int C, int M, bool DB>
 __global__ __launch_bounds__(256) void sha256_lds_kernel(const uint8_t* __restrict__ blob,
                                                          const uint64_t* __restrict__ off,
                                                          const uint32_t* __restrict__ len,
                                                          const uint32_t* __restrict__ order,
                                                          uint8_t* __restrict__ dig, uint32_t n,
                                                          uint32_t* __restrict__ ctr) {
-    using L = ShaLds<C, DB>;
+    using L = ShaLds<C, M, DB>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[L::LDS];
     const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
     uint8_t* const wbuf = lds + wid * L::NBUF * L::BUF;
+    const uint64_t blob0 = (uint64_t)(uintptr_t)blob;
     ShaQueue q;
-    // this lane's current message: start address, length, blocks, next block
-    bool act = false;
-    uint32_t mi = 0, ml = 0, nb = 0, b = 0;
-    uint64_t base = (uint64_t)(uintptr_t)blob;
-    uint32_t h[8];
-    auto start = [&](uint32_t idx) {
-        act = idx < n;
-        if (!act) return;
-        mi = order ? order[idx] : idx;
-        ml = len[mi];
-        base = (uint64_t)(uintptr_t)blob + off[mi];
-        b = 0;
-        nb = sha256_nblocks(ml);
-        h[0] = 0x6a09e667;
-        h[1] = 0xbb67ae85;
-        h[2] = 0x3c6ef372;
-        h[3] = 0xa54ff53a;
-        h[4] = 0x510e527f;
-        h[5] = 0x9b05688c;
-        h[6] = 0x1f83d9ab;
-        h[7] = 0x5be0cd19;
-    };
-    start(q.take(true, lane, n, ctr));
-    sha_lds_fetch<C>(wbuf, act ? base : (uint64_t)(uintptr_t)blob, lane);
+    // this lane's M current messages: index, length, blocks, next block, start address, state
+    bool act[M];
+    uint32_t mi[M], ml[M], nb[M], b[M];
+    uint64_t base[M], pf[M];
+    uint32_t h[M][8];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const uint32_t idx = q.take(true, lane, n, ctr);
+        act[m] = idx < n;
+        mi[m] = ml[m] = nb[m] = b[m] = 0;
+        base[m] = blob0;
+        if (act[m]) {
+            mi[m] = order ? order[idx] : idx;
+            ml[m] = len[mi[m]];
+            base[m] = blob0 + off[mi[m]];
+            nb[m] = sha256_nblocks(ml[m]);
+        }
+        sha_init(h[m]);
+        pf[m] = base[m];
+    }
+    sha_lds_fetch<C, M>(wbuf, pf, lane);
     for (uint32_t t = 0;; ++t) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step t's rows have landed
-        if (!__any(act)) break;
+        bool any = false;
+#pragma unroll
+        for (int m = 0; m < M; ++m) any = any || act[m];
+        if (!__any(any)) break;
         const uint8_t* cur = wbuf + (DB ? (t & 1u) * L::BUF : 0);
-        // lanes whose message ends in this step draw their next one now, so that step t+1's
-        // DMA fetches it
-        const bool fin = act && b + C >= nb;
-        const uint32_t nidx = q.take(fin, lane, n, ctr);
-        uint32_t nmi = 0, nml = 0;
-        uint64_t nbase = (uint64_t)(uintptr_t)blob, pf = nbase;
-        if (fin && nidx < n) {
-            nmi = order ? order[nidx] : nidx;
-            nml = len[nmi];
-            nbase += off[nmi];
-            pf = nbase;
-        } else if (act && !fin) {
-            pf = base + 64ull * (b + C);
+        // messages that end in this step draw their successors now, so that step t+1's DMA
+        // fetches them
+        bool fin[M];
+        uint32_t nidx[M], nmi[M], nml[M];
+        uint64_t nbase[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            fin[m] = act[m] && b[m] + C >= nb[m];
+            nidx[m] = q.take(fin[m], lane, n, ctr);
+            nmi[m] = nml[m] = 0;
+            nbase[m] = blob0;
+            pf[m] = blob0;
+            if (fin[m] && nidx[m] < n) {
+                nmi[m] = order ? order[nidx[m]] : nidx[m];
+                nml[m] = len[nmi[m]];
+                nbase[m] += off[nmi[m]];
+                pf[m] = nbase[m];
+            } else if (act[m] && !fin[m]) {
+                pf[m] = base[m] + 64ull * (b[m] + C);
+            }
         }
-        if (DB) sha_lds_fetch<C>(wbuf + ((t + 1u) & 1u) * L::BUF, pf, lane);
-        if (act) {
-            // this lane's row: bytes [o, o + 64 C) hold blocks b .. b + C - 1
-            const uint32_t o = (uint32_t)base & 15u;
-            const uint32_t* row = reinterpret_cast<const uint32_t*>(cur + lane * L::ROW) + (o >> 2);
-            const uint32_t sh = o & 3u;
-            // v_perm_b32 selector: big-endian word of stream bytes sh .. sh + 3 of (hi:lo)
-            const uint32_t sel = ((sh) << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
+        if (DB) sha_lds_fetch<C, M>(wbuf + ((t + 1u) & 1u) * L::BUF, pf, lane);
 #pragma unroll
-            for (int j = 0; j < C; ++j) {
-                const uint32_t bi = b + j;
-                if (bi < nb) {
-                    uint32_t w[16];
-                    uint32_t lo = row[16 * j];
+        for (int j = 0; j < C; ++j) {
+            uint32_t w[M][16];
+            bool live[M];
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const uint32_t hi = row[16 * j + i + 1];
-                        w[i] = __builtin_amdgcn_perm(hi, lo, sel);
-                        lo = hi;
-                    }
-                    const uint32_t full = ml >> 6;
-                    if (__builtin_expect(__any(bi >= full), 0)) {
-                        if (bi >= full) {
-                            const uint32_t rem = ml & 63u;
-                            const bool first = bi == full;
-                            const uint32_t krem = first ? rem : 0;
+            for (int m = 0; m < M; ++m) {
+                // this message's row: bytes [o, o + 64 C) hold blocks b .. b + C - 1
+                const uint32_t bi = b[m] + j;
+                live[m] = act[m] && bi < nb[m];
+                const uint32_t o = (uint32_t)base[m] & 15u;
+                const uint32_t* row = reinterpret_cast<const uint32_t*>(cur + (m * 64u + lane) * L::ROW) + (o >> 2);
+                const uint32_t sh = o & 3u;
+                // v_perm_b32 selector: big-endian word of stream bytes sh .. sh + 3 of (hi:lo)
+                const uint32_t sel = ((sh) << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
+                uint32_t lo = row[16 * j];
 #pragma unroll
-                            for (int i = 0; i < 16; ++i) {
-                                const uint32_t b0 = 4 * i;
-                                uint32_t keep_mask;
-                                if (b0 + 4 <= krem) keep_mask = 0xffffffffu;
-                                else if (b0 >= krem) keep_mask = 0;
-                                else keep_mask = 0xffffffffu << (8 * (4 - (krem - b0)));
-                                uint32_t v = w[i] & keep_mask;
-                                if (first && rem >= b0 && rem < b0 + 4) v |= 0x80u << (8 * (3 - (rem - b0)));
-                                w[i] = v;
-                            }
-                            if (bi + 1 == nb) {
-                                const uint64_t bits = (uint64_t)ml * 8;
-                                w[14] = (uint32_t)(bits >> 32);
-                                w[15] = (uint32_t)bits;
-                            }
+                for (int i = 0; i < 16; ++i) {
+                    const uint32_t hi = row[16 * j + i + 1];
+                    w[m][i] = __builtin_amdgcn_perm(hi, lo, sel);
+                    lo = hi;
+                }
+                const uint32_t full = ml[m] >> 6;
+                if (__builtin_expect(__any(live[m] && bi >= full), 0)) {
+                    if (bi >= full) {
+                        // the padded tail: rem data bytes, 0x80, zeros, the 64-bit bit length
+                        const uint32_t rem = ml[m] & 63u;
+                        const bool first = bi == full;
+                        const uint32_t krem = first ? rem : 0;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const uint32_t b0 = 4 * i;
+                            uint32_t keep_mask;
+                            if (b0 + 4 <= krem) keep_mask = 0xffffffffu;
+                            else if (b0 >= krem) keep_mask = 0;
+                            else keep_mask = 0xffffffffu << (8 * (4 - (krem - b0)));
+                            uint32_t v = w[m][i] & keep_mask;
+                            if (first && rem >= b0 && rem < b0 + 4) v |= 0x80u << (8 * (3 - (rem - b0)));
+                            w[m][i] = v;
+                        }
+                        if (bi + 1 == nb[m]) {
+                            const uint64_t bits = (uint64_t)ml[m] * 8;
+                            w[m][14] = (uint32_t)(bits >> 32);
+                            w[m][15] = (uint32_t)bits;
                         }
                     }
-                    compress(h, w);
                 }
             }
+            bool any_live = false;
+#pragma unroll
+            for (int m = 0; m < M; ++m) any_live = any_live || live[m];
+            if (any_live) compress_multi<M>(h, w, live);
         }
-        if (!DB) sha_lds_fetch<C>(wbuf, pf, lane);  // the step's reads are consumed: refill in place
-        if (fin) {
-            uint4* out = reinterpret_cast<uint4*>(dig + 32ull * mi);
-            out[0] = make_uint4(__builtin_bswap32(h[0]), __builtin_bswap32(h[1]), __builtin_bswap32(h[2]),
-                                __builtin_bswap32(h[3]));
-            out[1] = make_uint4(__builtin_bswap32(h[4]), __builtin_bswap32(h[5]), __builtin_bswap32(h[6]),
-                                __builtin_bswap32(h[7]));
-            act = false;
-            if (nidx < n) {
-                act = true;
-                mi = nmi;
-                ml = nml;
-                base = nbase;
-                b = 0;
-                nb = sha256_nblocks(ml);
-                h[0] = 0x6a09e667;
-                h[1] = 0xbb67ae85;
-                h[2] = 0x3c6ef372;
-                h[3] = 0xa54ff53a;
-                h[4] = 0x510e527f;
-                h[5] = 0x9b05688c;
-                h[6] = 0x1f83d9ab;
-                h[7] = 0x5be0cd19;
+        if (!DB) sha_lds_fetch<C, M>(wbuf, pf, lane);  // the step's reads are consumed: refill in place
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            if (fin[m]) {
+                uint4* out = reinterpret_cast<uint4*>(dig + 32ull * mi[m]);
+                out[0] = make_uint4(__builtin_bswap32(h[m][0]), __builtin_bswap32(h[m][1]), __builtin_bswap32(h[m][2]),
+                                    __builtin_bswap32(h[m][3]));
+                out[1] = make_uint4(__builtin_bswap32(h[m][4]), __builtin_bswap32(h[m][5]), __builtin_bswap32(h[m][6]),
+                                    __builtin_bswap32(h[m][7]));
+                act[m] = nidx[m] < n;
+                mi[m] = nmi[m];
+                ml[m] = nml[m];
+                base[m] = nbase[m];
+                b[m] = 0;
+                nb[m] = sha256_nblocks(nml[m]);
+                sha_init(h[m]);
+            } else if (act[m]) {
+                b[m] += C;
             }
-        } else if (act) {
-            b += C;
         }
     }
 }
@@ -360,8 +442,9 @@ extern "C" int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, 
     if (hipMemsetAsync(d_ctr, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     static int variant = -1;
     if (variant < 0) {
-        // A/B measurement only: 0 the per-lane-load kernel; 1..4 the LDS-staged kernel with
-        // (C blocks per step, double-buffered) = (1, yes), (2, yes), (2, no), (4, no)
+        // A/B measurement only: 0 the per-lane-load kernel; else the LDS-staged kernel with
+        // (C blocks per step, M messages per lane, double-buffered) = 1: (1, 1, yes),
+        // 2: (2, 1, yes), 3: (2, 1, no), 5: (1, 2, yes), 6: (1, 2, no), 7: (2, 2, no)
         const char* e = getenv("SBFT_SHA_VARIANT");
         variant = e ? atoi(e) : 2;
     }
@@ -379,10 +462,12 @@ extern "C" int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, 
                            d_len, d_order, d_dig, n, d_ctr);
         break;
     }
-    case 1: launch(sbft::sha256_lds_kernel<1, true>, sbft::ShaLds<1, true>::LDS); break;
-    case 3: launch(sbft::sha256_lds_kernel<2, false>, sbft::ShaLds<2, false>::LDS); break;
-    case 4: launch(sbft::sha256_lds_kernel<4, false>, sbft::ShaLds<4, false>::LDS); break;
-    default: launch(sbft::sha256_lds_kernel<2, true>, sbft::ShaLds<2, true>::LDS); break;
+    case 1: launch(sbft::sha256_lds_kernel<1, 1, true>, sbft::ShaLds<1, 1, true>::LDS); break;
+    case 3: launch(sbft::sha256_lds_kernel<2, 1, false>, sbft::ShaLds<2, 1, false>::LDS); break;
+    case 5: launch(sbft::sha256_lds_kernel<1, 2, true>, sbft::ShaLds<1, 2, true>::LDS); break;
+    case 6: launch(sbft::sha256_lds_kernel<1, 2, false>, sbft::ShaLds<1, 2, false>::LDS); break;
+    case 7: launch(sbft::sha256_lds_kernel<2, 2, false>, sbft::ShaLds<2, 2, false>::LDS); break;
+    default: launch(sbft::sha256_lds_kernel<2, 1, true>, sbft::ShaLds<2, 1, true>::LDS); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -80,3 +80,25 @@ def test_host_alloc_argument_handling():
     assert lib.sbft_gv_host_alloc(0, ctypes.byref(p)) == 0
     assert p.value is None
     lib.sbft_gv_host_free(None)
+
+
+def test_go_binding_uses_only_declared_symbols():
+    """go/gpuverify is uncompiled here (no Go toolchain): at least every C function and macro it
+    names must exist in include/*.h, and every api.Verifier / api.Signer method
+    (pkg/api/dependencies.go:46-71) must be defined."""
+    declared = _declared_symbols()
+    text = ""
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text += open(h).read()
+    macros = set(re.findall(r"#define\s+(SBFT_\w+)", text))
+    go = ""
+    for f in glob.glob(os.path.join(ROOT, "go", "gpuverify", "*.go")):
+        go += open(f).read()
+    used = set(re.findall(r"\bC\.(sbft_\w+)\s*\(", go))
+    assert used and not (used - declared), sorted(used - declared)
+    used_macros = set(re.findall(r"\bC\.(SBFT_\w+)", go))
+    assert not (used_macros - macros), sorted(used_macros - macros)
+    for m in ["VerifyProposal", "VerifyRequest", "VerifyConsenterSig", "VerifySignature", "VerificationSequence",
+              "RequestsFromProposal", "AuxiliaryData", "Sign", "SignProposal", "VerifyConsenterSigs"]:
+        assert re.search(r"func \(\w+ \*(Verifier|Signer)\) %s\(" % m, go), m
+    assert "elided" not in go

@@ -390,3 +390,16 @@ def test_pinned_single_allocation_and_mixed_inputs(gpu):
         assert np.array_equal(gpu.verify(*mixed), want)
     finally:
         block.close()
+
+
+@pytest.mark.parametrize("n", [5000, 70_000])
+def test_all_exceptional_batches(gpu_kernel, p256_vectors, n):
+    """A batch made only of tuples whose lean Shamir ladder hits an exceptional addition
+    (crafted R = infinity, P + P, P + (-P): golden categories r_infinity and shamir_exceptional)
+    goes whole to the fix-up kernel, whose grid covers the worst case; every verdict equals
+    the fixture's (5,000: latency kernels; 70,000: above their 32,768-tuple limit)."""
+    f, exp, cat, names = p256_vectors
+    sel = np.isin(cat, [names.index("r_infinity"), names.index("shamir_exceptional")])
+    idx = np.resize(np.nonzero(sel)[0], n)
+    got = gpu_kernel.verify(*split_fields(f[idx]))
+    assert np.array_equal(got, exp[idx])
