@@ -190,55 +190,6 @@ __device__ __forceinline__ void sha_lds_fetch(uint8_t* buf, const uint64_t (&chu
     }
 }
 
-// M independent compressions interleaved round by round: the M dependency chains give the
-// scheduler M x the instruction-level parallelism of one (SHA-256's rounds are a serial chain).
-// live[m] false: the state of message m is left unchanged.
-template <int M>
-__device__ __forceinline__ void compress_multi(uint32_t (&h)[M][8], uint32_t (&w)[M][16], const bool (&live)[M]) {
-    uint32_t a[M], b[M], c[M], d[M], e[M], f[M], g[M], hh[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        a[m] = h[m][0]; b[m] = h[m][1]; c[m] = h[m][2]; d[m] = h[m][3];
-        e[m] = h[m][4]; f[m] = h[m][5]; g[m] = h[m][6]; hh[m] = h[m][7];
-    }
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-            uint32_t wi;
-            if (i < 16) {
-                wi = w[m][i];
-            } else {
-                const uint32_t w15 = w[m][(i + 1) & 15], w2 = w[m][(i + 14) & 15];
-                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-                wi = w[m][i & 15] + s0 + w[m][(i + 9) & 15] + s1;
-                w[m][i & 15] = wi;
-            }
-            const uint32_t S1 = xor3(rotr(e[m], 6), rotr(e[m], 11), rotr(e[m], 25));
-            const uint32_t ch = __builtin_amdgcn_bitop3_b32(e[m], f[m], g[m], 0xCA);
-            const uint32_t t1 = hh[m] + S1 + ch + K256[i] + wi;
-            const uint32_t S0 = xor3(rotr(a[m], 2), rotr(a[m], 13), rotr(a[m], 22));
-            const uint32_t maj = __builtin_amdgcn_bitop3_b32(a[m], b[m], c[m], 0xE8);
-            hh[m] = g[m];
-            g[m] = f[m];
-            f[m] = e[m];
-            e[m] = d[m] + t1;
-            d[m] = c[m];
-            c[m] = b[m];
-            b[m] = a[m];
-            a[m] = t1 + S0 + maj;
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        if (live[m]) {
-            h[m][0] += a[m]; h[m][1] += b[m]; h[m][2] += c[m]; h[m][3] += d[m];
-            h[m][4] += e[m]; h[m][5] += f[m]; h[m][6] += g[m]; h[m][7] += hh[m];
-        }
-    }
-}
-
 __device__ __forceinline__ void sha_init(uint32_t (&h)[8]) {
     h[0] = 0x6a09e667;
     h[1] = 0xbb67ae85;
