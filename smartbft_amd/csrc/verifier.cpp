@@ -26,6 +26,11 @@
 #include <unordered_map>
 #include <vector>
 
+#include <climits>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 namespace {
 
 // ------------------------------------------------------------------ SHA-256 (host)
@@ -310,6 +315,26 @@ ProposalScratch& proposal_scratch() {
     return s;
 }
 
+// A one-shot "results are published" flag for the followers of a coalesced batch. They spin
+// briefly, then sleep on a futex; the leader's wake-up does not make them re-acquire a mutex
+// one after another (a condition variable's notify_all does: ~3-4 us per follower, 0.25 ms
+// for a 66-vote quorum).
+struct DoneFlag {
+    std::atomic<int> v{0};
+    void set() {
+        v.store(1, std::memory_order_release);
+        syscall(SYS_futex, reinterpret_cast<int*>(&v), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+    }
+    void wait() {
+        for (int i = 0; i < 256; ++i) {
+            if (v.load(std::memory_order_acquire)) return;
+            __builtin_ia32_pause();
+        }
+        while (!v.load(std::memory_order_acquire))
+            syscall(SYS_futex, reinterpret_cast<int*>(&v), FUTEX_WAIT_PRIVATE, 0, nullptr, nullptr, 0);
+    }
+};
+
 const char* REQ_MAGIC = "SBR1";
 const char* MSG_MAGIC = "SBC1";
 
@@ -492,9 +517,10 @@ struct sbft_verifier {
     };
     struct CsBatch {
         std::vector<CsEntry*> entries;
-        bool closed = false, done = false;
+        bool closed = false;
         int rc = 0;
-        std::condition_variable cv;
+        std::condition_variable cv;  // wakes the leader when the batch fills
+        DoneFlag done;               // wakes the followers when the results are published
     };
     std::mutex cs_mu;
     std::shared_ptr<CsBatch> cs_open;
@@ -1012,10 +1038,9 @@ static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const 
                 batch->closed = true;
                 v->cs_open.reset();
             }
-        } else {
-            batch->cv.wait(g, [&] { return batch->done; });
         }
     }
+    if (!leader) batch->done.wait();
     if (leader) {
         // closed: nobody else touches the entries until done is published
         const size_t n = batch->entries.size();
@@ -1030,14 +1055,12 @@ static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const 
         const int rc = v->consenter_batch(sigs.data(), n, props.data(), sts.data(), &whys);
         v->cs_launches++;
         v->cs_calls += n;
-        std::lock_guard<std::mutex> g(v->cs_mu);
         for (size_t i = 0; i < n; ++i) {
             batch->entries[i]->status = rc ? 0 : sts[i];
             if (!rc) batch->entries[i]->why = std::move(whys[i]);
         }
         batch->rc = rc;
-        batch->done = true;
-        batch->cv.notify_all();
+        batch->done.set();
     }
     st = me.status;
     why = std::move(me.why);
@@ -1289,9 +1312,10 @@ struct sbft_request_batcher {
     };
     struct Batch {
         std::vector<Entry*> entries;
-        bool closed = false, done = false;
+        bool closed = false;
         int rc = 0;
-        std::condition_variable cv;
+        std::condition_variable cv;  // wakes the leader when the batch fills
+        DoneFlag done;               // wakes the followers when the results are published
     };
     std::mutex mu;
     std::shared_ptr<Batch> open;
@@ -1346,10 +1370,9 @@ int sbft_request_batcher_verify(sbft_request_batcher* b, const uint8_t* req, siz
                 batch->closed = true;
                 b->open.reset();
             }
-        } else {
-            batch->cv.wait(g, [&] { return batch->done; });
         }
     }
+    if (!leader) batch->done.wait();
     if (leader) {
         // the batch is closed: nobody else touches its entries until done is published
         const size_t n = batch->entries.size();
@@ -1364,14 +1387,12 @@ int sbft_request_batcher_verify(sbft_request_batcher* b, const uint8_t* req, siz
         const int rc = b->v->requests_batch(reqs.data(), lens.data(), n, st.data(), parsed);
         b->launches++;
         b->requests += n;
-        std::lock_guard<std::mutex> g(b->mu);
         for (size_t i = 0; i < n; ++i) {
             batch->entries[i]->status = st[i];
             batch->entries[i]->parsed = std::move(parsed[i]);
         }
         batch->rc = rc;
-        batch->done = true;
-        batch->cv.notify_all();
+        batch->done.set();
     }
     if (batch->rc) {
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(batch->rc));
