@@ -311,7 +311,7 @@ class GpuVerifier:
                                              (d_qy, "qy"), (d_r, "r"), (d_s, "s"))]
         self._check(self.L.sbft_gv_sign_p256_dev(
             self.ctx, d_status.device.index, p[0], p[1], p[2], n, p[3], p[4], p[5], p[6],
-            _dev(d_status, n, "status"), self._stream(stream)), "sbft_gv_sign_p256_dev")
+            _dev(d_status, n, "status"), self._stream(stream, d_status.device)), "sbft_gv_sign_p256_dev")
 
     def sha256(self, blob: np.ndarray, off: np.ndarray, ln: np.ndarray) -> np.ndarray:
         blob, off, ln, n = _msgs(blob, off, ln)
@@ -366,9 +366,11 @@ class GpuVerifier:
 
     # ---- device-resident (torch tensors on a HIP device) ----
     @staticmethod
-    def _stream(stream):
+    def _stream(stream, device=None):
+        """The given stream, else the current stream of `device` (the device the call's
+        tensors live on: a stream of another device would be invalid for the launch)."""
         import torch
-        s = stream if stream is not None else torch.cuda.current_stream()
+        s = stream if stream is not None else torch.cuda.current_stream(device)
         return ctypes.c_void_p(s.cuda_stream)
 
     def verify_dev(self, d_digest, d_r, d_s, d_qx, d_qy, d_ok, stream=None):
@@ -377,7 +379,7 @@ class GpuVerifier:
         p = [_dev(t, 32 * n, w) for t, w in ((d_digest, "digest"), (d_r, "r"), (d_s, "s"), (d_qx, "qx"),
                                              (d_qy, "qy"))]
         self._check(self.L.sbft_gv_verify_p256_dev(
-            self.ctx, dev, *p, n, _dev(d_ok, n, "ok"), self._stream(stream)), "sbft_gv_verify_p256_dev")
+            self.ctx, dev, *p, n, _dev(d_ok, n, "ok"), self._stream(stream, d_ok.device)), "sbft_gv_verify_p256_dev")
 
     def sha256_verify_dev(self, d_blob, d_off, d_len, d_r, d_s, d_qx, d_qy, d_ok, d_dig, stream=None):
         """Device-resident hash + verify (sbft_gv_sha256_verify_p256_dev): digests of the
@@ -390,7 +392,7 @@ class GpuVerifier:
         self._check(self.L.sbft_gv_sha256_verify_p256_dev(
             self.ctx, d_ok.device.index, d_blob.data_ptr(), _dev(d_off, n, "offsets", d_off.dtype),
             _dev(d_len, n, "lengths", d_len.dtype), None, *p, n, _dev(d_ok, n, "ok"),
-            _dev(d_dig, 32 * n, "digests"), self._stream(stream)), "sbft_gv_sha256_verify_p256_dev")
+            _dev(d_dig, 32 * n, "digests"), self._stream(stream, d_ok.device)), "sbft_gv_sha256_verify_p256_dev")
 
     def kernel_timing(self, enable: bool):
         """Record HIP events around each device-resident verify's main kernel."""
@@ -416,5 +418,5 @@ class GpuVerifier:
         p_ord = _dev(d_order, n, "order", d_order.dtype if d_order.dtype in (torch.int32, torch.uint32)
                      else torch.int32) if d_order is not None else None
         self._check(self.L.sbft_gv_sha256_dev(self.ctx, d_dig.device.index, d_blob.data_ptr(), p_off, p_len,
-                                              p_ord, n, _dev(d_dig, 32 * n, "digests"), self._stream(stream)),
+                                              p_ord, n, _dev(d_dig, 32 * n, "digests"), self._stream(stream, d_dig.device)),
                     "sbft_gv_sha256_dev")
