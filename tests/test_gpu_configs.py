@@ -1,4 +1,4 @@
-"""GPU parity tests at the workloads of BASELINE.json configs 3 and 5, through the C ABI,
+"""GPU parity tests at the workloads of BASELINE.json configs 1, 3 and 5, through the C ABI,
 against the oracle (oracle/p256_oracle.c, the C restatement of Go crypto/ecdsa.Verify) and
 hashlib-independent SHA-256 (the oracle's).
 
@@ -9,7 +9,11 @@ Both the generic launch and the registered-client (keyed) launch.
 
 Config 5: hash + verify of payloads uniform in [1 KiB, 64 KiB] with corrupted signatures and
 tampered payloads, fused (tuples passed in) and framed (tuples gathered on the device from the
-signed-request layout), on the one-lane throughput kernel and the two-lane latency kernel."""
+signed-request layout), on the one-lane throughput kernel and the two-lane latency kernel,
+and streamed from host memory (sbft_gv_sha256_verify_p256_stream).
+
+Config 1: the naive_chain shape (4 nodes, 1k requests per proposal) driven through the plugin
+mirror in the library's call sequence (Go is absent: the protocol itself is out of scope)."""
 import hashlib
 
 import numpy as np
@@ -256,3 +260,55 @@ def test_config5_streamed_edges(gpu, config5_batch):
     assert gpu.sha256_verify_stream(blob, off[:0], ln[:0], z, z, z, z).shape == (0,)
     with pytest.raises(Exception):  # a message past the blob's end is rejected, not read
         gpu.sha256_verify_stream(blob[:100], off[:2], ln[:2], *[c[:2] for c in cols])
+
+
+# ---------------------------------------------------------------- config 1 (plumbing shape)
+def test_config1_four_nodes_1k_requests(gpu):
+    """BASELINE config 1's shape (examples/naive_chain: 4 nodes, f = 1, 1k signed requests per
+    proposal) driven through the plugin mirror the way the library drives an api.Verifier
+    (Go and the library are absent here; the call sequence follows view.go): every node
+    verifies the leader's proposal (view.go:555), signs it (SignProposal, view.go:481),
+    collects q-1 = 2 commit votes from the others (processCommits, view.go:519-551), and the next
+    proposal carries the previous decision's q signatures, which every node re-verifies
+    (verifyPrevCommitSignatures, view.go:606-647). A proposal with one forged request is
+    rejected by every node at the same index (view.go:386-393)."""
+    import hashlib
+    from smartbft_amd import plugin
+    q, f = plugin.compute_quorum(4)
+    assert (q, f) == (3, 1)
+    priv = lambda tag: (int.from_bytes(hashlib.sha256(b"c1-" + tag).digest(), "big") % oracle.N).to_bytes(32, "big")
+    signers = [plugin.Signer(gpu, i, priv(b"node%d" % i)) for i in range(1, 5)]
+    nodes = [plugin.Verifier(gpu, 1) for _ in range(4)]
+    for v in nodes:
+        for s in signers:
+            v.add_consenter(s.id, s.public_key())
+    clients = [plugin.Signer(gpu, 100 + c, priv(b"client%d" % c)) for c in range(16)]
+    prev_sigs, prev_prop = None, None
+    for seq in range(3):
+        reqs = [clients[i % 16].make_request(f"c{i % 16}", f"s{seq}-r{i}", b"tx-%d-%d" % (seq, i) * 4)
+                for i in range(1000)]
+        prop = plugin.Proposal(plugin.encode_payload(reqs), b"hdr-%d" % seq, b"md-%d" % seq, 1)
+        infos = [v.VerifyProposal(prop) for v in nodes]
+        assert all(x == infos[0] for x in infos) and len(infos[0]) == 1000
+        if prev_sigs is not None:
+            for v in nodes:
+                assert v.verify_prev_commit_signatures(prev_sigs, prev_prop, curr_vseq=1) is False
+        votes = [s.SignProposal(prop, b"prepares-from-%d" % s.id) for s in signers]
+        digest = prop.Digest()
+        decided = []
+        for k, v in enumerate(nodes):
+            others = [(votes[j], digest) for j in range(4) if j != k]
+            idx, log = v.collect_commits(others, prop, need=q - 1)
+            assert len(idx) == q - 1 and log == ""
+            decided.append([others[i][0] for i in idx] + [votes[k]])
+        prev_sigs, prev_prop = decided[0], prop
+    # a forged request: every node rejects the proposal at the same index
+    bad = list(reqs)
+    bad[517] = bad[517][:-1] + bytes([bad[517][-1] ^ 1])
+    badp = plugin.Proposal(plugin.encode_payload(bad), b"hdr-x", b"md-x", 1)
+    for v in nodes:
+        with pytest.raises(plugin.VerifyError) as ei:
+            v.VerifyProposal(badp)
+        assert ei.value.index == 517 and ei.value.code == plugin.EVERIFY
+    for v in nodes:
+        v.close()
