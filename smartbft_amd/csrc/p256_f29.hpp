@@ -758,4 +758,33 @@ SBFT_DEV fe f29_canon_plain(const f29& a) {
     return lo;
 }
 
+// The lean additions leave Z = 0 from the first exceptional case on (P + P, P + (-P),
+// R = infinity), so Z == 0 (mod p) flags the tuple for the general path (exc). Otherwise
+// x(R) mod n == r is checked projectively: X == r Z^2 or, when r + n < p, X == (r + n) Z^2.
+SBFT_DEV bool verify_final(const jp29& acc, const fe& rv, bool& exc) {
+    exc = fe_is_zero_raw(f29_canon_plain(acc.z));
+    const f29 r2 = f29_const(C29_R2);
+    f29 z2, lhs, rm;
+    f29_sqr(z2, acc.z);
+    const fe xc = f29_canon_plain(acc.x);
+    f29_mul(rm, f29_from_u256(rv), r2);
+    f29_mul(lhs, rm, z2);
+    bool accept = fe_eq(f29_canon_plain(lhs), xc);
+    // R.x in [n, p): compare with r + n as well when r + n < p
+    fe rn;
+    u64 c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        c = (u64)rv.v[k] + P256_N[k] + c;
+        rn.v[k] = lo32(c);
+        c >>= 32;
+    }
+    if (c == 0 && fe_lt(rn, P256_P)) {
+        f29_mul(rm, f29_from_u256(rn), r2);
+        f29_mul(lhs, rm, z2);
+        accept = accept || fe_eq(f29_canon_plain(lhs), xc);
+    }
+    return accept;
+}
+
 }  // namespace sbft

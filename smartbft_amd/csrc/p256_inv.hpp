@@ -211,9 +211,12 @@ SBFT_HD void reduce_unpack(uint32_t out[8], s30 a, bool P) {
     }
 }
 
-// out = x^-1 mod m for 0 < x < m (8 x 32-bit little-endian limbs; m = n, or p when P).
-// x = 0 gives 0. tab: SBFT_DIVSTEP5_TABLE (p256_inv_table.inc).
-SBFT_HD void inv_mod(uint32_t out[8], const uint32_t x[8], const uint32_t* tab, bool P) {
+// out = c x^-1 mod m for 0 < x < m and c < m (8 x 32-bit little-endian limbs; m = n, or p
+// when P; c = null means 1). x = 0 gives 0. tab: SBFT_DIVSTEP5_TABLE (p256_inv_table.inc).
+// Starting e at c instead of 1 keeps d x = c f, e x = c g (mod m), so the result comes out
+// scaled for free (c = 2^256 mod n: the Montgomery form the fn_ arithmetic takes).
+SBFT_HD void inv_mod(uint32_t out[8], const uint32_t x[8], const uint32_t* tab, bool P,
+                     const uint32_t* c = nullptr) {
     s30 f, g, d, e;
     mod30(f.v, P);
     pack30(g, x);
@@ -221,7 +224,10 @@ SBFT_HD void inv_mod(uint32_t out[8], const uint32_t x[8], const uint32_t* tab, 
         d.v[i] = 0;
         e.v[i] = 0;
     }
-    e.v[0] = 1;
+    if (c)
+        pack30(e, c);
+    else
+        e.v[0] = 1;
     int32_t delta = 1;
 SBFT_UNROLL1
     for (int batch = 0; batch < 26 && !is_zero30(g); ++batch) {
@@ -239,6 +245,86 @@ SBFT_UNROLL1
 }
 SBFT_HD void inv_mod_n(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) { inv_mod(out, x, tab, false); }
 SBFT_HD void inv_mod_p(uint32_t out[8], const uint32_t x[8], const uint32_t* tab) { inv_mod(out, x, tab, true); }
+// c x^-1 mod n
+SBFT_HD void inv_mod_n_scaled(uint32_t out[8], const uint32_t x[8], const uint32_t c[8], const uint32_t* tab) {
+    inv_mod(out, x, tab, false, c);
+}
+
+#if defined(__HIPCC__)
+// The same inversion on a whole wavefront, for latency paths (every lane passes the same x and
+// c and gets the result). Lane i < 9 holds limb i of f, g, d, e (lanes >= 9 hold zeros). Each
+// batch's 30 divsteps run wave-uniformly on the low words (LDS table, as above); the 2x2
+// transition matrix then updates every limb at once, two or three 64-bit mads per number per
+// lane, and the exact division by 2^30 is two parallel carry rounds (DPP shifts by one lane):
+// limbs end in [-2, 2^30 + 4), the top limb signed. The serial 9-limb carry chains of
+// update_fg / update_de (the one-lane form's critical path) are gone.
+__device__ __forceinline__ int32_t lane_limb(const int32_t v[9], int li) {
+    int32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r = li == k ? v[k] : r;
+    return r;
+}
+// (sum_i c_i 2^(30 i)) / 2^30 for c divisible by 2^30, limb i of c on lane i (lane 9 holds 0)
+__device__ __forceinline__ int32_t div30_lanes(int64_t c, bool top) {
+    const int32_t lo = (int32_t)((uint32_t)c & SBFT_M30);
+    const int32_t lo_up = __builtin_amdgcn_update_dpp(0, lo, 0x101, 0xf, 0xf, true);  // row_shl:1: lane i+1's
+    const int64_t x = (c >> 30) + (int64_t)lo_up;     // limb i of the quotient, |.| < 2^32
+    const int32_t lo2 = top ? (int32_t)x : (int32_t)((uint32_t)x & SBFT_M30);
+    const int32_t hi2 = top ? 0 : (int32_t)(x >> 30);  // in [-4, 4]
+    const int32_t hi_dn = __builtin_amdgcn_update_dpp(0, hi2, 0x111, 0xf, 0xf, true);  // row_shr:1: lane i-1's
+    return lo2 + hi_dn;
+}
+__device__ __forceinline__ void inv_mod_wave(uint32_t out[8], const uint32_t x[8], const uint32_t* tab, bool P,
+                                             const uint32_t* c = nullptr) {
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const bool on = lane < 9, top = lane == 8;
+    int32_t M[9];
+    mod30(M, P);
+    s30 xs, cs;
+    pack30(xs, x);
+    if (c) {
+        pack30(cs, c);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) cs.v[i] = i == 0 ? 1 : 0;
+    }
+    const int32_t m_i = on ? lane_limb(M, lane) : 0;
+    int32_t f_i = m_i, g_i = on ? lane_limb(xs.v, lane) : 0, d_i = 0, e_i = on ? lane_limb(cs.v, lane) : 0;
+    const uint32_t minv = P ? SBFT_PINV30 : SBFT_NINV30;
+    int32_t delta = 1;
+    SBFT_UNROLL1
+    for (int batch = 0; batch < 26; ++batch) {
+        if (__builtin_amdgcn_ballot_w64(g_i != 0) == 0) break;  // g == 0
+        const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(f_i, 0), g0 = (uint32_t)__builtin_amdgcn_readlane(g_i, 0);
+        int32_t u, v, q, r;
+        delta = divsteps30(delta, f0, g0, tab, u, v, q, r);
+        const int32_t d0 = __builtin_amdgcn_readlane(d_i, 0), e0 = __builtin_amdgcn_readlane(e_i, 0);
+        const int64_t cd0 = (int64_t)u * d0 + (int64_t)v * e0, ce0 = (int64_t)q * d0 + (int64_t)r * e0;
+        const int32_t md = (int32_t)((0u - (uint32_t)cd0 * minv) & SBFT_M30);
+        const int32_t me = (int32_t)((0u - (uint32_t)ce0 * minv) & SBFT_M30);
+        const int64_t cf = mac(mac(0, u, f_i), v, g_i);
+        const int64_t cg = mac(mac(0, q, f_i), r, g_i);
+        const int64_t cd = mac(mac(mac(0, u, d_i), v, e_i), md, m_i);
+        const int64_t ce = mac(mac(mac(0, q, d_i), r, e_i), me, m_i);
+        f_i = div30_lanes(cf, top);
+        g_i = div30_lanes(cg, top);
+        d_i = div30_lanes(cd, top);
+        e_i = div30_lanes(ce, top);
+        if (!on) f_i = g_i = d_i = e_i = 0;
+    }
+    s30 f, d;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        f.v[i] = __builtin_amdgcn_readlane(f_i, i);
+        d.v[i] = __builtin_amdgcn_readlane(d_i, i);
+    }
+    add_kn(f, 0, P);  // canonical limbs: f = +-1
+    if (f.v[8] < 0)
+        for (int i = 0; i < 9; ++i) d.v[i] = -d.v[i];
+    add_kn(d, 0, P);
+    reduce_unpack(out, d, P);
+}
+#endif
 
 #if defined(__HIPCC__)
 __device__ __constant__ static const uint32_t C_DIVSTEP5[SBFT_DIVSTEP5_WORDS] = SBFT_DIVSTEP5_TABLE;

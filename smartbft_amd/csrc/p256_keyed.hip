@@ -25,12 +25,18 @@
 //
 // Verdicts are bit-exact with Go crypto/ecdsa.Verify (same semantics as p256_verify.hip;
 // oracle/p256_oracle.c is the parity reference). An unregistered/invalid key id verifies false.
+#include "p256_f29.hpp"
 #include "p256_inv.hpp"
 #include "p256_point.hpp"
 #include "sbft_kernels.h"
 #include "sha256_dev.hpp"
 
 namespace sbft {
+
+// Phase marks for tools/keyed_phases.hip (which defines the macro before including this file)
+#ifndef SBFT_KEYED_MARK
+#define SBFT_KEYED_MARK(i) ((void)0)
+#endif
 
 #define COMB_WINDOWS 32
 #define COMB_ENTRIES 256
@@ -140,10 +146,17 @@ SBFT_DEV fe dpp_fe(const fe& a) {
 #define QB(J) ((J) * 0x55)               // quad_perm [J,J,J,J]
 #define PB0 0xA0                         // quad_perm [0,0,2,2]
 #define PB1 0xF5                         // quad_perm [1,1,3,3]
+// Two levels of two-way selects on the bits of j (v_cndmask): written as a j == 0/1/2 chain,
+// the selects over whole structs were lowered to a scratch array indexed by j.
+SBFT_DEV u32 pick4(bool b0, bool b1, u32 a0, u32 a1, u32 a2, u32 a3) {
+    const u32 lo = b0 ? a1 : a0, hi = b0 ? a3 : a2;
+    return b1 ? hi : lo;
+}
 SBFT_DEV fe sel4(u32 j, const fe& a0, const fe& a1, const fe& a2, const fe& a3) {
+    const bool b0 = (j & 1u) != 0, b1 = (j & 2u) != 0;
     fe o;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o.v[k] = j == 0 ? a0.v[k] : (j == 1 ? a1.v[k] : (j == 2 ? a2.v[k] : a3.v[k]));
+    for (int k = 0; k < 8; ++k) o.v[k] = pick4(b0, b1, a0.v[k], a1.v[k], a2.v[k], a3.v[k]);
     return o;
 }
 SBFT_DEV fe sel2(u32 j, const fe& a0, const fe& a1) {
@@ -289,6 +302,194 @@ SBFT_DEV bool x_matches_r(const jp& R, const fe& r) {
     return accept;
 }
 
+// ---- the same butterfly in radix-2^29 arithmetic (p256_f29.hpp), lean additions ----
+// A field product here is f29_mul_ilp: its 17 column sums are independent chains, so one
+// wavefront issues them back to back, where the 8 x 32 product above is one long carry chain
+// (~2,800 cycles per cooperative step against ~1,000). The additions have no case analysis
+// beyond infinity operands (digit-0 entries, selected around): P1 = +-P2 gives H = 0, hence
+// Z3 = 0, which every later level keeps; the kernel then re-runs the tuple on the exact
+// butterfly above. Limb bounds as in p29_add_jac_lean_i (p256_f29.hpp).
+#ifndef SBFT_KEYED_F29
+#define SBFT_KEYED_F29 1
+#endif
+__device__ __constant__ static const u32 C29_CONV256[9] = P256_F29_CONV256;
+
+template <int CTRL>
+SBFT_DEV f29 dpp29(const f29& a) {
+    f29 o;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) o.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)a.v[k], CTRL, 0xf, 0xf, false);
+    return o;
+}
+SBFT_DEV f29 sel2_29(bool j, const f29& a0, const f29& a1) {
+    f29 o;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) o.v[k] = j ? a1.v[k] : a0.v[k];
+    return o;
+}
+SBFT_DEV f29 sel4_29(u32 j, const f29& a0, const f29& a1, const f29& a2, const f29& a3) {
+    const bool b0 = (j & 1u) != 0, b1 = (j & 2u) != 0;
+    f29 o;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) o.v[k] = pick4(b0, b1, a0.v[k], a1.v[k], a2.v[k], a3.v[k]);
+    return o;
+}
+SBFT_DEV f29 shfl_xor29(const f29& a, int mask) {
+    f29 o;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) o.v[k] = shfl_xor_u32(a.v[k], mask);
+    return o;
+}
+SBFT_DEV void jp29_sel(jp29& out, bool c, const jp29& a) {
+    out.x = sel2_29(c, out.x, a.x);
+    out.y = sel2_29(c, out.y, a.y);
+    out.z = sel2_29(c, out.z, a.z);
+}
+
+// table entry (8 x 32 Montgomery, R = 2^256, canonical) -> affine f29 Montgomery (R = 2^261)
+SBFT_DEV void entry_to_f29(const fe& x, const fe& y, jp29& p) {
+    const f29 k = f29_const(C29_CONV256);  // 2^266 mod p
+    f29_mul_ilp(p.x, f29_from_u256(x), k);
+    f29_mul_ilp(p.y, f29_from_u256(y), k);
+    p.z = f29_const(C29_ONE);
+}
+
+// Level 0: affine P1 (even lane) + affine P2 (odd lane) on lane pairs, three product steps.
+SBFT_DEV void coop29_add_affine_pair(jp29& acc, bool& inf, u32 lane) {
+    const f29 ox = dpp29<0xB1>(acc.x), oy = dpp29<0xB1>(acc.y);  // quad_perm [1,0,3,2]
+    const bool oinf = __builtin_amdgcn_mov_dpp(inf ? 1 : 0, 0xB1, 0xf, 0xf, false) != 0;
+    const bool j = (lane & 1u) != 0;
+    jp29 p1, p2;
+    p1.x = sel2_29(j, acc.x, ox);
+    p1.y = sel2_29(j, acc.y, oy);
+    p2.x = sel2_29(j, ox, acc.x);
+    p2.y = sel2_29(j, oy, acc.y);
+    p1.z = p2.z = acc.z;  // ONE on every lane
+    const bool i1 = j ? oinf : inf, i2 = j ? inf : oinf;
+    f29 H, R, t, X3, VX, Y3;
+    f29_sub(H, p2.x, p1.x);  // |limb| < 2^29
+    f29_sub(R, p2.y, p1.y);
+    {
+        const f29 a = sel2_29(j, H, R);
+        f29_mul_ilp(t, a, a);  // HH | RR
+    }
+    const f29 HH = dpp29<PB0>(t), RR = dpp29<PB1>(t);
+    f29_mul_ilp(t, sel2_29(j, H, p1.x), HH);  // HHH | V = X1 HH
+    const f29 HHH = dpp29<PB0>(t), V = dpp29<PB1>(t);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] = RR.v[i] - HHH.v[i] - (V.v[i] << 1);  // (-3 2^29, 2^29)
+    f29_normalize(X3, t);
+    f29_sub(VX, V, X3);                                             // (-2^29.2, 2^29 + 2^26)
+    f29_mul_ilp(t, sel2_29(j, p1.y, R), sel2_29(j, HHH, VX));       // Y1 HHH | R (V - X3)
+    f29_sub(Y3, dpp29<PB1>(t), dpp29<PB0>(t));                      // N+-
+    jp29 out;
+    out.x = X3;
+    out.y = Y3;
+    out.z = H;
+    jp29_sel(out, i2, p1);
+    jp29_sel(out, i1, p2);
+    acc = out;
+    inf = i1 && i2;
+}
+
+// Levels >= 1: Jacobian P1 (lower half-group) + P2 (upper) on each quad, five product steps.
+SBFT_DEV void coop29_add_jac_quad(jp29& acc, bool& inf, u32 lane, int lvl) {
+    const int m = 1 << lvl;
+    jp29 o;
+    o.x = shfl_xor29(acc.x, m);
+    o.y = shfl_xor29(acc.y, m);
+    o.z = shfl_xor29(acc.z, m);
+    const bool oinf = shfl_xor_u32(inf ? 1u : 0u, m) != 0;
+    const bool hi = ((lane >> lvl) & 1u) != 0;
+    jp29 p1 = acc, p2 = o;
+    jp29_sel(p1, hi, o);
+    jp29_sel(p2, hi, acc);
+    const bool i1 = hi ? oinf : inf, i2 = hi ? inf : oinf;
+    const u32 j = lane & 3u;
+    f29 t, H, R, X3, VX, Y3;
+    // S1: A = Z1^2 (j0), B = Z2^2 (j1), C = Z1 Z2 (j2)
+    f29_mul_ilp(t, sel4_29(j, p1.z, p2.z, p1.z, p1.z), sel4_29(j, p1.z, p2.z, p2.z, p1.z));
+    const f29 A = dpp29<QB(0)>(t), B = dpp29<QB(1)>(t), C = dpp29<QB(2)>(t);
+    // S2: U1 = X1 B (j0), U2 = X2 A (j1), T1 = Z1 A (j2), T2 = Z2 B (j3)
+    f29_mul_ilp(t, sel4_29(j, p1.x, p2.x, p1.z, p2.z), sel4_29(j, B, A, A, B));
+    const f29 U1 = dpp29<QB(0)>(t), U2 = dpp29<QB(1)>(t), T1 = dpp29<QB(2)>(t), T2 = dpp29<QB(3)>(t);
+    f29_sub(H, U2, U1);  // N+-
+    // S3: S1 = Y1 T2 (j0), S2 = Y2 T1 (j1), Z3 = C H (j2), HH = H^2 (j3)
+    f29_mul_ilp(t, sel4_29(j, p1.y, p2.y, C, H), sel4_29(j, T2, T1, H, H));
+    const f29 S1 = dpp29<QB(0)>(t), S2 = dpp29<QB(1)>(t), Z3 = dpp29<QB(2)>(t), HH = dpp29<QB(3)>(t);
+    f29_sub(R, S2, S1);  // N+-
+    // S4: RR = R^2 (j0), HHH = H HH (j1), V = U1 HH (j2)
+    f29_mul_ilp(t, sel4_29(j, R, H, U1, R), sel4_29(j, R, HH, HH, R));
+    const f29 RR = dpp29<QB(0)>(t), HHH = dpp29<QB(1)>(t), V = dpp29<QB(2)>(t);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] = RR.v[i] - HHH.v[i] - (V.v[i] << 1);  // (-3 2^29, 2^29)
+    f29_normalize(X3, t);
+    f29_sub(VX, V, X3);  // (-2^29.2, 2^29 + 2^26)
+    // S5: S1 HHH (j0), R (V - X3) (j1)
+    f29_mul_ilp(t, sel2_29((j & 1u) != 0, S1, R), sel2_29((j & 1u) != 0, HHH, VX));
+    f29_sub(Y3, dpp29<QB(1)>(t), dpp29<QB(0)>(t));  // N+-
+    jp29 out;
+    out.x = X3;
+    out.y = Y3;
+    out.z = Z3;
+    jp29_sel(out, i2, p1);
+    jp29_sel(out, i1, p2);
+    acc = out;
+    inf = i1 && i2;
+}
+
+__device__ __constant__ static const u32 C29_P1[9] = P256_F29_P;
+__device__ __constant__ static const u32 C29_P3[9] = P256_F29_3P;
+
+// t == 0 (mod p) for an f29 product output (|t| < 2^256 + 2): t + 2p is one of p, 2p, 3p.
+SBFT_DEV bool f29_small_is_zero_modp(const f29& t) {
+    f29 u;
+    f29_add(u, t, f29_const(C29_2P));
+    f29_norm_chain(u, u);
+    bool e1 = true, e2 = true, e3 = true;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        e1 = e1 && u.v[k] == C29_P1[k];
+        e2 = e2 && u.v[k] == C29_2P[k];
+        e3 = e3 && u.v[k] == C29_P3[k];
+    }
+    return e1 || e2 || e3;
+}
+
+// The final check of the lean butterfly, spread over each quad (every lane holds R = acc):
+//   1: Z^2 | r R2 | (r + n) R2 | Z 1        2: r Z^2 | (r + n) Z^2 (Montgomery)
+//   3: (X - r Z^2) 1 | (X - (r + n) Z^2) 1, then each lane tests its value for 0 mod p.
+// exc: Z == 0 (an exceptional addition happened); the verdict: X == r Z^2, or X == (r + n) Z^2
+// when r + n < p. Both wave-uniform.
+SBFT_DEV bool keyed29_final(const jp29& acc, const fe& rv, u32 lane, bool& exc) {
+    fe rn;
+    u64 c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        c = (u64)rv.v[k] + P256_N[k] + c;
+        rn.v[k] = lo32(c);
+        c >>= 32;
+    }
+    const bool rn_ok = c == 0 && fe_lt(rn, P256_P);
+    const u32 j = lane & 3u;
+    const f29 r2 = f29_const(C29_R2);
+    f29 one;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) one.v[i] = i == 0 ? 1u : 0u;
+    f29 t;
+    f29_mul_ilp(t, sel4_29(j, acc.z, f29_from_u256(rv), f29_from_u256(rn), acc.z), sel4_29(j, acc.z, r2, r2, one));
+    const f29 z2 = dpp29<QB(0)>(t), rma = dpp29<QB(1)>(t), rmb = dpp29<QB(2)>(t), zt = dpp29<QB(3)>(t);
+    const bool odd = (j & 1u) != 0;
+    f29_mul_ilp(t, sel2_29(odd, rma, rmb), z2);  // r Z^2 | (r + n) Z^2
+    f29 d;
+    f29_sub(d, acc.x, t);                        // (-2^29 - 2^26, 2^29 + 2^26)
+    f29_mul_ilp(t, d, one);
+    const bool z = f29_small_is_zero_modp(t);
+    const bool za = __builtin_amdgcn_readlane(z ? 1 : 0, 0) != 0, zb = __builtin_amdgcn_readlane(z ? 1 : 0, 1) != 0;
+    exc = f29_small_is_zero_modp(zt);
+    return za || (rn_ok && zb);
+}
+
 // One wavefront per tuple. Digests come either precomputed (digest != null) or as messages
 // blob[off[t] .. +len[t]) hashed here (digest == null). key[t] indexes keytab (slot 0 is G's
 // table, so registered keys are 1 .. nkeys-1).
@@ -300,10 +501,12 @@ __global__ __launch_bounds__(128) void p256_verify_keyed_wave_kernel(
     const uint8_t* __restrict__ digest, const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint8_t* __restrict__ rr, const uint8_t* __restrict__ ss,
     const uint32_t* __restrict__ key, const uint4* const* __restrict__ keytab, uint32_t nkeys,
-    uint8_t* __restrict__ ok, uint32_t n) {
+    uint8_t* __restrict__ ok, uint32_t n, uint8_t mark) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     __shared__ u32 w_lds[8];
+    SBFT_KEYED_MARK(0);
     inv::stage_divstep_table(dtab);
+    SBFT_KEYED_MARK(1);
     const uint32_t t = blockIdx.x;
     const u32 lane = threadIdx.x & 63u;
     const u32 wave = threadIdx.x >> 6;
@@ -323,7 +526,8 @@ __global__ __launch_bounds__(128) void p256_verify_keyed_wave_kernel(
             sv = fe_zero();
             sv.v[0] = 1;
         }
-        inv::inv_mod_n(w.v, sv.v, dtab);
+        const fe rn = fe_const(C_ONEN);  // 2^256 mod n: w comes out in Montgomery form
+        inv::inv_mod_wave(w.v, sv.v, dtab, false, rn.v);
         if (lane == 0)
 #pragma unroll
             for (int k = 0; k < 8; ++k) w_lds[k] = w.v[k];
@@ -336,21 +540,22 @@ __global__ __launch_bounds__(128) void p256_verify_keyed_wave_kernel(
         for (int k = 0; k < 8; ++k) e_raw.v[k] = h[7 - k];
     }
     __syncthreads();
+    SBFT_KEYED_MARK(2);
     if (wave == 1) return;
-    fe w;
+    fe wm;  // s^-1 R mod n
 #pragma unroll
-    for (int k = 0; k < 8; ++k) w.v[k] = w_lds[k];
-    fe e, wm, u1, u2;
+    for (int k = 0; k < 8; ++k) wm.v[k] = w_lds[k];
+    // lanes 0-31 take the G windows of u1 = e s^-1, lanes 32-63 the Q windows of u2 = r s^-1:
+    // each lane needs one of the two products
+    fe e, u;
     fn_canon(e, e_raw);
-    fn_mul(wm, w, fe_const(C_R2N));  // w R
-    fn_mul(u1, e, wm);
-    fn_mul(u2, r, wm);
-    fn_canon(u1, u1);
-    fn_canon(u2, u2);
+    fn_mul(u, lane < 32 ? e : r, wm);
+    fn_canon(u, u);
+    SBFT_KEYED_MARK(3);
 
     // this lane's table point
     const u32 win = lane & 31u;
-    const u32 digit = byte_of(lane < 32 ? u1 : u2, win);
+    const u32 digit = byte_of(u, win);
     const uint4* tab = keytab[lane < 32 ? 0u : (valid ? kid : 0u)];
     const uint4* ent = tab + (size_t)(win * COMB_ENTRIES + digit) * COMB_ENTRY_U4;
     jp acc;
@@ -361,12 +566,34 @@ __global__ __launch_bounds__(128) void p256_verify_keyed_wave_kernel(
         acc.y = {{c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w}};
         acc.z = fe_const(C_ONEP);
     }
+    SBFT_KEYED_MARK(4);
     // butterfly: after level k every lane holds the sum of its aligned group of 2^(k+1) points
     // (the same representation on every lane of the group: the additions are cooperative)
-    coop_add_affine_pair(acc, inf, lane);
+    bool exact = !SBFT_KEYED_F29;
+    if (SBFT_KEYED_F29) {
+        jp29 a29;
+        entry_to_f29(acc.x, acc.y, a29);
+        bool inf29 = inf;
+        coop29_add_affine_pair(a29, inf29, lane);
+        SBFT_KEYED_MARK(5);
 #pragma unroll 1
-    for (int lvl = 1; lvl < 6; ++lvl) coop_add_jac_quad(acc, inf, lane, lvl);
-    if (lane == 0) ok[t] = (valid && !inf && x_matches_r(acc, r)) ? 1 : 0;
+        for (int lvl = 1; lvl < 6; ++lvl) coop29_add_jac_quad(a29, inf29, lane, lvl);
+        SBFT_KEYED_MARK(6);
+        bool exc = false;
+        const bool accept = keyed29_final(a29, r, lane, exc) && !inf29;
+        // every lane holds the same point: exc is wave-uniform
+        exact = __builtin_amdgcn_readfirstlane((!inf29 && exc) ? 1 : 0) != 0;
+        if (!exact && lane == 0) ok[t] = ((valid && accept) ? 1 : 0) | mark;
+    }
+    if (exact) {  // rare: an exceptional addition in the lean butterfly (or SBFT_KEYED_F29 0)
+        coop_add_affine_pair(acc, inf, lane);
+        SBFT_KEYED_MARK(5);
+#pragma unroll 1
+        for (int lvl = 1; lvl < 6; ++lvl) coop_add_jac_quad(acc, inf, lane, lvl);
+        SBFT_KEYED_MARK(6);
+        if (lane == 0) ok[t] = ((valid && !inf && x_matches_r(acc, r)) ? 1 : 0) | mark;
+    }
+    SBFT_KEYED_MARK(7);
 }
 
 // ---- latency-path signing (api.Signer: SignProposal at view.go:481, Sign at viewchanger.go:445)
@@ -491,10 +718,10 @@ extern "C" size_t sbft_comb_table_bytes(void) { return (size_t)COMB_KEY_U4 * 16;
 extern "C" int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint8_t* d_blob, const uint64_t* d_off,
                                              const uint32_t* d_len, const uint8_t* d_r, const uint8_t* d_s,
                                              const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
-                                             uint8_t* d_ok, uint32_t n, hipStream_t stream) {
+                                             uint8_t* d_ok, uint32_t n, uint8_t mark, hipStream_t stream) {
     if (n == 0) return 0;
     if (!d_digest && (!d_blob || !d_off || !d_len)) return -1;
     hipLaunchKernelGGL(sbft::p256_verify_keyed_wave_kernel, dim3(n), dim3(128), 0, stream, d_digest, d_blob, d_off,
-                       d_len, d_r, d_s, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n);
+                       d_len, d_r, d_s, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n, mark);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

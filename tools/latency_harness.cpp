@@ -10,6 +10,8 @@
 //       the last call returned. COALESCE_MAX <= 1 is the stock behaviour (a launch per call).
 //       Every 10th decision carries one bad signature (vote 7): its caller must get
 //       SBFT_V_EVERIFY with the reference's text, everyone else 0.
+//   quorum-batch VOTES DECISIONS
+//       the batch hook: one sbft_verifier_verify_consenter_sigs call per decision.
 //   quorum-cpu  CALLERS DECISIONS THREADS
 //       the same fan-out with the verify on the CPU: CALLERS votes verified by THREADS
 //       workers (one thread per vote when THREADS >= CALLERS), SHA-256(Msg) + ECDSA_do_verify
@@ -112,6 +114,64 @@ static void priv_of(uint64_t tag, uint8_t out[32]) {
     SHA256_Final(out, &c);
     out[0] &= 0x7f;
     out[31] |= 1;
+}
+
+// quorum-batch VOTES DECISIONS: the patched library's batch hook, one
+// sbft_verifier_verify_consenter_sigs call with all VOTES signatures per decision, from one
+// thread; 8 proposals in rotation (the digest memo misses every call). Latency = the call.
+static int quorum_batch(int votes, int decisions) {
+    sbft_gv_ctx* ctx = nullptr;
+    if (sbft_gv_init(nullptr, &ctx)) {
+        std::fprintf(stderr, "no GPU\n");
+        return 1;
+    }
+    sbft_verifier* v = sbft_verifier_new(ctx, 1);
+    std::vector<sbft_signer*> signers;
+    for (int i = 1; i <= votes; ++i) {
+        uint8_t d[32], pub[65];
+        priv_of(1000 + i, d);
+        signers.push_back(sbft_signer_new(ctx, i, d));
+        sbft_signer_public_key(signers.back(), pub);
+        sbft_verifier_add_consenter(v, i, pub);
+    }
+    const int NB = 8;
+    std::vector<std::string> payloads(NB);
+    std::vector<sbft_proposal> props(NB);
+    std::vector<std::vector<std::vector<uint8_t>>> msgs(NB), vals(NB);
+    std::vector<std::vector<sbft_signature>> sigs(NB);
+    for (int b = 0; b < NB; ++b) {
+        payloads[b] = std::string(1300, 'a' + b);
+        props[b] = sbft_proposal{(const uint8_t*)payloads[b].data(), payloads[b].size(), (const uint8_t*)"h", 1,
+                                 (const uint8_t*)"m", 1, 1};
+        for (int i = 0; i < votes; ++i) {
+            std::vector<uint8_t> m(256), sig(64);
+            size_t ml = 0;
+            sbft_signer_sign_proposal(signers[i], &props[b], nullptr, 0, m.data(), m.size(), &ml, sig.data());
+            m.resize(ml);
+            msgs[b].push_back(m);
+            vals[b].push_back(sig);
+        }
+        for (int i = 0; i < votes; ++i)
+            sigs[b].push_back(sbft_signature{(uint64_t)(i + 1), vals[b][i].data(), 64, msgs[b][i].data(), msgs[b][i].size()});
+    }
+    std::vector<int32_t> st(votes);
+    int wrong = 0;
+    std::vector<double> t;
+    for (int g = -5; g < decisions; ++g) {
+        const int b = (g + 8) % NB;
+        const auto t0 = Clock::now();
+        const int rc = sbft_verifier_verify_consenter_sigs(v, sigs[b].data(), votes, &props[b], st.data());
+        const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        if (g >= 0) t.push_back(us);
+        if (rc) wrong++;
+        for (int i = 0; i < votes; ++i) wrong += st[i] != 0;
+    }
+    std::printf("{\"mode\": \"quorum-batch\", \"votes\": %d, \"decisions\": %d, \"p50_ms\": %.4f, \"p99_ms\": %.4f, "
+                "\"wrong_verdicts\": %d}\n", votes, decisions, pct(t, 50) / 1e3, pct(t, 99) / 1e3, wrong);
+    for (auto* s : signers) sbft_signer_free(s);
+    sbft_verifier_free(v);
+    sbft_gv_destroy(ctx);
+    return wrong ? 2 : 0;
 }
 
 static int quorum_gpu(int callers, int decisions, int cmax, int cwait) {
@@ -275,12 +335,13 @@ static int proposal_cpu(int requests, int decisions, int threads) {
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-cpu|proposal-cpu ...\n", argv[0]);
+        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-cpu|proposal-cpu ...\n", argv[0]);
         return 1;
     }
     const std::string mode = argv[1];
     auto arg = [&](int i, int def) { return argc > i ? std::atoi(argv[i]) : def; };
     if (mode == "quorum-gpu") return quorum_gpu(arg(2, 66), arg(3, 200), arg(4, 0), arg(5, 0));
+    if (mode == "quorum-batch") return quorum_batch(arg(2, 67), arg(3, 200));
     if (mode == "quorum-cpu") return quorum_cpu(arg(2, 66), arg(3, 200), arg(4, 66));
     if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
     std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
