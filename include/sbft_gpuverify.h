@@ -161,8 +161,10 @@ int sbft_gv_sha256_verify_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_b
 /* Batched key derivation + ECDSA signing with caller-supplied nonces (the api.Signer side,
  * pkg/api/dependencies.go:46-52; also the synthetic-workload generator). For each k:
  * Q = d*G (qx, qy), r = x(k*G) mod n, s = k^-1 (digest + r d) mod n; status[k] = 1 on
- * success, 0 if d or k is outside [1, n-1] or r or s came out 0. Nonces must be secret and
- * unique per key (RFC 6979 or a CSPRNG) — the engine does not generate them. */
+ * success, 0 if d or k is outside [1, n-1] or r or s came out 0. qx = qy = NULL skips the key
+ * derivation (a signer that knows its public key; the latency path then runs one scalar
+ * multiplication instead of two). Nonces must be secret and unique per key (RFC 6979 or a
+ * CSPRNG) — the engine does not generate them. */
 int sbft_gv_sign_p256(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_t* digest,
                       size_t n, uint8_t* qx, uint8_t* qy, uint8_t* r, uint8_t* s, uint8_t* status);
 int sbft_gv_sign_p256_dev(sbft_gv_ctx* ctx, int device, const void* d_d, const void* d_k,

@@ -925,10 +925,16 @@ int sbft_gv_sign_p256(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, cons
                       size_t n, uint8_t* qx, uint8_t* qy, uint8_t* r, uint8_t* s, uint8_t* status) {
     if (!ctx) return SBFT_GV_EINVAL;
     if (n == 0) return SBFT_GV_OK;
-    if (!d || !k || !digest || !qx || !qy || !r || !s || !status || n > 0xffffffffu) return SBFT_GV_EINVAL;
-    // latency path (api.Signer: one signature per call): a wavefront per signature over G's comb
-    // table instead of one lane running two scalar multiplications alone
+    if (!d || !k || !digest || !r || !s || !status || !qx != !qy || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    // latency path (api.Signer: one signature per call): two wavefronts per signature over G's
+    // comb table instead of one lane running two scalar multiplications alone
     if (n <= kSignWaveMax) return sign_wave(ctx, d, k, digest, n, qx, qy, r, s, status);
+    std::vector<uint8_t> qtmp;  // the one-lane kernel always derives Q
+    if (!qx) {
+        qtmp.resize(64 * n);
+        qx = qtmp.data();
+        qy = qtmp.data() + 32 * n;
+    }
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
         return enqueue_sign(c, d, k, digest, qx, qy, r, s, status);
     });
@@ -1000,22 +1006,43 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     std::vector<uint32_t>& len = len_tl;
     off.clear();
     len.clear();
+    static const bool trace = getenv("SBFT_VP_TRACE") != nullptr;  // diagnostics
+    using TC = std::chrono::steady_clock;
+    const auto t0 = TC::now();
     Slot* sl = ctx->slots[ctx->rr.fetch_add(1) % ctx->slots.size()];
     std::unique_lock<std::mutex> lk(sl->mu);
     HIPCHK(hipSetDevice(sl->device));
     int rc = sl->reserve_blob(blob_len + SBFT_GV_SHA_BLOB_PAD);  // + the hash kernel's over-read
     if (rc) return rc;
-    // the parse runs on the helper while this thread stages the payload for the DMA
-    int prc = 0;
-    const bool async = ctx->helper.try_submit([&] { prc = prepare(off, len); });
-    const hipError_t ce =
-        blob_len ? hipMemcpyAsync(sl->bbuf, blob, blob_len, hipMemcpyHostToDevice, sl->stream) : hipSuccess;
-    if (async)
-        ctx->helper.wait();
-    else
-        prc = prepare(off, len);
+    // the helper stages the payload for the DMA (a pageable copy runs on the CPU) while this
+    // thread parses: the parse is a chain of dependent loads through the payload, fastest on
+    // the caller's core, whose caches typically hold it; the copy streams it from anywhere
+    hipError_t ce = hipSuccess;
+    const int dev = sl->device;
+    auto copy = [&] {
+        if (blob_len && (ce = hipSetDevice(dev)) == hipSuccess)
+            ce = hipMemcpyAsync(sl->bbuf, blob, blob_len, hipMemcpyHostToDevice, sl->stream);
+    };
+    const bool async = ctx->helper.try_submit(copy);
+    if (!async) copy();
+    const auto t1 = TC::now();
+    const int prc = prepare(off, len);
+    const auto t2 = TC::now();
+    if (async) ctx->helper.wait();
     const int sync_rc = hipStreamSynchronize(sl->stream) == hipSuccess && ce == hipSuccess ? SBFT_GV_OK
                                                                                            : SBFT_GV_EDEVICE;
+    const auto t3 = TC::now();
+    struct Tr {
+        bool on;
+        TC::time_point a, b, c, d;
+        bool async;
+        ~Tr() {
+            if (!on) return;
+            auto us = [](TC::time_point x, TC::time_point y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
+            fprintf(stderr, "vp async=%d submit=%.1f parse=%.1f copy_wait_sync=%.1f rest=%.1f us\n", (int)async, us(a, b),
+                    us(b, c), us(c, d), us(d, TC::now()));
+        }
+    } tr{trace, t0, t1, t2, t3, async};
     if (prc) return prc;
     if (sync_rc) return sync_rc;
     const size_t n = off.size();
@@ -1486,14 +1513,17 @@ int sign_wave(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_
     uint8_t* b = sl->dbuf;
     HIPCHK(hipMemcpyAsync(b, h, in_bytes, hipMemcpyHostToDevice, sl->stream));
     uint8_t* o = b + in_bytes;
-    if (sbft_launch_p256_sign_wave(b, b + f, b + 2 * f, (const void* const*)sl->d_keytab, o, o + f, o + 2 * f,
-                                   o + 3 * f, o + 4 * f, (uint32_t)n, sl->stream))
+    const bool want_q = qx != nullptr;
+    if (sbft_launch_p256_sign_wave(b, b + f, b + 2 * f, (const void* const*)sl->d_keytab, want_q ? o : nullptr,
+                                   want_q ? o + f : nullptr, o + 2 * f, o + 3 * f, o + 4 * f, (uint32_t)n, sl->stream))
         return SBFT_GV_ELAUNCH;
     HIPCHK(hipMemcpyAsync(h + in_bytes, o, out_bytes, hipMemcpyDeviceToHost, sl->stream));
     HIPCHK(hipStreamSynchronize(sl->stream));
     const uint8_t* ho = h + in_bytes;
-    std::memcpy(qx, ho, 32 * n);
-    std::memcpy(qy, ho + f, 32 * n);
+    if (want_q) {
+        std::memcpy(qx, ho, 32 * n);
+        std::memcpy(qy, ho + f, 32 * n);
+    }
     std::memcpy(r, ho + 2 * f, 32 * n);
     std::memcpy(s, ho + 3 * f, 32 * n);
     std::memcpy(status, ho + 4 * f, n);

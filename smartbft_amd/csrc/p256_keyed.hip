@@ -597,92 +597,109 @@ __global__ __launch_bounds__(128) void p256_verify_keyed_wave_kernel(
 }
 
 // ---- latency-path signing (api.Signer: SignProposal at view.go:481, Sign at viewchanger.go:445)
-// One wavefront per signature over G's comb table (keytab slot 0): R = k G from 32 table points
-// and the cooperative butterfly (no doublings), then r = x(R) mod n and s = k^-1 (e + r d) mod n
-// with safegcd inversions. Same outputs and status as p256_sign_kernel (Q = d G, r, s), which
-// keeps the throughput path (one signature per lane, bench workload generation).
-SBFT_DEV void affine_x_y(const jp& R, fe& x, fe& y, const uint32_t* dtab) {
-    // R.z is Montgomery (z R); its inverse as a plain number is z^-1 R^-1, and two
-    // multiplications by R^2 give z^-1 R (Montgomery form of z^-1)
-    fe zc, zi, zi2, zi3, t;
-    fp_canon(zc, R.z);
-    inv::inv_mod_p(zi.v, zc.v, dtab);
-    const fe r2p = fe_const(C_R2P);
-    fp_mul(zi, zi, r2p);
-    fp_mul(zi, zi, r2p);
-    fp_sqr(zi2, zi);
-    fp_mul(zi3, zi2, zi);
-    const fe one_plain = {{1, 0, 0, 0, 0, 0, 0, 0}};
-    fp_mul(t, R.x, zi2);
-    fp_mul(t, t, one_plain);
-    fp_canon(x, t);
-    fp_mul(t, R.y, zi3);
-    fp_mul(t, t, one_plain);
-    fp_canon(y, t);
-}
+// Two wavefronts per signature over G's comb table (keytab slot 0). Wave 1 inverts k (mod n,
+// scaled to Montgomery form) while wave 0 computes R = k G from 32 table points with the lean
+// radix-2^29 butterfly above and makes it affine (one wave-wide inversion mod p); they meet at
+// one barrier for s = k^-1 (e + r d). Q = d G (same butterfly, a second inversion) only when
+// the caller asks for it (qx_out != null): a signer derives its key once. The lean additions
+// never meet an exceptional case here: every partial sum of the butterfly is a multiple
+// 0 < m < k < n of G over disjoint windows, so two of them never coincide or cancel (a Z = 0
+// would only mark the signature failed, which the caller retries with another nonce). Same
+// outputs and status as p256_sign_kernel (one signature per lane, bench workload generation).
 
-// k G on the whole wavefront (every lane returns it); inf set if k G = infinity (k = 0)
-SBFT_DEV void wave_mul_g(jp& acc, bool& inf, const fe& k, const uint4* gtab, u32 lane) {
+// k G on the whole wavefront (lanes < 32: window `lane` of k; lanes >= 32 add nothing)
+SBFT_DEV void wave29_mul_g(jp29& acc, bool& inf, const fe& k, const uint4* gtab, u32 lane) {
     const u32 win = lane & 31u;
     const u32 digit = lane < 32 ? byte_of(k, win) : 0u;
     const uint4* ent = gtab + (size_t)(win * COMB_ENTRIES + digit) * COMB_ENTRY_U4;
     inf = digit == 0;
-    {
-        const uint4 a = ent[0], b = ent[1], c = ent[2], d = ent[3];
-        acc.x = {{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
-        acc.y = {{c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w}};
-        acc.z = fe_const(C_ONEP);
-    }
-    coop_add_affine_pair(acc, inf, lane);
+    const uint4 a = ent[0], b = ent[1], c = ent[2], d = ent[3];
+    const fe x = {{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+    const fe y = {{c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w}};
+    entry_to_f29(x, y, acc);
+    coop29_add_affine_pair(acc, inf, lane);
 #pragma unroll 1
-    for (int lvl = 1; lvl < 6; ++lvl) coop_add_jac_quad(acc, inf, lane, lvl);
+    for (int lvl = 1; lvl < 6; ++lvl) coop29_add_jac_quad(acc, inf, lane, lvl);
 }
 
-__global__ __launch_bounds__(64) void p256_sign_wave_kernel(const uint8_t* __restrict__ dd, const uint8_t* __restrict__ kk,
-                                                            const uint8_t* __restrict__ ee, const uint4* const* __restrict__ keytab,
-                                                            uint8_t* __restrict__ qx_out, uint8_t* __restrict__ qy_out,
-                                                            uint8_t* __restrict__ r_out, uint8_t* __restrict__ s_out,
-                                                            uint8_t* __restrict__ status, uint32_t n) {
+// Affine coordinates (plain, canonical) of a Jacobian f29 point; bad when Z == 0.
+SBFT_DEV void affine29(const jp29& p, fe& x, fe* y, bool& bad, const uint32_t* dtab) {
+    const fe zc = f29_canon_plain(p.z);
+    bad = fe_is_zero_raw(zc);
+    fe zi;
+    inv::inv_mod_wave(zi.v, zc.v, dtab, true);  // plain Z^-1 (0 for Z == 0)
+    f29 zm, z2, t;
+    f29_mul_ilp(zm, f29_from_u256(zi), f29_const(C29_R2));  // Montgomery form
+    f29_mul_ilp(z2, zm, zm);
+    f29_mul_ilp(t, p.x, z2);
+    x = f29_canon_plain(t);
+    if (y) {
+        f29 z3;
+        f29_mul_ilp(z3, z2, zm);
+        f29_mul_ilp(t, p.y, z3);
+        *y = f29_canon_plain(t);
+    }
+}
+
+__global__ __launch_bounds__(128) void p256_sign_wave_kernel(const uint8_t* __restrict__ dd, const uint8_t* __restrict__ kk,
+                                                             const uint8_t* __restrict__ ee, const uint4* const* __restrict__ keytab,
+                                                             uint8_t* __restrict__ qx_out, uint8_t* __restrict__ qy_out,
+                                                             uint8_t* __restrict__ r_out, uint8_t* __restrict__ s_out,
+                                                             uint8_t* __restrict__ status, uint32_t n) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    __shared__ u32 kinv_lds[8];
     inv::stage_divstep_table(dtab);
     const uint32_t t = blockIdx.x;
-    const u32 lane = threadIdx.x;
-    if (t >= n) return;  // uniform per wave
-    const fe d = load_be32(dd + 32ull * t), k = load_be32(kk + 32ull * t), e_raw = load_be32(ee + 32ull * t);
+    const u32 lane = threadIdx.x & 63u;
+    const u32 wave = threadIdx.x >> 6;
+    if (t >= n) return;  // uniform per workgroup
+    const fe d = load_be32(dd + 32ull * t), k = load_be32(kk + 32ull * t);
     bool ok = !fe_is_zero_raw(d) && fe_lt(d, P256_N) && !fe_is_zero_raw(k) && fe_lt(k, P256_N);
-    const uint4* gtab = keytab[0];
-    jp P;
-    bool inf;
-    fe x, y;
-    // Q = d G (the public key) and R = k G
-    wave_mul_g(P, inf, d, gtab, lane);
-    affine_x_y(P, x, y, dtab);
-    if (lane == 0) {
-        store_be32(qx_out + 32ull * t, x);
-        store_be32(qy_out + 32ull * t, y);
-    }
-    wave_mul_g(P, inf, k, gtab, lane);
-    ok = ok && !inf;
-    affine_x_y(P, x, y, dtab);
-    fe r, e;
-    fn_canon(r, x);  // x < p < 2n
-    fn_canon(e, e_raw);
-    fe kinv, km, dm, rd, sum, sv;
-    {
+    fe r;
+    if (wave == 1) {
         fe kv = k;
         if (!ok) {
             kv = fe_zero();
             kv.v[0] = 1;
         }
-        inv::inv_mod_n(kinv.v, kv.v, dtab);  // plain k^-1
+        const fe rn = fe_const(C_ONEN);
+        fe kinv;
+        inv::inv_mod_wave(kinv.v, kv.v, dtab, false, rn.v);  // k^-1 R mod n
+        if (lane == 0)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) kinv_lds[i] = kinv.v[i];
+    } else {
+        const uint4* gtab = keytab[0];
+        jp29 P;
+        bool inf, bad;
+        fe x;
+        if (qx_out) {  // Q = d G (the public key)
+            fe y;
+            wave29_mul_g(P, inf, d, gtab, lane);
+            affine29(P, x, &y, bad, dtab);
+            if (lane == 0) {
+                store_be32(qx_out + 32ull * t, x);
+                store_be32(qy_out + 32ull * t, y);
+            }
+        }
+        wave29_mul_g(P, inf, k, gtab, lane);  // R = k G
+        affine29(P, x, nullptr, bad, dtab);
+        ok = ok && !inf && !bad;
+        fn_canon(r, x);  // x < p < 2n
     }
-    const fe r2n = fe_const(C_R2N);
-    fn_mul(dm, d, r2n);          // d R
-    fn_mul(rd, r, dm);           // r d (plain, lazily reduced)
+    __syncthreads();
+    if (wave == 1) return;
+    fe kinv;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kinv.v[i] = kinv_lds[i];
+    const fe e_raw = load_be32(ee + 32ull * t);
+    fe e, dm, rd, sum, sv;
+    fn_canon(e, e_raw);
+    fn_mul(dm, d, fe_const(C_R2N));  // d R
+    fn_mul(rd, r, dm);               // r d (plain, lazily reduced)
     fn_canon(rd, rd);
-    fn_add(sum, e, rd);          // e + r d mod n
-    fn_mul(km, kinv, r2n);       // k^-1 R
-    fn_mul(sv, sum, km);         // (e + r d) k^-1 (plain)
+    fn_add(sum, e, rd);              // e + r d mod n
+    fn_mul(sv, sum, kinv);           // (e + r d) k^-1 (plain)
     fn_canon(sv, sv);
     ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(sv);
     if (lane == 0) {
@@ -698,7 +715,7 @@ extern "C" int sbft_launch_p256_sign_wave(const uint8_t* d_d, const uint8_t* d_k
                                           const void* const* d_keytab, uint8_t* d_qx, uint8_t* d_qy, uint8_t* d_r,
                                           uint8_t* d_s, uint8_t* d_status, uint32_t n, hipStream_t stream) {
     if (n == 0) return 0;
-    hipLaunchKernelGGL(sbft::p256_sign_wave_kernel, dim3(n), dim3(64), 0, stream, d_d, d_k, d_e,
+    hipLaunchKernelGGL(sbft::p256_sign_wave_kernel, dim3(n), dim3(128), 0, stream, d_d, d_k, d_e,
                        (const uint4* const*)d_keytab, d_qx, d_qy, d_r, d_s, d_status, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

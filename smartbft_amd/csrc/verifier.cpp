@@ -13,6 +13,8 @@
 
 #include <array>
 #include <atomic>
+#include <thread>
+#include <functional>
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
@@ -383,6 +385,7 @@ bool parse_payload(const uint8_t* p, size_t len, std::vector<Req>& out) {
     for (uint32_t i = 0; i < count; ++i) {
         uint32_t l;
         const uint8_t* q;
+        __builtin_prefetch(p + r.pos + 2048);  // keep the chain of length prefixes in L1
         if (!r.u32(l)) return false;
         const size_t at = r.pos;
         if (!r.take(l, q)) return false;
@@ -1466,9 +1469,9 @@ int sbft_signer_sign(sbft_signer* s, const uint8_t* data, size_t len, uint8_t si
     uint8_t e[32];
     sha256(data ? data : (const uint8_t*)"", len, e);
     for (int attempt = 0; attempt < 8; ++attempt) {
-        uint8_t k[32], qx[32], qy[32], st = 0;
+        uint8_t k[32], st = 0;
         rfc6979_nonce(s->d, e, attempt, k);
-        const int rc = sbft_gv_sign_p256(s->ctx, s->d, k, e, 1, qx, qy, sig64, sig64 + 32, &st);
+        const int rc = sbft_gv_sign_p256(s->ctx, s->d, k, e, 1, nullptr, nullptr, sig64, sig64 + 32, &st);
         if (rc) return rc;
         if (st) return 0;
     }
