@@ -278,6 +278,17 @@ def latency_configs(gv, calls: int):
     out["commit_quorum_n100"] = {"p50_ms": p50, "p99_ms": p99, "calls": calls, "signatures": q,
                                  "python_wrapper_p50_ms": _pcts(tp)[0],
                                  "path": "sbft_verifier_verify_consenter_sigs (C ABI), host buffers"}
+    # the same hook timed in C (no ctypes), 8 proposals in rotation (the digest memo misses)
+    qb = _harness("quorum-batch", q, calls)
+    if qb:
+        assert qb["wrong_verdicts"] == 0
+        out["commit_quorum_n100"]["c_harness"] = qb
+    # SignProposal's signing (view.go:481), one message at a time: the GPU signer against
+    # OpenSSL ECDSA_do_sign on one core
+    sg = _harness("sign", calls)
+    if sg:
+        assert sg["failures"] == 0
+        out["sign_one"] = sg
     # the unmodified library: 66 goroutines (view.go:537-541), one VerifyConsenterSig each
     # (:834), released together per decision (tools/latency_harness quorum-gpu); stock = one
     # launch per call, coalesced = sbft_verifier_coalesce_consenter_sigs(66, 50 us)

@@ -55,6 +55,16 @@ func (sg *Signer) Close() {
 	runtime.SetFinalizer(sg, nil)
 }
 
+// Presign turns on the pre-signature pool (include/sbft_verifier.h sbft_signer_presign):
+// randomized nonces whose r, k^-1 and k^-1 r d the GPU computes `pool` at a time, so Sign and
+// SignProposal cost one host product and no launch. 0 returns to RFC 6979 nonces.
+func (sg *Signer) Presign(pool int) error {
+	if rc := C.sbft_signer_presign(sg.s, C.size_t(pool)); rc != 0 {
+		return fmt.Errorf("gpuverify: presign: %s", C.GoString(C.sbft_gv_strerror(rc)))
+	}
+	return nil
+}
+
 // PublicKey returns the 65-byte SEC1 uncompressed public key.
 func (sg *Signer) PublicKey() []byte {
 	out := make([]byte, 65)

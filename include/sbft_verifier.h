@@ -140,6 +140,13 @@ void sbft_signer_free(sbft_signer* s);
 int sbft_signer_public_key(const sbft_signer* s, uint8_t pubkey65[65]);
 /* Signer.Sign: 64-byte r||s over SHA-256(data). */
 int sbft_signer_sign(sbft_signer* s, const uint8_t* data, size_t len, uint8_t sig64[64]);
+/* Pre-signature pool (off by default). With pool > 0 the signer draws random nonces k from
+ * the kernel's CSPRNG (getrandom) and has the GPU compute, for `pool` nonces per launch,
+ * r = x(kG) mod n, A = k^-1 and B = k^-1 r d (mod n); a signature then costs the host
+ * s = A e + B (mod n) and no launch, and the pool refills (one launch) when it runs out.
+ * Signatures become randomized instead of RFC 6979-deterministic; each nonce is used once and
+ * then erased. pool = 0 returns to RFC 6979 nonces, one launch per signature. */
+int sbft_signer_presign(sbft_signer* s, size_t pool);
 /* Signer.SignProposal: builds Msg = "SBC1"|digest|aux into msg (msg_cap) and signs it. */
 int sbft_signer_sign_proposal(sbft_signer* s, const sbft_proposal* p, const uint8_t* aux, size_t aux_len,
                               uint8_t* msg, size_t msg_cap, size_t* msg_len, uint8_t sig64[64]);

@@ -7,6 +7,7 @@
 // the structure-of-arrays batches; there is no CPU verification path.
 #include "../../include/sbft_verifier.h"
 #include "engine_internal.h"
+#include "modn_host.hpp"
 
 #include <cpuid.h>
 #include <immintrin.h>
@@ -30,6 +31,7 @@
 
 #include <climits>
 #include <linux/futex.h>
+#include <sys/random.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -321,19 +323,29 @@ ProposalScratch& proposal_scratch() {
 // briefly, then sleep on a futex; the leader's wake-up does not make them re-acquire a mutex
 // one after another (a condition variable's notify_all does: ~3-4 us per follower, 0.25 ms
 // for a 66-vote quorum).
+// The wake-up is a tree: set() wakes two sleepers and every sleeper that wakes wakes two more.
+// One FUTEX_WAKE of all 65 followers of a commit quorum runs their 65 wake-ups one after
+// another inside the leader's system call (~80 us); the tree spreads them over the cores.
 struct DoneFlag {
     std::atomic<int> v{0};
+    void wake2() { syscall(SYS_futex, reinterpret_cast<int*>(&v), FUTEX_WAKE_PRIVATE, 2, nullptr, nullptr, 0); }
     void set() {
         v.store(1, std::memory_order_release);
-        syscall(SYS_futex, reinterpret_cast<int*>(&v), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+        wake2();
     }
-    void wait() {
-        for (int i = 0; i < 256; ++i) {
+    // spin: pause iterations before sleeping (0 when the wait is known to be long: a follower
+    // spinning on a busy host only delays the callers that still have to arrive)
+    void wait(int spin = 256) {
+        for (int i = 0; i < spin; ++i) {
             if (v.load(std::memory_order_acquire)) return;
             __builtin_ia32_pause();
         }
-        while (!v.load(std::memory_order_acquire))
+        bool slept = false;
+        while (!v.load(std::memory_order_acquire)) {
             syscall(SYS_futex, reinterpret_cast<int*>(&v), FUTEX_WAIT_PRIVATE, 0, nullptr, nullptr, 0);
+            slept = true;
+        }
+        if (slept) wake2();
     }
 };
 
@@ -537,10 +549,11 @@ struct sbft_verifier {
     };
     struct CsBatch {
         std::vector<CsEntry*> entries;
-        bool closed = false;
+        bool closed = false;  // no more entries (full, or the leader's window ended)
         int rc = 0;
-        std::condition_variable cv;  // wakes the leader when the batch fills
-        DoneFlag done;               // wakes the followers when the results are published
+        std::chrono::steady_clock::time_point t_open;  // the leader's arrival
+        std::condition_variable cv;                    // wakes the leader when the batch fills
+        DoneFlag done;                                 // wakes the followers when the results are published
     };
     std::mutex cs_mu;
     std::shared_ptr<CsBatch> cs_open;
@@ -1043,6 +1056,7 @@ static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const 
         std::unique_lock<std::mutex> g(v->cs_mu);
         if (!v->cs_open) {
             v->cs_open = std::make_shared<Batch>();
+            v->cs_open->t_open = std::chrono::steady_clock::now();
             leader = true;
         }
         batch = v->cs_open;
@@ -1053,15 +1067,19 @@ static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const 
             batch->cv.notify_all();  // wakes the leader early
         }
         if (leader) {
-            batch->cv.wait_until(g, std::chrono::steady_clock::now() + v->cs_wait, [&] { return batch->closed; });
+            // a sleep, not a spin: with more callers than cores a spinning leader delays the
+            // arrivals it waits for (the timed wait also oversleeps by the kernel's timer slack)
+            batch->cv.wait_until(g, batch->t_open + v->cs_wait, [&] { return batch->closed; });
             if (!batch->closed) {
                 batch->closed = true;
                 v->cs_open.reset();
             }
         }
     }
-    if (!leader) batch->done.wait();
+    if (!leader) batch->done.wait(0);  // the batch is one launch away: sleep at once
     if (leader) {
+        static const bool trace = getenv("SBFT_CS_TRACE") != nullptr;  // diagnostics
+        const auto tc = std::chrono::steady_clock::now();
         // closed: nobody else touches the entries until done is published
         const size_t n = batch->entries.size();
         std::vector<sbft_signature> sigs(n);
@@ -1081,6 +1099,10 @@ static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const 
         }
         batch->rc = rc;
         batch->done.set();
+        if (trace)
+            fprintf(stderr, "cs n=%zu gather=%.1f batch=%.1f us\n", n,
+                    std::chrono::duration<double, std::micro>(tc - batch->t_open).count(),
+                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc).count());
     }
     st = me.status;
     why = std::move(me.why);
@@ -1438,7 +1460,71 @@ struct sbft_signer {
     uint64_t id;
     uint8_t d[32];
     uint8_t qx[32], qy[32];
+    // pre-signature pool (sbft_signer_presign): r and the mod-n factors A = k^-1, B = k^-1 r d
+    struct Presig {
+        uint8_t r[32];
+        sbft::modn::u64 a[4], b[4];
+    };
+    std::mutex pool_mu;
+    std::vector<Presig> pool;
+    size_t pool_size = 0;
+    ~sbft_signer() {
+        std::memset(d, 0, sizeof d);
+        for (Presig& p : pool) std::memset(&p, 0, sizeof p);
+    }
 };
+
+// One launch of 2m signatures over m fresh random nonces: tuple 2i signs e = 0 (s = k^-1 r d
+// = B), tuple 2i+1 signs e = 1 (s = k^-1 (1 + r d) = A + B), so A = s(2i+1) - s(2i). Caller
+// holds pool_mu.
+static int presign_refill(sbft_signer* s, size_t m) {
+    std::vector<uint8_t> dd(64 * m), kk(64 * m), ee(64 * m, 0), r(64 * m), sv(64 * m), st(2 * m);
+    for (size_t i = 0; i < m; ++i) {
+        uint8_t k[32];
+        do {  // rejection sampling: 0 < k < n
+            size_t got = 0;
+            while (got < 32) {
+                const ssize_t g = getrandom(k + got, 32 - got, 0);
+                if (g <= 0) return SBFT_GV_EDEVICE;
+                got += (size_t)g;
+            }
+        } while (is_zero32(k) || cmp_be32(k, N_BE) >= 0);
+        for (int t = 0; t < 2; ++t) {
+            std::memcpy(&dd[32 * (2 * i + t)], s->d, 32);
+            std::memcpy(&kk[32 * (2 * i + t)], k, 32);
+        }
+        ee[32 * (2 * i + 1) + 31] = 1;
+        std::memset(k, 0, sizeof k);
+    }
+    const int rc = sbft_gv_sign_p256(s->ctx, dd.data(), kk.data(), ee.data(), 2 * m, nullptr, nullptr, r.data(),
+                                     sv.data(), st.data());
+    std::memset(kk.data(), 0, kk.size());
+    std::memset(dd.data(), 0, dd.size());
+    if (rc) return rc;
+    for (size_t i = 0; i < m; ++i) {
+        if (!st[2 * i] || !st[2 * i + 1]) continue;  // s came out 0 for this nonce: skip it
+        sbft_signer::Presig p;
+        std::memcpy(p.r, &r[32 * 2 * i], 32);
+        sbft::modn::u64 s0[4], s1[4], neg[4] = {0, 0, 0, 0};
+        sbft::modn::from_be32(s0, &sv[32 * 2 * i]);
+        sbft::modn::from_be32(s1, &sv[32 * (2 * i + 1)]);
+        // A = s1 - s0 = s1 + (n - s0)
+        if (!sbft::modn::is_zero(s0)) {
+            std::memcpy(neg, sbft::modn::N, sizeof neg);
+            sbft::modn::u64 bw = 0;
+            for (int j = 0; j < 4; ++j) {
+                const unsigned __int128 dlt = (unsigned __int128)neg[j] - s0[j] - bw;
+                neg[j] = (sbft::modn::u64)dlt;
+                bw = (sbft::modn::u64)(dlt >> 64) & 1u;
+            }
+        }
+        sbft::modn::add_mod(p.a, s1, neg);
+        std::memcpy(p.b, s0, sizeof s0);
+        s->pool.push_back(p);
+    }
+    std::memset(sv.data(), 0, sv.size());
+    return 0;
+}
 
 sbft_signer* sbft_signer_new(sbft_gv_ctx* ctx, uint64_t id, const uint8_t priv32[32]) {
     if (!ctx || !priv32 || is_zero32(priv32) || cmp_be32(priv32, N_BE) >= 0) return nullptr;
@@ -1464,10 +1550,44 @@ int sbft_signer_public_key(const sbft_signer* s, uint8_t pubkey65[65]) {
     return 0;
 }
 
+int sbft_signer_presign(sbft_signer* s, size_t pool) {
+    if (!s || pool > (1u << 20)) return SBFT_GV_EINVAL;
+    std::lock_guard<std::mutex> g(s->pool_mu);
+    s->pool_size = pool;
+    for (auto& p : s->pool) std::memset(&p, 0, sizeof p);
+    s->pool.clear();
+    return pool ? presign_refill(s, pool) : 0;
+}
+
 int sbft_signer_sign(sbft_signer* s, const uint8_t* data, size_t len, uint8_t sig64[64]) {
     if (!s || (!data && len) || !sig64) return SBFT_GV_EINVAL;
     uint8_t e[32];
     sha256(data ? data : (const uint8_t*)"", len, e);
+    {
+        std::lock_guard<std::mutex> g(s->pool_mu);
+        while (s->pool_size) {  // pooled: s = A e + B (mod n), no launch
+            if (s->pool.empty()) {
+                const int rc = presign_refill(s, s->pool_size);
+                if (rc) return rc;
+                if (s->pool.empty()) return SBFT_V_EVERIFY;
+            }
+            sbft_signer::Presig p = s->pool.back();
+            std::memset(&s->pool.back(), 0, sizeof p);
+            s->pool.pop_back();
+            sbft::modn::u64 ev[4], t[4], sg[4];
+            sbft::modn::from_be32(ev, e);
+            sbft::modn::mul_mod(t, p.a, ev);
+            sbft::modn::add_mod(sg, t, p.b);
+            const bool zero = sbft::modn::is_zero(sg);
+            if (!zero) {
+                std::memcpy(sig64, p.r, 32);
+                sbft::modn::to_be32(sig64 + 32, sg);
+            }
+            std::memset(&p, 0, sizeof p);
+            if (zero) continue;  // s = 0: take the next nonce
+            return 0;
+        }
+    }
     for (int attempt = 0; attempt < 8; ++attempt) {
         uint8_t k[32], st = 0;
         rfc6979_nonce(s->d, e, attempt, k);

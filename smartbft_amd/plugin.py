@@ -145,6 +145,7 @@ def _lib():
     L.sbft_signer_free.restype = None
     L.sbft_signer_public_key.argtypes = [_vp, _u8p]
     L.sbft_signer_sign.argtypes = [_vp, _u8p, ctypes.c_size_t, _u8p]
+    L.sbft_signer_presign.argtypes = [_vp, ctypes.c_size_t]
     L.sbft_signer_sign_proposal.argtypes = [_vp, P, _u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t, sz, _u8p]
     L.sbft_make_request.restype = ctypes.c_int64
     L.sbft_make_request.argtypes = [_vp, ctypes.c_char_p, ctypes.c_char_p, _u8p, ctypes.c_size_t, _u8p,
@@ -452,6 +453,14 @@ class Signer:
         out = (ctypes.c_uint8 * 65)()
         self.L.sbft_signer_public_key(self.h, out)
         return bytes(out)
+
+    def presign(self, pool: int) -> None:
+        """Pre-signature pool (include/sbft_verifier.h sbft_signer_presign): randomized
+        nonces, r / k^-1 / k^-1 r d computed `pool` at a time on the GPU, one host product per
+        signature. 0 returns to RFC 6979 nonces."""
+        rc = self.L.sbft_signer_presign(self.h, pool)
+        if rc:
+            raise VerifyError(rc, f"presign: code {rc}")
 
     def Sign(self, data: bytes) -> bytes:
         keep = []

@@ -110,6 +110,37 @@ def test_signer_rfc6979_known_answer(gpu):
         "F7CB1C942D657C41D436C7A1B6E29F65F3E900DBB9AFF4064DC4AB2F843ACDA8")
 
 
+def test_presign_pool_signatures(gpu):
+    """Pooled signer (sbft_signer_presign): randomized signatures, valid under the oracle,
+    through pool refills (pool 5, 23 signatures), and SignProposal verifies on the keyed path;
+    presign(0) returns to the RFC 6979 known answer."""
+    x = bytes.fromhex("C9AFA9D845BA75166B5C215767B1D6934E50C3DB36E89B127B8A622B120F6721")
+    s = plugin.Signer(gpu, 9, x)
+    pub = s.public_key()
+    qx, qy = pub[1:33], pub[33:]
+    s.presign(5)
+    sigs = []
+    for i in range(23):
+        m = b"pooled-%d" % i
+        sig = s.Sign(m)
+        sigs.append(sig)
+        e = hashlib.sha256(m).digest()
+        assert oracle.verify_batch(*[np.frombuffer(b, dtype=np.uint8).reshape(1, 32)
+                                     for b in (e, sig[:32], sig[32:], qx, qy)])[0], i
+    assert len({sg[:32] for sg in sigs}) == len(sigs)  # fresh nonce per signature
+    assert s.Sign(b"sample") != s.Sign(b"sample")    # randomized
+    v = plugin.Verifier(gpu, 1)
+    v.add_consenter(9, pub)
+    p = plugin.Proposal(b"pooled-block" * 50, b"h", b"m", 1)
+    sp = s.SignProposal(p, b"aux")
+    assert v.VerifyConsenterSig(sp, p) == b"aux"
+    s.presign(0)
+    assert s.Sign(b"sample").hex().upper() == (
+        "EFD48B2AACB6A8FD1140DD9CD45E81D69D2C877B56AAF991C34D0EA84EAF3716"
+        "F7CB1C942D657C41D436C7A1B6E29F65F3E900DBB9AFF4064DC4AB2F843ACDA8")
+    v.close()
+
+
 def test_consenter_sig_roundtrip_and_binding(net):
     v, nodes, clients = net
     p, _ = _proposal(clients, 10)

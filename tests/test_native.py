@@ -37,3 +37,23 @@ def test_safegcd_inverse_matches_pow(inv_exe, mod):
     assert len(out) == len(xs)
     bad = [hex(x) for x, o in zip(xs, out) if int(o, 16) != scale * pow(x, -1, M) % M]
     assert not bad, bad[:4]
+
+
+def test_host_mod_n_arithmetic(tmp_path):
+    """modn_host.hpp (the pooled signer's online s = A e + B) against Python big integers."""
+    exe = str(tmp_path / "modn_test")
+    subprocess.run(["g++", "-O2", "-Wall", "-Werror", "-o", exe,
+                    os.path.join(ROOT, "tests", "native", "modn_test.cpp")], check=True)
+    rng = random.Random(7)
+    edge = [0, 1, 2, N - 1, N - 2, N // 2, 2**255, 2**256 - 1, 2**256 - N, N, N + 1, 2**128 - 1]
+    pairs = [(a, b) for a in edge for b in edge]
+    pairs += [(rng.randrange(2**256), rng.randrange(2**256)) for _ in range(20000)]
+    out = subprocess.run([exe], input="".join("%064x %064x\n" % p for p in pairs), capture_output=True,
+                         text=True, check=True).stdout.split("\n")
+    assert len([l for l in out if l]) == len(pairs)
+    for (a, b), line in zip(pairs, out):
+        # inputs are reduced once on load (any 256-bit value is < 2n)
+        ar, br = (a - N if a >= N else a), (b - N if b >= N else b)
+        m, s = line.split()
+        assert int(m, 16) == ar * br % N, (hex(a), hex(b))
+        assert int(s, 16) == (ar + br) % N, (hex(a), hex(b))

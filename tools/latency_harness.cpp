@@ -12,6 +12,9 @@
 //       SBFT_V_EVERIFY with the reference's text, everyone else 0.
 //   quorum-batch VOTES DECISIONS
 //       the batch hook: one sbft_verifier_verify_consenter_sigs call per decision.
+//   sign CALLS
+//       one signature at a time from one thread: sbft_signer_sign (RFC 6979, and with the
+//       pre-signature pool of 1,024) vs OpenSSL ECDSA_do_sign.
 //   quorum-cpu  CALLERS DECISIONS THREADS
 //       the same fan-out with the verify on the CPU: CALLERS votes verified by THREADS
 //       workers (one thread per vote when THREADS >= CALLERS), SHA-256(Msg) + ECDSA_do_verify
@@ -64,7 +67,10 @@ static double pct(std::vector<double> v, double p) {
 // Returns per-round wall times (release -> last thread done), microseconds. Release and
 // completion go through futexes and atomics, not a mutex: a mutex makes the n wake-ups (and
 // the n completions) queue one behind another, which would add ~2-4 us per thread to every
-// round (Go's goroutines, which this emulates, do not pay that).
+// round (Go's goroutines, which this emulates, do not pay that). The release is a wake-up tree
+// (the main thread wakes two, every woken thread two more): one FUTEX_WAKE of all n runs the n
+// wake-ups serially inside one system call (~1-1.5 us each), slower than the Go runtime
+// starting n goroutines on its GOMAXPROCS threads.
 static long futex(std::atomic<int>* a, int op, int val) {
     return syscall(SYS_futex, reinterpret_cast<int*>(a), op, val, nullptr, nullptr, 0);
 }
@@ -77,7 +83,12 @@ static std::vector<double> fan_out(size_t n, int rounds, const std::function<voi
             int seen = -1;
             for (;;) {
                 int g;
-                while ((g = gen.load(std::memory_order_acquire)) == seen && !stop.load()) futex(&gen, FUTEX_WAIT_PRIVATE, seen);
+                bool slept = false;
+                while ((g = gen.load(std::memory_order_acquire)) == seen && !stop.load()) {
+                    futex(&gen, FUTEX_WAIT_PRIVATE, seen);
+                    slept = true;
+                }
+                if (slept) futex(&gen, FUTEX_WAKE_PRIVATE, 2);  // the release is a wake-up tree
                 if (stop.load()) return;
                 seen = g;
                 run(i, g);
@@ -92,7 +103,7 @@ static std::vector<double> fan_out(size_t n, int rounds, const std::function<voi
         remaining.store((int)n);
         const auto t0 = Clock::now();
         gen.store(r, std::memory_order_release);
-        futex(&gen, FUTEX_WAKE_PRIVATE, INT_MAX);
+        futex(&gen, FUTEX_WAKE_PRIVATE, 2);
         int d;
         while ((d = done_gen.load(std::memory_order_acquire)) != r) futex(&done_gen, FUTEX_WAIT_PRIVATE, d);
         out.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
@@ -313,6 +324,65 @@ static int quorum_cpu(int callers, int decisions, int threads) {
     return 0;
 }
 
+// sign CALLS: SignProposal's signing (view.go:481) one message at a time from one thread:
+// sbft_signer_sign (RFC 6979 nonce on the host, the GPU latency-path kernel) against OpenSSL
+// ECDSA_do_sign (ecp_nistz256, random nonce) on the same 128-byte messages.
+static int sign_both(int calls) {
+    sbft_gv_ctx* ctx = nullptr;
+    if (sbft_gv_init(nullptr, &ctx)) {
+        std::fprintf(stderr, "no GPU\n");
+        return 1;
+    }
+    uint8_t d[32];
+    priv_of(4242, d);
+    sbft_signer* sg = sbft_signer_new(ctx, 1, d);
+    std::vector<uint8_t> msg(128, 7), sig(64);
+    std::vector<double> tg, tc;
+    int bad = 0;
+    for (int i = -5; i < calls; ++i) {
+        msg[0] = (uint8_t)i;
+        msg[1] = (uint8_t)(i >> 8);
+        const auto t0 = Clock::now();
+        bad += sbft_signer_sign(sg, msg.data(), msg.size(), sig.data()) != 0;
+        if (i >= 0) tg.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+    }
+    // the pre-signature pool (sbft_signer_presign): refills of 1,024 included in the samples
+    std::vector<double> tp;
+    if (sbft_signer_presign(sg, 1024)) bad++;
+    for (int i = 0; i < 3 * calls; ++i) {
+        msg[0] = (uint8_t)i;
+        msg[1] = (uint8_t)(i >> 8);
+        const auto t0 = Clock::now();
+        bad += sbft_signer_sign(sg, msg.data(), msg.size(), sig.data()) != 0;
+        tp.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+    }
+    EC_KEY* k = EC_KEY_new_by_curve_name(NID_X9_62_prime256v1);
+    EC_KEY_generate_key(k);
+    for (int i = -5; i < calls; ++i) {
+        msg[0] = (uint8_t)i;
+        msg[1] = (uint8_t)(i >> 8);
+        const auto t0 = Clock::now();
+        uint8_t h[32];
+        sha256_ll(msg.data(), msg.size(), h);
+        ECDSA_SIG* s = ECDSA_do_sign(h, 32, k);
+        if (i >= 0) tc.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+        bad += s == nullptr;
+        ECDSA_SIG_free(s);
+    }
+    EC_KEY_free(k);
+    double tp_mean = 0;
+    for (double x : tp) tp_mean += x;
+    tp_mean /= tp.empty() ? 1 : (double)tp.size();
+    std::printf("{\"mode\": \"sign\", \"calls\": %d, \"gpu_rfc6979_p50_ms\": %.4f, \"gpu_rfc6979_p99_ms\": %.4f, "
+                "\"gpu_pooled_p50_ms\": %.4f, \"gpu_pooled_p99_ms\": %.4f, \"gpu_pooled_mean_ms\": %.4f, "
+                "\"openssl_1core_p50_ms\": %.4f, \"openssl_1core_p99_ms\": %.4f, \"failures\": %d}\n",
+                calls, pct(tg, 50) / 1e3, pct(tg, 99) / 1e3, pct(tp, 50) / 1e3, pct(tp, 99) / 1e3, tp_mean / 1e3,
+                pct(tc, 50) / 1e3, pct(tc, 99) / 1e3, bad);
+    sbft_signer_free(sg);
+    sbft_gv_destroy(ctx);
+    return bad ? 2 : 0;
+}
+
 static int proposal_cpu(int requests, int decisions, int threads) {
     auto tup = cpu_tuples(requests, 64 + 150, 256 + 150);  // body = ids + payload + key
     std::atomic<int> bad{0};
@@ -335,13 +405,14 @@ static int proposal_cpu(int requests, int decisions, int threads) {
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-cpu|proposal-cpu ...\n", argv[0]);
+        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|sign|quorum-cpu|proposal-cpu ...\n", argv[0]);
         return 1;
     }
     const std::string mode = argv[1];
     auto arg = [&](int i, int def) { return argc > i ? std::atoi(argv[i]) : def; };
     if (mode == "quorum-gpu") return quorum_gpu(arg(2, 66), arg(3, 200), arg(4, 0), arg(5, 0));
     if (mode == "quorum-batch") return quorum_batch(arg(2, 67), arg(3, 200));
+    if (mode == "sign") return sign_both(arg(2, 200));
     if (mode == "quorum-cpu") return quorum_cpu(arg(2, 66), arg(3, 200), arg(4, 66));
     if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
     std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
