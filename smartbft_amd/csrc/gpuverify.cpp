@@ -341,6 +341,9 @@ struct sbft_gv_ctx {
     // keyed batches (per device) of at most this many signatures take the zero-copy path
     // (enqueue_keyed); SBFT_KEYED_ZC_MAX overrides (0 = never)
     size_t keyed_zc_max = 1024;
+    // ... and batches of at least this many the four-lane kernel (p256_verify_keyed_lanes_kernel,
+    // batched s^-1) instead of a wavefront per signature; SBFT_KEYED_LANES_MIN overrides (0 = never)
+    size_t keyed_lanes_min = 1025;
     // registered public keys (x || y big-endian); index = key id, entry 0 = the generator
     std::mutex keys_mu;
     std::vector<std::array<uint8_t, 64>> keys;
@@ -391,6 +394,7 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     if (opts && opts->pair_max) ctx->pair_max = opts->pair_max < 0 ? 0u : (uint32_t)opts->pair_max;
     if (opts && opts->quad_max) ctx->quad_max = opts->quad_max < 0 ? 0u : (uint32_t)opts->quad_max;
     if (const char* e = getenv("SBFT_KEYED_ZC_MAX")) ctx->keyed_zc_max = (size_t)strtoull(e, nullptr, 10);
+    if (const char* e = getenv("SBFT_KEYED_LANES_MIN")) ctx->keyed_lanes_min = (size_t)strtoull(e, nullptr, 10);
     for (int d = 0; d < ndev && d < 32; ++d) {
         if (!(mask & (1u << d))) continue;
         auto* s = new Slot();
@@ -1352,7 +1356,7 @@ int build_tables(Slot* sl, const std::vector<std::array<uint8_t, 64>>& keys, siz
 //     commit-quorum call). A fault is caught by polling the stream now and then.
 int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t blob_len, const uint64_t* off,
                   const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint32_t* key, uint32_t nkeys,
-                  bool zc, uint8_t* ok_out) {
+                  bool zc, uint8_t* ok_out, size_t lanes_min) {
     Slot* sl = c.slot;
     const size_t n = c.count, b = c.begin;
     static const bool trace = getenv("SBFT_KEYED_TRACE") != nullptr;  // diagnostics
@@ -1368,9 +1372,13 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
     }
     const size_t span = blob ? hi - lo : 0;
     const size_t f32 = align_up(32 * n, 256), fk = align_up(4 * n, 256);
-    const size_t fmsg = blob ? align_up(span + 128, 256) + align_up(8 * n, 256) + fk : f32;
+    const size_t fblob = align_up(span + SBFT_GV_SHA_BLOB_PAD, 256);  // + the hash kernel's over-read
+    const size_t fmsg = blob ? fblob + align_up(8 * n, 256) + fk : f32;
     const size_t fok = align_up(n, 256);
     const size_t in_bytes = 2 * f32 + fk + fmsg;
+    // large batches: the four-lane kernel, with digests from the hash kernel (counter | digests)
+    const bool lanes = !zc && lanes_min && n >= lanes_min;
+    const size_t fextra = lanes ? 256 + f32 : 0;
     HIPCHK(hipSetDevice(sl->device));
     int rc;
     uint8_t *h, *d;
@@ -1380,7 +1388,7 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
         h = sl->zc;
         d = sl->zc_dev;
     } else {
-        rc = sl->reserve(in_bytes + fok);
+        rc = sl->reserve(in_bytes + fok + fextra);
         if (rc) return rc;
         rc = sl->reserve_pinned(in_bytes + fok);
         if (rc) return rc;
@@ -1393,8 +1401,8 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
     uint8_t* m = h + 2 * f32 + fk;
     if (blob) {
         std::memcpy(m, blob + lo, span);
-        std::memset(m + span, 0, 128);
-        uint64_t* o = (uint64_t*)(m + align_up(span + 128, 256));
+        std::memset(m + span, 0, fblob - span);
+        uint64_t* o = (uint64_t*)(m + fblob);
         for (size_t k = 0; k < n; ++k) o[k] = off[b + k] - lo;
         std::memcpy((uint8_t*)o + align_up(8 * n, 256), len + b, 4 * n);
     } else {
@@ -1409,14 +1417,27 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
     }
     const uint8_t* dm = d + 2 * f32 + fk;
     const uint8_t* d_blob = blob ? dm : nullptr;
-    const uint64_t* d_off = blob ? (const uint64_t*)(dm + align_up(span + 128, 256)) : nullptr;
+    const uint64_t* d_off = blob ? (const uint64_t*)(dm + fblob) : nullptr;
     const uint32_t* d_len = blob ? (const uint32_t*)((const uint8_t*)d_off + align_up(8 * n, 256)) : nullptr;
     uint8_t* d_ok = d + in_bytes;
     const auto t1 = std::chrono::steady_clock::now();
-    if (sbft_launch_p256_verify_keyed(blob ? nullptr : dm, d_blob, d_off, d_len, d, d + f32,
-                                      (const uint32_t*)(d + 2 * f32), (const void* const*)sl->d_keytab, nkeys, d_ok,
-                                      (uint32_t)n, zc ? 2 : 0, sl->stream))
+    if (lanes) {
+        uint8_t* x = d + in_bytes + fok;  // hash counter | digests
+        const uint8_t* dig = dm;
+        if (blob) {
+            if (sbft_launch_sha256(d_blob, d_off, d_len, nullptr, x + 256, (uint32_t)n, (uint32_t*)x, sl->stream))
+                return SBFT_GV_ELAUNCH;
+            dig = x + 256;
+        }
+        if (sbft_launch_p256_verify_keyed_lanes(dig, d, d + f32, (const uint32_t*)(d + 2 * f32),
+                                                (const void* const*)sl->d_keytab, nkeys, d_ok, (uint32_t)n,
+                                                sl->stream))
+            return SBFT_GV_ELAUNCH;
+    } else if (sbft_launch_p256_verify_keyed(blob ? nullptr : dm, d_blob, d_off, d_len, d, d + f32,
+                                             (const uint32_t*)(d + 2 * f32), (const void* const*)sl->d_keytab, nkeys,
+                                             d_ok, (uint32_t)n, zc ? 2 : 0, sl->stream)) {
         return SBFT_GV_ELAUNCH;
+    }
     if (!zc) {
         HIPCHK(hipMemcpyAsync(h + in_bytes, d_ok, n, hipMemcpyDeviceToHost, sl->stream));
         c.out_off = in_bytes;
@@ -1480,8 +1501,10 @@ int run_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* blob, size
         std::lock_guard<std::mutex> lk(c.slot->mu);
         int rc = ensure_tables(c.slot, nkeys);
         if (rc == SBFT_GV_OK && c.count <= ctx->keyed_zc_max)
-            return enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, true, ok_out);
-        if (rc == SBFT_GV_OK) rc = enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, false, ok_out);
+            return enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, true, ok_out, 0);
+        if (rc == SBFT_GV_OK)
+            rc = enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, false, ok_out,
+                               ctx->keyed_lanes_min);
         (void)hipSetDevice(c.slot->device);
         if (hipStreamSynchronize(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
         // the verdicts sit in the slot's pinned staging, which the lock still protects

@@ -700,6 +700,31 @@ SBFT_DEV f29 f29_from_u256(const fe& a) {
     }
     return r;
 }
+// x R mod p (8 x 32 Montgomery form, R = 2^256, canonical) -> the radix-2^29 Montgomery form
+// x 2^261 mod p without a multiplication: the 9 limbs of 32 x R (< 2^261; limb i = bits
+// [29 i - 5, 29 i + 24) of x R), then its 2^256 multiple q folded back with
+// 2^256 = 2^224 - 2^192 - 2^96 + 1 (mod p): q << 21 at limb 7, -q << 18 at limb 6, -q << 9 at
+// limb 3, +q at limb 0 (q < 32). Out: value in [0, 2^257), limbs 0..7 in (-2^23, 2^29 + 2^26),
+// limb 8 in [0, 2^24) (within N').
+SBFT_DEV f29 f29_from_mont256(const fe& a) {
+    f29 r;
+    r.v[0] = (a.v[0] << 5) & F29_MASK;
+#pragma unroll
+    for (int i = 1; i < 9; ++i) {
+        const int bit = 29 * i - 5, w = bit >> 5, s = bit & 31;
+        const u32 lo = a.v[w];
+        const u32 hi = (w + 1 < 8) ? a.v[w + 1] : 0u;
+        r.v[i] = __builtin_amdgcn_alignbit(hi, lo, s) & F29_MASK;
+    }
+    const u32 q = r.v[8] >> 24;
+    r.v[8] &= 0x00FFFFFFu;
+    r.v[7] += q << 21;
+    r.v[6] -= q << 18;
+    r.v[3] -= q << 9;
+    r.v[0] += q;
+    return r;
+}
+
 // Full normalisation to [0, 2^261) limbs-in-range form via a carry chain; |x| < 2^260 in,
 // value x mod 2^261 out (callers add a multiple of p first when x may be negative).
 SBFT_DEV void f29_norm_chain(f29& r, const f29& a) {

@@ -38,11 +38,7 @@ namespace sbft {
 #define SBFT_KEYED_MARK(i) ((void)0)
 #endif
 
-#define COMB_WINDOWS 32
-#define COMB_ENTRIES 256
-// uint4 units per entry (64 B: x limbs 0..7, y limbs 0..7) and per key table
-#define COMB_ENTRY_U4 4
-#define COMB_KEY_U4 (COMB_WINDOWS * COMB_ENTRIES * COMB_ENTRY_U4)
+// comb table layout (COMB_*): p256_point.hpp
 
 SBFT_DEV void to_affine_mont(fe& x, fe& y, const jp& p) {
     fe zi, zi2, zi3;
@@ -121,14 +117,6 @@ SBFT_DEV void shfl_xor_fe(fe& o, const fe& a, int mask) {
     for (int k = 0; k < 8; ++k) o.v[k] = shfl_xor_u32(a.v[k], mask);
 }
 
-// byte w (0..31, little-endian) of a 256-bit value, w lane-varying
-SBFT_DEV u32 byte_of(const fe& a, u32 w) {
-    const u32 limb_i = w >> 2;
-    u32 limb = a.v[0];
-#pragma unroll
-    for (int k = 1; k < 8; ++k) limb = (limb_i == (u32)k) ? a.v[k] : limb;
-    return (limb >> (8 * (w & 3))) & 255u;
-}
 
 
 // ---- cooperative point additions (latency path) ----
@@ -275,32 +263,6 @@ SBFT_DEV void coop_add_jac_quad(jp& acc, bool& inf, u32 lane, int lvl) {
     finish_add(acc, inf, p1, i1, p2, i2, H, R, X3, Y3, Z3);
 }
 
-// x(R) mod n == r, projectively; r is the plain (non-Montgomery) 256-bit value in [1, n)
-SBFT_DEV bool x_matches_r(const jp& R, const fe& r) {
-    const fe r2p = fe_const(C_R2P);
-    fe z2, lhs, xc, rm;
-    fp_sqr(z2, R.z);
-    fp_canon(xc, R.x);
-    fp_mul(rm, r, r2p);
-    fp_mul(lhs, rm, z2);
-    fp_canon(lhs, lhs);
-    bool accept = fe_eq(lhs, xc);
-    fe rn;
-    u64 c = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        c = (u64)r.v[k] + P256_N[k] + c;
-        rn.v[k] = lo32(c);
-        c >>= 32;
-    }
-    if (c == 0 && fe_lt(rn, P256_P)) {
-        fp_mul(rm, rn, r2p);
-        fp_mul(lhs, rm, z2);
-        fp_canon(lhs, lhs);
-        accept = accept || fe_eq(lhs, xc);
-    }
-    return accept;
-}
 
 // ---- the same butterfly in radix-2^29 arithmetic (p256_f29.hpp), lean additions ----
 // A field product here is f29_mul_ilp: its 17 column sums are independent chains, so one
@@ -312,7 +274,6 @@ SBFT_DEV bool x_matches_r(const jp& R, const fe& r) {
 #ifndef SBFT_KEYED_F29
 #define SBFT_KEYED_F29 1
 #endif
-__device__ __constant__ static const u32 C29_CONV256[9] = P256_F29_CONV256;
 
 template <int CTRL>
 SBFT_DEV f29 dpp29(const f29& a) {
@@ -348,9 +309,8 @@ SBFT_DEV void jp29_sel(jp29& out, bool c, const jp29& a) {
 
 // table entry (8 x 32 Montgomery, R = 2^256, canonical) -> affine f29 Montgomery (R = 2^261)
 SBFT_DEV void entry_to_f29(const fe& x, const fe& y, jp29& p) {
-    const f29 k = f29_const(C29_CONV256);  // 2^266 mod p
-    f29_mul_ilp(p.x, f29_from_u256(x), k);
-    f29_mul_ilp(p.y, f29_from_u256(y), k);
+    p.x = f29_from_mont256(x);
+    p.y = f29_from_mont256(y);
     p.z = f29_const(C29_ONE);
 }
 

@@ -418,4 +418,49 @@ SBFT_DEV void store_be32(uint8_t* p, const fe& a) {
                       __builtin_bswap32(a.v[0]));
 }
 
+// Registered-key comb tables (p256_keyed.hip builds them; the keyed kernels of p256_keyed.hip
+// and p256_verify.hip read them): table[w][j] = j 2^(8w) Q, w = 0..31, j = 0..255 (j = 0: zeros),
+// affine, 8 x 32 Montgomery form (R = 2^256) mod p, canonical.
+#define COMB_WINDOWS 32
+#define COMB_ENTRIES 256
+// uint4 units per entry (64 B: x limbs 0..7, y limbs 0..7) and per key table
+#define COMB_ENTRY_U4 4
+#define COMB_KEY_U4 (COMB_WINDOWS * COMB_ENTRIES * COMB_ENTRY_U4)
+
+// byte w (0..31, little-endian) of a 256-bit value, w lane-varying
+SBFT_DEV u32 byte_of(const fe& a, u32 w) {
+    const u32 limb_i = w >> 2;
+    u32 limb = a.v[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) limb = (limb_i == (u32)k) ? a.v[k] : limb;
+    return (limb >> (8 * (w & 3))) & 255u;
+}
+
+// x(R) mod n == r, projectively; r is the plain (non-Montgomery) 256-bit value in [1, n)
+SBFT_DEV bool x_matches_r(const jp& R, const fe& r) {
+    const fe r2p = fe_const(C_R2P);
+    fe z2, lhs, xc, rm;
+    fp_sqr(z2, R.z);
+    fp_canon(xc, R.x);
+    fp_mul(rm, r, r2p);
+    fp_mul(lhs, rm, z2);
+    fp_canon(lhs, lhs);
+    bool accept = fe_eq(lhs, xc);
+    fe rn;
+    u64 c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        c = (u64)r.v[k] + P256_N[k] + c;
+        rn.v[k] = lo32(c);
+        c >>= 32;
+    }
+    if (c == 0 && fe_lt(rn, P256_P)) {
+        fp_mul(rm, rn, r2p);
+        fp_mul(lhs, rm, z2);
+        fp_canon(lhs, lhs);
+        accept = accept || fe_eq(lhs, xc);
+    }
+    return accept;
+}
+
 }  // namespace sbft

@@ -1061,6 +1061,148 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
         }
     }
 }
+// ---- registered keys, large batches: four lanes per signature (p256_verify_keyed_lanes) ----
+// For batches too large for one wavefront per signature (p256_keyed.hip's latency kernel),
+// each signature takes a quad: lane j sums 16 comb entries with lean mixed additions in
+// radix 2^29 — j = 0, 1: windows 0-15 / 16-31 of u1 over G's table; j = 2, 3: the same of u2
+// over the key's table — then the quad adds the four partial sums (two lean Jacobian
+// additions) and checks x(R) = r. Each lane inverts s itself (safegcd, LDS divstep table).
+// No partial sum inside a chain or of two chains of the same scalar can meet an exceptional
+// case (they are m P for distinct 0 < m < n over disjoint windows); only G part + Q part can
+// (u1 G = +-u2 Q, craftable with related keys). That shows as Z = 0, and the quad then
+// recomputes the signature with the exact 8 x 32 additions (infinity, doubling, cancellation).
+SBFT_DEV void jp29_pick(jp29& out, bool c, const jp29& a) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        out.x.v[k] = c ? a.x.v[k] : out.x.v[k];
+        out.y.v[k] = c ? a.y.v[k] : out.y.v[k];
+        out.z.v[k] = c ? a.z.v[k] : out.z.v[k];
+    }
+}
+// acc + (partner lane's acc) with infinity flags, lean (quad_perm control CTRL picks the partner)
+template <int CTRL>
+SBFT_DEV void quad_combine(jp29& acc, bool& inf) {
+    jp29 o;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        o.x.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.x.v[k], CTRL, 0xf, 0xf, false);
+        o.y.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.y.v[k], CTRL, 0xf, 0xf, false);
+        o.z.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.z.v[k], CTRL, 0xf, 0xf, false);
+    }
+    const bool oinf = __builtin_amdgcn_mov_dpp(inf ? 1 : 0, CTRL, 0xf, 0xf, false) != 0;
+    jp29 sum = acc;
+    p29_add_jac_lean(sum, o);
+    jp29_pick(sum, inf, o);
+    jp29_pick(sum, oinf && !inf, acc);
+    acc = sum;
+    inf = inf && oinf;
+}
+
+__global__ __launch_bounds__(256) void p256_verify_keyed_lanes_kernel(const uint8_t* __restrict__ digest,
+                                                                      const uint8_t* __restrict__ rr,
+                                                                      const uint8_t* __restrict__ ss,
+                                                                      const uint32_t* __restrict__ key,
+                                                                      const uint4* const* __restrict__ keytab,
+                                                                      uint32_t nkeys, uint8_t* __restrict__ ok,
+                                                                      uint32_t n) {
+    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    inv::stage_divstep_table(dtab);  // ends with a barrier
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t t = gid >> 2, j = gid & 3u;
+    const bool active = t < n;
+    const uint32_t idx = active ? t : n - 1;
+    const fe r = load_be32(rr + 32ull * idx);
+    const fe s = load_be32(ss + 32ull * idx);
+    const uint32_t kid = key[idx];
+    const bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
+                       kid >= 1 && kid < nkeys && keytab[kid] != nullptr;
+    // s^-1 in Montgomery form by each lane's own safegcd (the scaled start, p256_inv.hpp): at
+    // these batch sizes the launch-wide batched inversion's two kernels cost ~90 us of latency
+    fe w;
+    {
+        fe sv = s;
+        if (!valid) {
+            sv = fe_zero();
+            sv.v[0] = 1;
+        }
+        const fe rn = fe_const(C_ONEN);  // 2^256 mod n
+        inv::inv_mod(w.v, sv.v, dtab, false, rn.v);
+    }
+    fe e, u;
+    fn_canon(e, load_be32(digest + 32ull * idx));
+    fn_mul(u, j < 2 ? e : r, w);  // u1 = e s^-1 (j < 2) or u2 = r s^-1 (plain)
+    fn_canon(u, u);
+    const uint4* tab = keytab[j < 2 ? 0u : (valid ? kid : 0u)];
+    const u32 w0 = 16u * (j & 1u);
+    // 16 entries, the next one's loads issued before the current addition
+    jp29 acc;
+    bool inf = true;
+    acc.z = f29_const(C29_ONE);
+    uint4 cur[4], nxt[4];
+    auto entry = [&](u32 i, uint4 (&en)[4]) {
+        const u32 win = w0 + i;
+        const uint4* p = tab + (size_t)(win * COMB_ENTRIES + byte_of(u, win)) * COMB_ENTRY_U4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) en[k] = p[k];
+    };
+    entry(0, nxt);
+#pragma unroll 1
+    for (u32 i = 0; i < 16; ++i) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+        if (i < 15) entry(i + 1, nxt);
+        const bool zero = byte_of(u, w0 + i) == 0;
+        const fe ex = {{cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w}};
+        const fe ey = {{cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w}};
+        const f29 x2 = f29_from_mont256(ex), y2 = f29_from_mont256(ey);
+        jp29 sum = acc;
+        p29_add_aff_lean(sum, x2, y2);
+        if (!zero) {
+            if (inf) {
+                acc.x = x2;
+                acc.y = y2;
+                acc.z = f29_const(C29_ONE);
+            } else {
+                acc = sum;
+            }
+            inf = false;
+        }
+    }
+    quad_combine<0xB1>(acc, inf);  // quad_perm [1,0,3,2]: u1 G on lanes 0-1, u2 Q on lanes 2-3
+    quad_combine<0x4E>(acc, inf);  // quad_perm [2,3,0,1]: R on every lane
+    bool exc = false;
+    bool accept = verify_final(acc, r, exc) && !inf;
+    exc = exc && !inf;
+    if (__builtin_expect(__any(exc), 0)) {  // rare: the exact recomputation on the quad's lane 0
+        fe u1v, u2v;  // every lane of the quad gets both scalars (DPP before the branch)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            u1v.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)u.v[k], 0x00, 0xf, 0xf, false);  // quad_perm [0,0,0,0]
+            u2v.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)u.v[k], 0xAA, 0xf, 0xf, false);  // quad_perm [2,2,2,2]
+        }
+        if (exc && j == 0) {
+            jp a8;
+            bool inf8 = true;
+            a8.x = a8.y = a8.z = fe_zero();
+            const uint4* qt = keytab[valid ? kid : 0u];
+#pragma unroll 1
+            for (u32 h = 0; h < 64; ++h) {
+                const u32 win = h & 31u;
+                const fe& uu = h < 32 ? u1v : u2v;
+                const u32 d = byte_of(uu, win);
+                const uint4* en = (h < 32 ? keytab[0] : qt) + (size_t)(win * COMB_ENTRIES + d) * COMB_ENTRY_U4;
+                jp b;
+                b.x = {{en[0].x, en[0].y, en[0].z, en[0].w, en[1].x, en[1].y, en[1].z, en[1].w}};
+                b.y = {{en[2].x, en[2].y, en[2].z, en[2].w, en[3].x, en[3].y, en[3].z, en[3].w}};
+                b.z = fe_const(C_ONEP);
+                pt_add_jac(a8, inf8, b, d != 0);
+            }
+            accept = !inf8 && x_matches_r(a8, r);
+        }
+    }
+    if (active && j == 0) ok[t] = (valid && accept) ? 1 : 0;
+}
+
 }  // namespace sbft
 
 // Workspace layout (sbft_verify_work_bytes): [0, 4(n+1)) fixup counter + list, then the
@@ -1133,6 +1275,18 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
     hipLaunchKernelGGL(sbft::p256_verify_fixup_kernel, dim3(fix_blocks), dim3(threads), 0, stream,
                        d_digest, d_r, d_s, d_qx, d_qy, d_ok, (const uint32_t*)d_work);
     SBFT_STEP("fixup");
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Registered-key verify of a large batch, four lanes per signature.
+extern "C" int sbft_launch_p256_verify_keyed_lanes(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
+                                                   const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
+                                                   uint8_t* d_ok, uint32_t n, hipStream_t stream) {
+    if (n == 0) return 0;
+    const unsigned threads = 256;
+    const unsigned kblocks = (unsigned)((4ull * n + threads - 1) / threads);
+    hipLaunchKernelGGL(sbft::p256_verify_keyed_lanes_kernel, dim3(kblocks), dim3(threads), 0, stream, d_digest, d_r,
+                       d_s, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -68,6 +68,11 @@ int sbft_launch_comb_build(const uint8_t* d_qx, const uint8_t* d_qy, void* d_tab
 // Either d_digest (n x 32 B) or the messages (d_blob, d_off, d_len) hashed in the launch.
 // d_ok[t] = verdict (0/1) | mark: a nonzero mark lets a host polling d_ok in mapped memory see
 // each verdict land (the zero-copy latency path).
+// Large batches against registered keys (p256_verify.hip): four lanes per signature, each
+// lane inverting s itself; digests precomputed.
+int sbft_launch_p256_verify_keyed_lanes(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
+                                        const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
+                                        uint8_t* d_ok, uint32_t n, hipStream_t stream);
 int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint8_t* d_blob, const uint64_t* d_off,
                                   const uint32_t* d_len, const uint8_t* d_r, const uint8_t* d_s,
                                   const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,

@@ -86,6 +86,37 @@ def test_golden_vectors_keyed(gpu, p256_vectors):
     assert not got[ids == 0].any()
 
 
+@pytest.mark.parametrize("path", ["wave", "lanes"])
+def test_golden_vectors_keyed_paths(p256_vectors, path, monkeypatch):
+    """Every golden category (R = infinity and Shamir-exceptional included) through each keyed
+    kernel on its own: the wavefront per signature (zero-copy latency path) and the four-lane
+    kernel with the batched s^-1 (large batches), whichever the batch size would pick."""
+    from smartbft_amd import GpuVerifier
+    if path == "wave":
+        monkeypatch.setenv("SBFT_KEYED_ZC_MAX", "100000")
+        monkeypatch.setenv("SBFT_KEYED_LANES_MIN", "0")
+    else:
+        monkeypatch.setenv("SBFT_KEYED_ZC_MAX", "0")
+        monkeypatch.setenv("SBFT_KEYED_LANES_MIN", "1")
+    g = GpuVerifier(device_mask=1)
+    f, exp, cat, names = p256_vectors
+    rng = np.random.default_rng(11)
+    keep = []
+    for c in np.unique(cat):
+        idx = np.nonzero(cat == c)[0]
+        keep.extend(idx if len(idx) <= 160 else rng.choice(idx, 40, replace=False))
+    keep = np.sort(np.array(keep))
+    rows = f[keep]
+    ids = _register_all(g, rows)
+    d, r, s, _, _ = split_fields(rows)
+    for n in (len(keep), 1, 2, 1025):  # whole set, tiny and just past the zero-copy bound
+        sel = np.arange(min(n, len(keep)))
+        got = g.verify_keyed(d[sel], r[sel], s[sel], ids[sel])
+        bad = np.nonzero(got != exp[keep][sel])[0]
+        assert len(bad) == 0, (n, {names[c]: int((cat[keep][sel][bad] == c).sum()) for c in np.unique(cat[keep][sel][bad])})
+    g.close()
+
+
 def _signed(n, nkeys, seed, corrupt=0.3):
     rng = random.Random(seed)
     keys = [rng.randrange(1, N) for _ in range(nkeys)]
