@@ -916,13 +916,12 @@ int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* 
     if (!ctx) return SBFT_GV_EINVAL;
     if (n == 0) return SBFT_GV_OK;
     if (!digest || !r || !s || !qx || !qy || !ok_out || n > 0xffffffffu) return SBFT_GV_EINVAL;
-    // Large chunks are cut into sub-batches whose copies (copy stream) overlap the verify of
-    // the earlier ones. From pageable memory each copy first blocks this thread while the
-    // runtime stages it, which still overlaps with the kernels already queued.
-    static const bool pipe_pageable = getenv("SBFT_PIPE_PAGEABLE") ? atoi(getenv("SBFT_PIPE_PAGEABLE")) != 0 : true;
-    const bool pipe = n >= 2 * kPipeSub &&
-                      (pipe_pageable || (is_pinned(digest) && is_pinned(r) && is_pinned(s) && is_pinned(qx) &&
-                                         is_pinned(qy)));
+    // Page-locked inputs: large chunks are cut into sub-batches whose copies (copy stream)
+    // overlap the verify of the earlier ones. The same pipeline over pageable inputs measured
+    // no gain (51.2 vs 52.2 M verifies/s, profiles/r02c_host_pipe_ab.txt): the runtime's
+    // staging of a pageable copy does not overlap the queued kernels.
+    const bool pipe = n >= 2 * kPipeSub && is_pinned(digest) && is_pinned(r) && is_pinned(s) && is_pinned(qx) &&
+                      is_pinned(qy);
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
         if (pipe && c.lanes == 1 && c.count >= 2 * kPipeSub)
             return enqueue_verify_piped(c, digest, r, s, qx, qy, ok_out);
