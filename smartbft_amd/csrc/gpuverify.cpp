@@ -734,6 +734,15 @@ int enqueue_verify_piped(const Chunk& c, const uint8_t* digest, const uint8_t* r
     if (!gcomb) return SBFT_GV_ENOMEM;
     uint8_t* base = sl->dbuf;
     const uint8_t* src[5] = {digest, r, s, qx, qy};
+    // pageable inputs: each sub-batch is first gathered into page-locked staging by four host
+    // threads (~60 GB/s, far ahead of the ~10 GB/s the kernels consume), so its DMA runs at the
+    // pinned rate while earlier sub-batches verify
+    const bool stage = !(is_pinned(digest) && is_pinned(r) && is_pinned(s) && is_pinned(qx) && is_pinned(qy));
+    uint8_t* hst = nullptr;
+    if (stage) {
+        if ((rc = sl->reserve_pinned(5 * f))) return rc;
+        hst = sl->pin;
+    }
     hipEvent_t ev_start = sl->sub_ev[subs], ev_join = sl->sub_ev[subs + 1];
     // the copy stream and the second compute stream start after earlier work on the slot's
     // stream (which may still read dbuf)
@@ -746,9 +755,19 @@ int enqueue_verify_piped(const Chunk& c, const uint8_t* digest, const uint8_t* r
         HIPCHK(hipStreamWaitEvent(sl->stream2, ev_start, 0));
         for (size_t i = 0; i < subs; ++i) {
             const size_t b = cut[i], m = cut[i + 1] - b;
+            if (stage) {
+                auto part = [&](size_t lo, size_t hi) {
+                    for (int k = 0; k < 5; ++k)
+                        std::memcpy(hst + k * f + 32 * (b + lo), src[k] + 32 * (c.begin + b + lo), 32 * (hi - lo));
+                };
+                std::thread th[3];
+                for (int t = 1; t < 4; ++t) th[t - 1] = std::thread(part, m * t / 4, m * (t + 1) / 4);
+                part(0, m / 4);
+                for (auto& x : th) x.join();
+            }
             for (int k = 0; k < 5; ++k)
-                HIPCHK(hipMemcpyAsync(base + k * f + 32 * b, src[k] + 32 * (c.begin + b), 32 * m,
-                                      hipMemcpyHostToDevice, sl->copy_stream));
+                HIPCHK(hipMemcpyAsync(base + k * f + 32 * b, stage ? hst + k * f + 32 * b : src[k] + 32 * (c.begin + b),
+                                      32 * m, hipMemcpyHostToDevice, sl->copy_stream));
             HIPCHK(hipEventRecord(sl->sub_ev[i], sl->copy_stream));
         }
         for (size_t i = 0; i < subs; ++i) {
@@ -916,12 +935,14 @@ int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* 
     if (!ctx) return SBFT_GV_EINVAL;
     if (n == 0) return SBFT_GV_OK;
     if (!digest || !r || !s || !qx || !qy || !ok_out || n > 0xffffffffu) return SBFT_GV_EINVAL;
-    // Page-locked inputs: large chunks are cut into sub-batches whose copies (copy stream)
-    // overlap the verify of the earlier ones. The same pipeline over pageable inputs measured
-    // no gain (51.2 vs 52.2 M verifies/s, profiles/r02c_host_pipe_ab.txt): the runtime's
-    // staging of a pageable copy does not overlap the queued kernels.
-    const bool pipe = n >= 2 * kPipeSub && is_pinned(digest) && is_pinned(r) && is_pinned(s) && is_pinned(qx) &&
-                      is_pinned(qy);
+    // Large chunks are cut into sub-batches whose copies (copy stream) overlap the verify of
+    // the earlier ones; pageable inputs are gathered into page-locked staging first (handing
+    // the runtime pageable pointers measured no overlap: 51.2 vs 52.2 M verifies/s; staged: 53.0-53.8,
+    // profiles/r02c_host_pipe_ab.txt). SBFT_PIPE_PAGEABLE=0 keeps pageable inputs unpipelined.
+    static const bool pipe_pageable = getenv("SBFT_PIPE_PAGEABLE") ? atoi(getenv("SBFT_PIPE_PAGEABLE")) != 0 : true;
+    const bool pipe = n >= 2 * kPipeSub &&
+                      (pipe_pageable || (is_pinned(digest) && is_pinned(r) && is_pinned(s) && is_pinned(qx) &&
+                                         is_pinned(qy)));
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
         if (pipe && c.lanes == 1 && c.count >= 2 * kPipeSub)
             return enqueue_verify_piped(c, digest, r, s, qx, qy, ok_out);
