@@ -346,8 +346,9 @@ def test_framed_hash_then_verify(mode):
 def test_pinned_inputs_pipelined_host_verify(gpu):
     """sbft_gv_verify_p256 with all five inputs in sbft_gv_host_alloc memory takes the
     copy/compute pipeline (a 65,536 then 262,144-tuple sub-batches on a copy stream + events,
-    verified on two alternating compute streams: gpuverify.cpp enqueue_verify_piped): verdicts byte-identical to the pageable path and to the workload's
-    construction, including the ragged last sub-batch."""
+    verified on two alternating compute streams: gpuverify.cpp enqueue_verify_piped): verdicts
+    byte-identical to the pageable call (the same pipeline over page-locked staging) and to the
+    workload's construction, including the ragged last sub-batch."""
     import torch
     from smartbft_amd import PinnedArray
     from smartbft_amd.workload import make_workload
@@ -372,7 +373,8 @@ def test_pinned_inputs_pipelined_host_verify(gpu):
 def test_pinned_single_allocation_and_mixed_inputs(gpu):
     """INTEGRATION.md's layout: the five arrays at offsets inside ONE sbft_gv_host_alloc
     block (interior pointers must be recognised as pinned), and a call where one input is
-    pageable (falls back to the plain path). Both byte-identical to the workload verdicts."""
+    pageable (the pipeline then stages every sub-batch through page-locked memory). Both
+    byte-identical to the workload verdicts."""
     import torch
     from smartbft_amd import PinnedArray
     from smartbft_amd.workload import make_workload
