@@ -13,15 +13,17 @@
 // generator's table is key slot 0). Then u1*G + u2*Q = sum_w table_G[w][byte_w(u1)] +
 // sum_w table_Q[w][byte_w(u2)]: 64 table points and NO doublings.
 //
-// p256_verify_keyed_wave_kernel (latency path, one wavefront per signature):
-//   all lanes: [optional SHA-256 of the message] ; range checks ; w = s^-1 (safegcd,
-//   p256_inv.hpp) ; u1 = e w, u2 = r w
+// p256_verify_keyed_wave_kernel (latency path, one workgroup of two wavefronts per signature):
+//   wave 1: w = s^-1 R mod n (lane-parallel scaled safegcd, p256_inv.hpp inv_mod_wave)
+//   wave 0: [SHA-256 of the message] ; then u = e w (lanes < 32) or r w (lanes >= 32)
 //   lane l: loads ONE table point (l < 32: G window l of u1; l >= 32: Q window l-32 of u2)
-//   6-level butterfly reduction over the wave (ds_swizzle/bpermute exchanges), every
-//   addition the general one (infinity on either side, doubling, cancellation)
-//   lane 0: accept iff R != infinity and x(R) = r (mod n), projectively against r and r + n.
-// The dependent chain is ~6 point additions + one inversion instead of 256 doublings, which
-// is what makes a 67-signature commit quorum a ~100 us launch instead of a ~2 ms one.
+//   6-level butterfly over the wave in radix 2^29 with lean additions (quad-cooperative
+//   products, DPP broadcasts); Z = 0 at the end marks an exceptional addition, and only then
+//   the wave re-runs the butterfly with the exact 8 x 32 additions (infinity, doubling,
+//   cancellation); accept iff R != infinity and x(R) = r (mod n), projectively (r and r + n).
+// The dependent chain is ~6 point additions + one inversion instead of 256 doublings: a
+// 67-signature commit quorum is one ~42 us kernel (the phase timeline).
+// Large batches take p256_verify.hip's four-lane kernel over the same tables.
 //
 // Verdicts are bit-exact with Go crypto/ecdsa.Verify (same semantics as p256_verify.hip;
 // oracle/p256_oracle.c is the parity reference). An unregistered/invalid key id verifies false.
