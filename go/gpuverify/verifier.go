@@ -31,6 +31,7 @@ import (
 
 	"github.com/hyperledger-labs/SmartBFT/pkg/api"
 	"github.com/hyperledger-labs/SmartBFT/pkg/types"
+	protos "github.com/hyperledger-labs/SmartBFT/smartbftprotos"
 )
 
 // Options of the engine context (sbft_gv_opts).
@@ -363,4 +364,31 @@ func (v *Verifier) PruneSet(reqs [][]byte) ([]int, error) {
 		out[i] = int(idx[i])
 	}
 	return out, nil
+}
+
+// CommitSignaturesDigest is a drop-in for internal/bft/util.go:557-579 (called at view.go:598 to
+// check the leader's PrevCommitSignatureDigest and at view.go:984 to fill it): SHA-256 of the
+// Go-asn1 DER of the signatures, computed by the library on the host without copying values or
+// messages. nil for no signatures, as the original.
+func CommitSignaturesDigest(sigs []*protos.Signature) []byte {
+	if len(sigs) == 0 {
+		return nil
+	}
+	var p pinner
+	defer p.Unpin()
+	arr := make([]C.sbft_signature, len(sigs))
+	for i, s := range sigs {
+		arr[i] = C.sbft_signature{
+			id:    C.uint64_t(s.Signer),
+			value: p.bytes(s.Value), value_len: C.size_t(len(s.Value)),
+			msg: p.bytes(s.Msg), msg_len: C.size_t(len(s.Msg)),
+		}
+	}
+	p.Pin(&arr[0])
+	out := make([]byte, 32)
+	p.Pin(&out[0])
+	if C.sbft_commit_signatures_digest(&arr[0], C.size_t(len(sigs)), (*C.uint8_t)(unsafe.Pointer(&out[0]))) != 32 {
+		panic("gpuverify: CommitSignaturesDigest failed")
+	}
+	return out
 }

@@ -129,6 +129,11 @@ int64_t sbft_verifier_auxiliary_data(const uint8_t* msg, size_t msg_len, uint8_t
 /* types.Proposal.Digest (pkg/types/types.go:50-69): hex(SHA-256(ASN.1 DER of the proposal)),
  * 64 characters + NUL into out65. */
 void sbft_proposal_digest(const sbft_proposal* p, char out65[65]);
+/* CommitSignaturesDigest (internal/bft/util.go:557-579; callers view.go:598 checks the leader's
+ * PrevCommitSignatureDigest, view.go:984 fills it): SHA-256 of the ASN.1 DER of the signatures
+ * as Go's encoding/asn1 marshals IntDoubleBytes. Returns 32 with the digest in out32, 0 for no
+ * signatures (Go returns nil), SBFT_GV_EINVAL on NULL pointers. Host only (no GPU). */
+int sbft_commit_signatures_digest(const sbft_signature* sigs, size_t n, uint8_t out32[32]);
 /* Host SHA-256 (no GPU), used for Proposal.Digest and small messages. */
 void sbft_sha256_host(const uint8_t* msg, size_t len, uint8_t out[32]);
 

@@ -843,6 +843,61 @@ void sbft_proposal_digest(const sbft_proposal* p, char out65[65]) {
     out65[64] = 0;
 }
 
+int sbft_commit_signatures_digest(const sbft_signature* sigs, size_t n, uint8_t out32[32]) {
+    // CommitSignaturesDigest (internal/bft/util.go:557-579): SHA-256 over Go asn1.Marshal of
+    // IntDoubleBytes{A: [{A: int64(Signer), B: Value, C: Msg}, ...]}, i.e.
+    //   SEQUENCE { SEQUENCE { SEQUENCE { INTEGER signer, OCTET STRING value, OCTET STRING msg } ... } }
+    // No signatures: nil (returns 0, out32 untouched). Values and messages are hashed in place;
+    // only the tag/length prefixes are built.
+    if (n == 0) return 0;
+    if (!sigs || !out32) return SBFT_GV_EINVAL;
+    std::vector<uint8_t> ints;  // the n INTEGER encodings, back to back
+    std::vector<uint32_t> int_end(n);
+    std::vector<size_t> elem(n);
+    size_t inner = 0;
+    for (size_t i = 0; i < n; ++i) {
+        der_int64(ints, (int64_t)sigs[i].id);
+        int_end[i] = (uint32_t)ints.size();
+        std::vector<uint8_t> l;
+        der_len(l, sigs[i].value_len);
+        size_t body = (int_end[i] - (i ? int_end[i - 1] : 0)) + 1 + l.size() + sigs[i].value_len;
+        l.clear();
+        der_len(l, sigs[i].msg_len);
+        body += 1 + l.size() + sigs[i].msg_len;
+        elem[i] = body;
+        l.clear();
+        der_len(l, body);
+        inner += 1 + l.size() + body;
+    }
+    std::vector<uint8_t> hdr;
+    std::vector<uint8_t> mid;
+    mid.push_back(0x30);
+    der_len(mid, inner);
+    hdr.push_back(0x30);
+    der_len(hdr, mid.size() + inner);
+    Sha256 h;
+    h.update(hdr.data(), hdr.size());
+    h.update(mid.data(), mid.size());
+    for (size_t i = 0; i < n; ++i) {
+        std::vector<uint8_t> t;
+        t.push_back(0x30);
+        der_len(t, elem[i]);
+        const size_t i0 = i ? int_end[i - 1] : 0;
+        t.insert(t.end(), ints.begin() + i0, ints.begin() + int_end[i]);
+        t.push_back(0x04);
+        der_len(t, sigs[i].value_len);
+        h.update(t.data(), t.size());
+        if (sigs[i].value_len) h.update(sigs[i].value, sigs[i].value_len);
+        t.clear();
+        t.push_back(0x04);
+        der_len(t, sigs[i].msg_len);
+        h.update(t.data(), t.size());
+        if (sigs[i].msg_len) h.update(sigs[i].msg, sigs[i].msg_len);
+    }
+    h.final(out32);
+    return 32;
+}
+
 sbft_verifier* sbft_verifier_new(sbft_gv_ctx* ctx, uint64_t verification_sequence) {
     // ctx may be NULL for a parse-only verifier (RequestsFromProposal, AuxiliaryData);
     // verification calls on it fail with SBFT_GV_ENODEV.

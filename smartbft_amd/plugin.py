@@ -137,6 +137,7 @@ def _lib():
     L.sbft_verifier_auxiliary_data.argtypes = [_u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t]
     L.sbft_proposal_digest.argtypes = [P, ctypes.c_char_p]
     L.sbft_proposal_digest.restype = None
+    L.sbft_commit_signatures_digest.argtypes = [S, ctypes.c_size_t, _u8p]
     L.sbft_sha256_host.argtypes = [_u8p, ctypes.c_size_t, _u8p]
     L.sbft_sha256_host.restype = None
     L.sbft_signer_new.restype = _vp
@@ -181,6 +182,18 @@ def sha256_host(b: bytes) -> bytes:
     keep = []
     _lib().sbft_sha256_host(_buf(b, keep), len(b), out)
     return bytes(out)
+
+
+def CommitSignaturesDigest(sigs: list[Signature]) -> bytes | None:
+    """internal/bft/util.go:557-579: SHA-256 of the Go-asn1 DER of the signatures; None (Go's
+    nil) for an empty list."""
+    keep = []
+    arr = (_Signature * max(1, len(sigs)))(*[_sig(s, keep) for s in sigs])
+    out = (ctypes.c_uint8 * 32)()
+    rc = _lib().sbft_commit_signatures_digest(arr, len(sigs), out)
+    if rc < 0:
+        raise VerifyError(rc, "commit signatures digest: invalid arguments")
+    return bytes(out) if rc == 32 else None
 
 
 def compute_quorum(n: int) -> tuple[int, int]:

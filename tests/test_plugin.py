@@ -51,6 +51,40 @@ def test_proposal_digest_matches_go_asn1(size, vseq):
     assert p.Digest() == _go_digest(p)
 
 
+def _go_commit_sigs_digest(sigs):
+    # util.go:557-579: asn1.Marshal(IntDoubleBytes{A: [{int64(Signer), Value, Msg}...]})
+    if not sigs:
+        return None
+    elems = b""
+    for s in sigs:
+        v = s.ID - (1 << 64) if s.ID >= 1 << 63 else s.ID  # int64(sig.Signer)
+        iv = _go_int64(v)
+        e = b"\x02" + _der_len(len(iv)) + iv
+        e += b"\x04" + _der_len(len(s.Value)) + s.Value + b"\x04" + _der_len(len(s.Msg)) + s.Msg
+        elems += b"\x30" + _der_len(len(e)) + e
+    inner = b"\x30" + _der_len(len(elems)) + elems
+    return hashlib.sha256(b"\x30" + _der_len(len(inner)) + inner).digest()
+
+
+def test_commit_signatures_digest_matches_go_asn1():
+    """CommitSignaturesDigest (internal/bft/util.go:557-579) against the Go-asn1 restatement:
+    nil for no signatures, the reference tests' {Signer: 1}, {Signer: 2}, {Signer: 3}
+    (view_test.go:227), signer ids across the int64 length steps and above 2^63 (the Go code
+    casts to int64), and value/msg lengths across the DER short/long length forms."""
+    S = plugin.Signature
+    assert plugin.CommitSignaturesDigest([]) is None
+    three = [S(1, b"", b""), S(2, b"", b""), S(3, b"", b"")]
+    assert plugin.CommitSignaturesDigest(three) == _go_commit_sigs_digest(three)
+    import random
+    rng = random.Random(11)
+    ids = [0, 1, 127, 128, 255, 256, 65535, (1 << 63) - 1, 1 << 63, (1 << 64) - 1]
+    lens = [0, 1, 71, 72, 127, 128, 255, 256, 70000]
+    for n in (1, 2, 5, 67, 300):
+        sigs = [S(rng.choice(ids) if rng.random() < 0.5 else rng.randrange(1 << 64),
+                  rng.randbytes(rng.choice(lens)), rng.randbytes(rng.choice(lens))) for _ in range(n)]
+        assert plugin.CommitSignaturesDigest(sigs) == _go_commit_sigs_digest(sigs), n
+
+
 def test_host_sha256():
     """Host SHA-256 (SHA-NI when the CPU has it) against hashlib: every length 0..300, then
     random lengths up to 200 KB."""
