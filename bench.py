@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer rate")
     ap.add_argument("--sha-messages", type=int, default=2_097_152,
                     help="config 5: 16M requests over 8 GPUs = 2M per GPU (~68 GB of payload in HBM)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for the barrier and the max-time reduction (no data-path "
+                         "collective); gloo lets a one-GPU box rehearse the torchrun path with "
+                         "several ranks on its one device")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_verify_latest.json"))
     return ap.parse_args()
 
@@ -446,8 +450,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+        # one GPU per rank on the node; a box with fewer devices than ranks (a gloo rehearsal)
+        # maps ranks onto its devices round-robin
+        local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
@@ -510,7 +520,8 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        elapsed, mismatches = reduce_timing(elapsed, mismatches, device=dev)
+        elapsed, mismatches = reduce_timing(elapsed, mismatches,
+                                            device=dev if args.dist_backend == "nccl" else None)
     step_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     avg_step_gpu_ms = sum(step_ms) / len(step_ms)
     launches, kern_total_ms = gv.kernel_time()
