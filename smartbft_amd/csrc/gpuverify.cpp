@@ -161,31 +161,69 @@ struct Slot {
     uint8_t* pin = nullptr;
     size_t pin_cap = 0;
     // mapped, coherent (fine-grained) host memory for the zero-copy keyed path: the kernel
-    // reads its inputs and writes its verdicts here over PCIe (keyed_zero_copy)
-    uint8_t* zc = nullptr;
-    uint8_t* zc_dev = nullptr;
-    size_t zc_cap = 0;
-    int reserve_zc(size_t bytes) {
-        if (bytes <= zc_cap) return SBFT_GV_OK;
-        if (zc) {
-            (void)hipStreamSynchronize(stream);  // the last kernel that read it has drained
-            (void)hipHostFree(zc);
+    // reads its inputs and writes its verdicts here over PCIe (enqueue_keyed). Several lanes,
+    // each with its own stream and buffer and lock, and none holds `mu`: concurrent small
+    // batches (the consenter coalescer's back-to-back batches, quorum calls of different
+    // decisions) run side by side on the device instead of queueing behind one another.
+    struct ZcLane {
+        std::mutex mu;
+        hipStream_t stream = nullptr;
+        uint8_t* host = nullptr;
+        uint8_t* dev = nullptr;
+        size_t cap = 0;
+        // caller holds mu and has selected the slot's device
+        int reserve(size_t bytes) {
+            if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+                stream = nullptr;
+                return SBFT_GV_EDEVICE;
+            }
+            if (bytes <= cap) return SBFT_GV_OK;
+            if (host) {
+                (void)hipStreamSynchronize(stream);  // the last kernel that read it has drained
+                (void)hipHostFree(host);
+            }
+            host = dev = nullptr;
+            cap = 0;
+            size_t want = std::max(bytes, (size_t)1 << 18);
+            want = (want + 4095) & ~(size_t)4095;
+            if (hipHostMalloc((void**)&host, want, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+                host = nullptr;
+                return SBFT_GV_ENOMEM;
+            }
+            if (hipHostGetDevicePointer((void**)&dev, host, 0) != hipSuccess) {
+                (void)hipHostFree(host);
+                host = nullptr;
+                return SBFT_GV_EDEVICE;
+            }
+            cap = want;
+            return SBFT_GV_OK;
         }
-        zc = zc_dev = nullptr;
-        zc_cap = 0;
-        size_t want = std::max(bytes, (size_t)1 << 18);
-        want = (want + 4095) & ~(size_t)4095;
-        if (hipHostMalloc((void**)&zc, want, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
-            zc = nullptr;
-            return SBFT_GV_ENOMEM;
+        void release() {
+            if (stream) (void)hipStreamSynchronize(stream);
+            if (host) (void)hipHostFree(host);
+            if (stream) (void)hipStreamDestroy(stream);
+            host = dev = nullptr;
+            stream = nullptr;
+            cap = 0;
         }
-        if (hipHostGetDevicePointer((void**)&zc_dev, zc, 0) != hipSuccess) {
-            (void)hipHostFree(zc);
-            zc = nullptr;
-            return SBFT_GV_EDEVICE;
+    };
+    static constexpr int kZcLanes = 4;
+    ZcLane zcl[kZcLanes];
+    std::atomic<uint32_t> zc_rr{0};
+    // A free lane (locked into lk), or, when all are busy, the next one in turn (waits for it).
+    ZcLane& acquire_zc(std::unique_lock<std::mutex>& lk) {
+        const uint32_t s = zc_rr.fetch_add(1, std::memory_order_relaxed);
+        for (int i = 0; i < kZcLanes; ++i) {
+            ZcLane& z = zcl[(s + i) % kZcLanes];
+            std::unique_lock<std::mutex> t(z.mu, std::try_to_lock);
+            if (t.owns_lock()) {
+                lk = std::move(t);
+                return z;
+            }
         }
-        zc_cap = want;
-        return SBFT_GV_OK;
+        ZcLane& z = zcl[s % kZcLanes];
+        lk = std::unique_lock<std::mutex>(z.mu);
+        return z;
     }
     // fixed-base comb table for u1*G of the generic verify (p256_verify.hip), built on first use
     std::mutex gcomb_mu;
@@ -431,7 +469,7 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
         if (s->d_keytab) (void)hipFree(s->d_keytab);
         for (void* t : s->retired) (void)hipFree(t);
         if (s->pin) (void)hipHostFree(s->pin);
-        if (s->zc) (void)hipHostFree(s->zc);
+        for (auto& z : s->zcl) z.release();
         if (s->gcomb) (void)hipFree(s->gcomb);
         for (auto& kv : s->ws) {
             (void)hipStreamSynchronize(kv.first);
@@ -1381,8 +1419,10 @@ int build_tables(Slot* sl, const std::vector<std::array<uint8_t, 64>>& keys, siz
 //     commit-quorum call). A fault is caught by polling the stream now and then.
 int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t blob_len, const uint64_t* off,
                   const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint32_t* key, uint32_t nkeys,
-                  bool zc, uint8_t* ok_out, size_t lanes_min) {
+                  void** keytab, Slot::ZcLane* zl, uint8_t* ok_out, size_t lanes_min) {
     Slot* sl = c.slot;
+    const bool zc = zl != nullptr;
+    hipStream_t st = zc ? zl->stream : sl->stream;  // (the lane's stream is created by its reserve)
     const size_t n = c.count, b = c.begin;
     static const bool trace = getenv("SBFT_KEYED_TRACE") != nullptr;  // diagnostics
     const auto t0 = std::chrono::steady_clock::now();
@@ -1408,10 +1448,11 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
     int rc;
     uint8_t *h, *d;
     if (zc) {
-        rc = sl->reserve_zc(in_bytes + fok);
+        rc = zl->reserve(in_bytes + fok);
         if (rc) return rc;
-        h = sl->zc;
-        d = sl->zc_dev;
+        st = zl->stream;
+        h = zl->host;
+        d = zl->dev;
     } else {
         rc = sl->reserve(in_bytes + fok + fextra);
         if (rc) return rc;
@@ -1438,7 +1479,7 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
         std::memset((void*)okh, 0, n);
         std::atomic_thread_fence(std::memory_order_seq_cst);
     } else {
-        HIPCHK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, sl->stream));
+        HIPCHK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st));
     }
     const uint8_t* dm = d + 2 * f32 + fk;
     const uint8_t* d_blob = blob ? dm : nullptr;
@@ -1450,21 +1491,21 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
         uint8_t* x = d + in_bytes + fok;  // hash counter | digests
         const uint8_t* dig = dm;
         if (blob) {
-            if (sbft_launch_sha256(d_blob, d_off, d_len, nullptr, x + 256, (uint32_t)n, (uint32_t*)x, sl->stream))
+            if (sbft_launch_sha256(d_blob, d_off, d_len, nullptr, x + 256, (uint32_t)n, (uint32_t*)x, st))
                 return SBFT_GV_ELAUNCH;
             dig = x + 256;
         }
         if (sbft_launch_p256_verify_keyed_lanes(dig, d, d + f32, (const uint32_t*)(d + 2 * f32),
-                                                (const void* const*)sl->d_keytab, nkeys, d_ok, (uint32_t)n,
-                                                sl->stream))
+                                                (const void* const*)keytab, nkeys, d_ok, (uint32_t)n,
+                                                st))
             return SBFT_GV_ELAUNCH;
     } else if (sbft_launch_p256_verify_keyed(blob ? nullptr : dm, d_blob, d_off, d_len, d, d + f32,
-                                             (const uint32_t*)(d + 2 * f32), (const void* const*)sl->d_keytab, nkeys,
-                                             d_ok, (uint32_t)n, zc ? 2 : 0, sl->stream)) {
+                                             (const uint32_t*)(d + 2 * f32), (const void* const*)keytab, nkeys,
+                                             d_ok, (uint32_t)n, zc ? 2 : 0, st)) {
         return SBFT_GV_ELAUNCH;
     }
     if (!zc) {
-        HIPCHK(hipMemcpyAsync(h + in_bytes, d_ok, n, hipMemcpyDeviceToHost, sl->stream));
+        HIPCHK(hipMemcpyAsync(h + in_bytes, d_ok, n, hipMemcpyDeviceToHost, st));
         c.out_off = in_bytes;
         return SBFT_GV_OK;
     }
@@ -1479,7 +1520,7 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
         }
         cpu_relax();
         if ((spin & 4095u) == 0) {  // every few ms at worst: has the launch failed or ended short?
-            const hipError_t q = hipStreamQuery(sl->stream);
+            const hipError_t q = hipStreamQuery(st);
             if (q == hipSuccess) {
                 std::atomic_thread_fence(std::memory_order_seq_cst);
                 for (; seen < n && okh[seen]; ++seen) {
@@ -1523,13 +1564,24 @@ int run_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* blob, size
     std::vector<Chunk> chunks = plan(ctx, n);
     return for_each_device(chunks.size(), [&](size_t i) {
         Chunk& c = chunks[i];
+        if (c.count <= ctx->keyed_zc_max) {
+            // zero-copy: the slot lock only for the tables, then a lane of its own
+            void** keytab;
+            {
+                std::lock_guard<std::mutex> lk(c.slot->mu);
+                const int rc = ensure_tables(c.slot, nkeys);
+                if (rc) return rc;
+                keytab = c.slot->d_keytab;  // entries [0, nkeys) never change; old arrays are retired
+            }
+            std::unique_lock<std::mutex> zlk;
+            Slot::ZcLane& zl = c.slot->acquire_zc(zlk);
+            return enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, keytab, &zl, ok_out, 0);
+        }
         std::lock_guard<std::mutex> lk(c.slot->mu);
         int rc = ensure_tables(c.slot, nkeys);
-        if (rc == SBFT_GV_OK && c.count <= ctx->keyed_zc_max)
-            return enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, true, ok_out, 0);
         if (rc == SBFT_GV_OK)
-            rc = enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, false, ok_out,
-                               ctx->keyed_lanes_min);
+            rc = enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, c.slot->d_keytab, nullptr,
+                               ok_out, ctx->keyed_lanes_min);
         (void)hipSetDevice(c.slot->device);
         if (hipStreamSynchronize(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
         // the verdicts sit in the slot's pinned staging, which the lock still protects
