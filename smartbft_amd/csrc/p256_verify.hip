@@ -9,8 +9,8 @@
 //   4. R = u2*Q + u1*G. u2*Q: 256 doublings with radix-16 regular signed-odd digits (never
 //      zero, so every addition is live and select-free) over [1,3,..,15]Q, built per lane with
 //      co-Z additions and made affine with one safegcd inversion mod p (scratch; 64 mixed
-//      additions). u1*G: 17 mixed additions from a 16-window fixed-base comb table in HBM
-//      (built once per device), after the ladder
+//      additions). u1*G: K + 1 mixed additions from a fixed-base comb table of K W-bit windows
+//      in HBM (built once per device), after the ladder
 //   5. R = infinity -> reject; accept iff X == r*Z^2 or (r+n < p and X == (r+n)*Z^2)
 // Exceptional additions (P + P, P + (-P), infinity) leave Z = 0; such lanes are re-verified by
 // the fully case-split p256_verify_fixup_kernel, so adversarial inputs cost only themselves.
@@ -383,13 +383,22 @@ __global__ __launch_bounds__(256) void p256_sinv_totals_kernel(uint32_t nb, sinv
 }
 
 // ------------------------------------------------------------ fixed-base comb for u1*G
-// u1*G is summed from a 16-window comb table in HBM after the Q ladder (17 mixed additions,
-// no doublings). The 33 radix-256 additions of an LDS table inside the ladder it replaced
-// were 1.6 M instructions per 1,000 verifies more.
-#define SBFT_GCOMB_WINDOWS 16
-#define SBFT_GCOMB_ENTRIES 32768  // odd digits 1, 3, ..., 65535
+// u1*G is summed from a comb table in HBM after the Q ladder (K + 1 mixed additions, no
+// doublings): W-bit windows, K = ceil(256 / W) of them, 2^(W-1) odd multiples each. The 33
+// radix-256 additions of an LDS table inside the ladder it replaced were 1.6 M instructions per
+// 1,000 verifies more. Wider windows trade HBM for additions (entries are gathered, never
+// scanned): W = 16: 17 additions, 42 MB; W = 20: 14, 0.55 GB; W = 24: 12, 7.4 GB.
+#ifndef SBFT_GCOMB_W
+#define SBFT_GCOMB_W 16
+#endif
+#define SBFT_GCOMB_WINDOWS ((256 + SBFT_GCOMB_W - 1) / SBFT_GCOMB_W)
+#define SBFT_GCOMB_ENTRIES (1u << (SBFT_GCOMB_W - 1))  // odd digits 1, 3, ..., 2^W - 1
 // entry = 20 words (80 B, five 16-B loads): x limbs 0..8, pad, y limbs 0..8, pad (f29 Montgomery)
-#define SBFT_GCOMB_BYTES ((size_t)(SBFT_GCOMB_WINDOWS * SBFT_GCOMB_ENTRIES + 1) * 80)
+#define SBFT_GCOMB_BYTES ((size_t)(SBFT_GCOMB_WINDOWS * (size_t)SBFT_GCOMB_ENTRIES + 1) * 80)
+static_assert(SBFT_GCOMB_W >= 8 && SBFT_GCOMB_W <= 26, "window bits: digits are read from one 32-bit word");
+constexpr int kGWin = SBFT_GCOMB_W;
+constexpr int kGK = SBFT_GCOMB_WINDOWS;  // windows; entry kGK of the table is 2^(W K) G
+constexpr u32 kGMask = (1u << SBFT_GCOMB_W) - 1u;
 
 // affine (x, y) of P as canonical plain integers (8 x 32 domain; one Fermat inversion)
 SBFT_DEV void comb_affine(fe& x, fe& y, const jp& p) {
@@ -406,9 +415,36 @@ SBFT_DEV void comb_affine(fe& x, fe& y, const jp& p) {
     fp_canon(y, t);
 }
 
-// table[w][j] = (2j+1) 2^(16 w) G for w < 16, j < 32768; table[16][0] = 2^256 G. One point
-// per thread through the (case-split) fixed-base multiplication of the signer; built once per
-// device (~42 MB of the 288 GB).
+// 2^e mod n (e <= 280) by modular doubling
+SBFT_DEV fe pow2_mod_n(uint32_t e) {
+    fe x = fe_zero();
+    x.v[0] = 1;
+#pragma unroll 1
+    for (uint32_t i = 0; i < e; ++i) {
+        fe t, d;
+        u32 c = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            t.v[k] = (x.v[k] << 1) | c;
+            c = x.v[k] >> 31;
+        }
+        u64 bw = 0;  // 2x < 2n: subtract n once if 2x >= n
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const u64 v = (u64)t.v[k] - P256_N[k] - bw;
+            d.v[k] = lo32(v);
+            bw = v >> 63;
+        }
+        const bool ge = c || !bw;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x.v[k] = ge ? d.v[k] : t.v[k];
+    }
+    return x;
+}
+
+// table[w][j] = (2j+1) 2^(W w) G for w < K, j < 2^(W-1); table[K][0] = 2^(W K) G. One point per
+// thread through the (case-split) fixed-base multiplication of the signer; built once per
+// device.
 __global__ __launch_bounds__(256) void p256_gcomb_build_kernel(uint4* __restrict__ table) {
     __shared__ u32 gtab4[2 * 8 * P256_GTAB4_ENTRIES];
     for (int i = threadIdx.x; i < 2 * 8 * P256_GTAB4_ENTRIES; i += blockDim.x) gtab4[i] = C_GTAB[i];
@@ -416,28 +452,15 @@ __global__ __launch_bounds__(256) void p256_gcomb_build_kernel(uint4* __restrict
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t total = SBFT_GCOMB_WINDOWS * SBFT_GCOMB_ENTRIES + 1;
     if (gid >= total) return;
-    fe d = fe_zero();
-    if (gid < SBFT_GCOMB_WINDOWS * SBFT_GCOMB_ENTRIES) {
-        const uint32_t w = gid / SBFT_GCOMB_ENTRIES, j = gid % SBFT_GCOMB_ENTRIES;
-        const uint32_t odd = 2 * j + 1, bit = 16 * w;
-        d.v[bit >> 5] = odd << (bit & 31);  // 16 w is 0 or 16 mod 32: no spill into the next limb
-        if (!fe_lt(d, P256_N)) {           // < 2^256 < 2n: one subtraction
-            u64 b = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const u64 t = (u64)d.v[k] - P256_N[k] - b;
-                d.v[k] = lo32(t);
-                b = t >> 63;
-            }
-        }
-    } else {  // 2^256 mod n = 2^256 - n
-        u64 b = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const u64 t = (u64)0 - P256_N[k] - b;
-            d.v[k] = lo32(t);
-            b = t >> 63;
-        }
+    // scalar (2j + 1) 2^(W w) mod n: 2^(W w) mod n into Montgomery form, times the odd digit
+    const uint32_t w = gid / SBFT_GCOMB_ENTRIES, j = gid % SBFT_GCOMB_ENTRIES;
+    fe d = pow2_mod_n((uint32_t)kGWin * w);
+    if (w < (uint32_t)kGK) {
+        fe odd = fe_zero();
+        odd.v[0] = 2 * j + 1;
+        fn_mul(d, d, fe_const(C_R2N));  // 2^(W w) R
+        fn_mul(d, d, odd);              // (2j + 1) 2^(W w)
+        fn_canon(d, d);
     }
     jp P;
     bool inf;
@@ -688,9 +711,9 @@ SBFT_DEV int q_digit(const fe& k2, int i) {
     return 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & (2 * kQTab - 1)) - (2 * kQTab - 1);
 }
 
-// u1*G by the fixed-base comb in HBM (no doublings): u1 = sum_{i<16} d_i 2^(16 i) + 2^256
-// with d_i = 2*((u1 >> (16 i + 1)) & 0xFFFF) - 0xFFFF (odd, nonzero), i.e. 16 mixed additions
-// of table[i][(|d_i| - 1) / 2] = |d_i| 2^(16 i) G plus one of table[16][0] = 2^256 G.
+// u1*G by the fixed-base comb in HBM (no doublings): u1 = sum_{i<K} d_i 2^(W i) + 2^(W K) with
+// d_i = 2*((u1 >> (W i + 1)) & (2^W - 1)) - (2^W - 1) (odd, nonzero), i.e. K mixed additions of
+// table[i][(|d_i| - 1) / 2] = |d_i| 2^(W i) G plus one of table[K][0] = 2^(W K) G.
 // The next entry's five 16-B loads are issued before the current addition. add(acc, x, y) is
 // the mixed addition of the calling kernel.
 // PINGPONG (latency kernel): two entry buffers in fixed registers, loop unrolled by two, so
@@ -698,23 +721,24 @@ SBFT_DEV int q_digit(const fe& k2, int i) {
 // the rotated one-buffer loop exposed an HBM round trip per addition).
 template <bool PINGPONG = false, class AddAff>
 SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __restrict__ gcomb, AddAff add) {
+    constexpr int T = kGK + 1;  // entries summed
     fe k1 = u1;
     uint4 cur[5], nxt[5];
     int dneg_cur = 0, dneg_nxt = 0;
     // digit i of u1 -> (entry pointer, negative?)
     auto digit = [&](int i, const uint4*& ptr, int& neg) {
-        if (i < 16) {
-            const u32 bits = (k1.v[0] >> 1) & 0xFFFFu;  // bits 16i+1 .. 16i+16 (k1 shifted)
-            const int d = 2 * (int)bits - 0xFFFF;
+        if (i < kGK) {
+            const u32 bits = (k1.v[0] >> 1) & kGMask;  // bits W i + 1 .. W i + W (k1 shifted)
+            const int d = 2 * (int)bits - (int)kGMask;
             const u32 j = (u32)((d < 0 ? -d : d) >> 1);
             ptr = gcomb + ((size_t)i * SBFT_GCOMB_ENTRIES + j) * 5;
             neg = d < 0;
-            // k1 >>= 16 for the next window
+            // k1 >>= W for the next window
 #pragma unroll
-            for (int k = 0; k < 7; ++k) k1.v[k] = __builtin_amdgcn_alignbit(k1.v[k + 1], k1.v[k], 16);
-            k1.v[7] >>= 16;
+            for (int k = 0; k < 7; ++k) k1.v[k] = __builtin_amdgcn_alignbit(k1.v[k + 1], k1.v[k], kGWin);
+            k1.v[7] >>= kGWin;
         } else {
-            ptr = gcomb + (size_t)16 * SBFT_GCOMB_ENTRIES * 5;
+            ptr = gcomb + (size_t)kGK * SBFT_GCOMB_ENTRIES * 5;
             neg = 0;
         }
     };
@@ -734,29 +758,32 @@ SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __re
         digit(0, ptr, dneg_cur);
 #pragma unroll
         for (int k = 0; k < 5; ++k) cur[k] = ptr[k];
+        int i = 0;
 #pragma unroll 1
-        for (int i = 0; i < 16; i += 2) {
+        for (; i + 1 < T; i += 2) {
             digit(i + 1, ptr, dneg_nxt);
 #pragma unroll
             for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
             add_entry(cur, dneg_cur);
-            digit(i + 2, ptr, dneg_cur);  // i + 2 <= 16: entry 16 is 2^256 G
+            if (i + 2 < T) {
+                digit(i + 2, ptr, dneg_cur);
 #pragma unroll
-            for (int k = 0; k < 5; ++k) cur[k] = ptr[k];
+                for (int k = 0; k < 5; ++k) cur[k] = ptr[k];
+            }
             add_entry(nxt, dneg_nxt);
         }
-        add_entry(cur, dneg_cur);
+        if (i < T) add_entry(cur, dneg_cur);  // odd entry count: the last one
         return;
     }
     digit(0, ptr, dneg_nxt);
 #pragma unroll
     for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
 #pragma unroll 1
-    for (int i = 0; i < 17; ++i) {
+    for (int i = 0; i < T; ++i) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) cur[k] = nxt[k];
         dneg_cur = dneg_nxt;
-        if (i < 16) {
+        if (i + 1 < T) {
             digit(i + 1, ptr, dneg_nxt);
 #pragma unroll
             for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
@@ -931,17 +958,17 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
         verify_scalars(w, valid, e_raw, r, u1, u2, neg1, neg2);
     }
 
-    // comb entry i of u1 (see comb_add_u1g): |d_i| 2^(16 i) G for i < 16, 2^256 G for i = 16
+    // comb entry i of u1 (see comb_add_u1g): |d_i| 2^(W i) G for i < K, 2^(W K) G for i = K
     auto comb_entry = [&](int i, uint4 (&en)[5], bool& dneg) {
         const uint4* ptr;
-        if (i < 16) {
-            const int b = 16 * i + 1, lw = b >> 5;
+        if (i < kGK) {
+            const int b = kGWin * i + 1, lw = b >> 5;
             const u32 lo = u1.v[lw], hi = lw < 7 ? u1.v[lw + 1] : 0u;
-            const int d = 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & 0xFFFFu) - 0xFFFF;
+            const int d = 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & kGMask) - (int)kGMask;
             ptr = gcomb + ((size_t)i * SBFT_GCOMB_ENTRIES + (u32)((d < 0 ? -d : d) >> 1)) * 5;
             dneg = d < 0;
         } else {
-            ptr = gcomb + (size_t)16 * SBFT_GCOMB_ENTRIES * 5;
+            ptr = gcomb + (size_t)kGK * SBFT_GCOMB_ENTRIES * 5;
             dneg = false;
         }
 #pragma unroll
@@ -968,10 +995,11 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
     // quad: the tuple's 17 comb points (signs applied) staged in LDS over the divstep table,
     // which the inversions are done with: [entry][x limbs, y limbs][tuple]
     u32* const ctab = dtab;
-    static_assert(!kQuad || 17 * 18 * kTuples <= SBFT_DIVSTEP5_WORDS, "comb points fit the divstep table");
+    static_assert(!kQuad || (kGK + 1) * 18 * kTuples <= SBFT_DIVSTEP5_WORDS, "comb points fit the divstep table");
+    static_assert(!kQuad || kGK <= kQDigits, "the comb lanes take one entry per ladder digit");
     if constexpr (kQuad) {
         __syncthreads();  // every lane of the workgroup is past its inversions
-        for (int e = threadIdx.x & 3; e < 17; e += 4) {
+        for (int e = threadIdx.x & 3; e < kGK + 1; e += 4) {
             uint4 en[5];
             bool dn;
             comb_entry(e, en, dn);
@@ -1018,8 +1046,8 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
         }
         if ((d2 < 0) != neg2) f29_neg(y2, y2);
         if constexpr (kQuad) {
-            // comb lanes: entry j + 1 while j + 1 <= 16, then their accumulator is final
-            const int ce = j + 1 <= 16 ? j + 1 : 16;
+            // comb lanes: entry j + 1 while j + 1 <= K, then their accumulator is final
+            const int ce = j + 1 <= kGK ? j + 1 : kGK;
             if (comb_role)
 #pragma unroll
                 for (int k = 0; k < 9; ++k) {
@@ -1028,7 +1056,7 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
                 }
             jp29 tt = acc;
             p29_add_aff_pair(tt, x2, y2, odd);
-            if (!comb_role || j + 1 <= 16) acc = tt;
+            if (!comb_role || j + 1 <= kGK) acc = tt;
         } else {
             p29_add_aff_pair(acc, x2, y2, odd);
         }
