@@ -45,6 +45,7 @@ extern "C" {
 #define SBFT_GV_ENOMEM (-3)     /* device or pinned allocation failed */
 #define SBFT_GV_ELAUNCH (-4)    /* kernel launch failed */
 #define SBFT_GV_EDEVICE (-5)    /* HIP runtime error during copy/sync */
+#define SBFT_GV_ESELFTEST (-6)  /* sbft_gv_init: a device failed the engine's known-answer self-test */
 
 typedef struct sbft_gv_ctx sbft_gv_ctx;
 

@@ -406,6 +406,68 @@ static const std::array<uint8_t, 64> kGXY = {
     0x4f, 0xe3, 0x42, 0xe2, 0xfe, 0x1a, 0x7f, 0x9b, 0x8e, 0xe7, 0xeb, 0x4a, 0x7c, 0x0f, 0x9e, 0x16,
     0x2b, 0xce, 0x33, 0x57, 0x6b, 0x31, 0x5e, 0xce, 0xcb, 0xb6, 0x40, 0x68, 0x37, 0xbf, 0x51, 0xf5};
 
+#define HIPCHK(x)                                   \
+    do {                                            \
+        if ((x) != hipSuccess) return SBFT_GV_EDEVICE; \
+    } while (0)
+
+#include "p256_post_vectors.inc"
+
+// Power-on self-test (sbft_gv_init, every device; SBFT_GV_SELFTEST=0 skips it): 72 known-answer
+// tuples (tools/gen_post_vectors.py: four of every golden-fixture category, including R = infinity
+// and Shamir-exceptional ones for the fix-up kernel) through the throughput kernel and both
+// latency kernels, and six SHA-256 known answers at unaligned offsets. The radix-2^29 field code
+// relies on the compiler not seeing its limb ranges (p256_f29.hpp: ROCm 7.2 miscompiled the
+// range-visible form): a toolchain or driver that breaks it makes the context refuse to start
+// (SBFT_GV_ESELFTEST) instead of returning wrong verdicts.
+static int power_on_selftest(Slot* sl) {
+    HIPCHK(hipSetDevice(sl->device));
+    const size_t n = SBFT_POST_N;
+    const size_t f = align_up(32 * n, 256), fo = align_up(n, 256);
+    int rc = sl->reserve(5 * f + fo + sbft_verify_work_bytes(n));
+    if (rc) return rc;
+    const void* gcomb = sl->gcomb_table();
+    if (!gcomb) return SBFT_GV_ENOMEM;
+    std::vector<uint8_t> h(5 * f, 0), ok(n);
+    for (size_t k = 0; k < n; ++k)
+        for (int fld = 0; fld < 5; ++fld) std::memcpy(&h[fld * f + 32 * k], kPostVectors[k] + 32 * fld, 32);
+    uint8_t* base = sl->dbuf;
+    uint32_t* work = (uint32_t*)(base + 5 * f + fo);
+    HIPCHK(hipMemcpyAsync(base, h.data(), 5 * f, hipMemcpyHostToDevice, sl->stream));
+    for (int lanes : {1, 2, 4}) {
+        HIPCHK(hipMemsetAsync(base + 5 * f, 0xEE, n, sl->stream));
+        if (sbft_launch_p256_verify(base, base + f, base + 2 * f, base + 3 * f, base + 4 * f, base + 5 * f, (uint32_t)n,
+                                    work, gcomb, sl->stream, nullptr, nullptr, lanes))
+            return SBFT_GV_ELAUNCH;
+        HIPCHK(hipMemcpyAsync(ok.data(), base + 5 * f, n, hipMemcpyDeviceToHost, sl->stream));
+        HIPCHK(hipStreamSynchronize(sl->stream));
+        for (size_t k = 0; k < n; ++k)
+            if (ok[k] != kPostVectors[k][160]) return SBFT_GV_ESELFTEST;
+    }
+    // SHA-256: blob (+ the kernel's over-read pad) | off | len | counter | digests
+    const size_t m = SBFT_POST_SHA_N, fb = align_up(SBFT_POST_SHA_BLOB + SBFT_GV_SHA_BLOB_PAD, 256);
+    if ((rc = sl->reserve(fb + 3 * 256 + 32 * m))) return rc;
+    uint8_t* b = sl->dbuf;
+    std::vector<uint8_t> blob(fb, 0);
+    std::memcpy(blob.data(), kPostShaBlob, SBFT_POST_SHA_BLOB);
+    uint64_t off[SBFT_POST_SHA_N];
+    uint32_t len[SBFT_POST_SHA_N];
+    for (size_t k = 0; k < m; ++k) {
+        off[k] = kPostShaOff[k];
+        len[k] = kPostShaLen[k];
+    }
+    uint8_t dig[SBFT_POST_SHA_N][32];
+    HIPCHK(hipMemcpyAsync(b, blob.data(), fb, hipMemcpyHostToDevice, sl->stream));
+    HIPCHK(hipMemcpyAsync(b + fb, off, sizeof off, hipMemcpyHostToDevice, sl->stream));
+    HIPCHK(hipMemcpyAsync(b + fb + 256, len, sizeof len, hipMemcpyHostToDevice, sl->stream));
+    if (sbft_launch_sha256(b, (const uint64_t*)(b + fb), (const uint32_t*)(b + fb + 256), nullptr, b + fb + 768,
+                           (uint32_t)m, (uint32_t*)(b + fb + 512), sl->stream))
+        return SBFT_GV_ELAUNCH;
+    HIPCHK(hipMemcpyAsync(dig, b + fb + 768, sizeof dig, hipMemcpyDeviceToHost, sl->stream));
+    HIPCHK(hipStreamSynchronize(sl->stream));
+    return std::memcmp(dig, kPostShaDigest, sizeof dig) == 0 ? SBFT_GV_OK : SBFT_GV_ESELFTEST;
+}
+
 extern "C" {
 
 const char* sbft_gv_strerror(int code) {
@@ -416,6 +478,7 @@ const char* sbft_gv_strerror(int code) {
     case SBFT_GV_ENOMEM: return "allocation failed";
     case SBFT_GV_ELAUNCH: return "kernel launch failed";
     case SBFT_GV_EDEVICE: return "HIP runtime error";
+    case SBFT_GV_ESELFTEST: return "device failed the known-answer self-test";
     default: return "unknown error";
     }
 }
@@ -451,6 +514,16 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     // key id 0: the generator G (its comb table serves u1*G on the keyed path)
     ctx->keys.push_back(kGXY);
     ctx->key_valid.push_back(1);
+    const char* st = getenv("SBFT_GV_SELFTEST");
+    if (!st || std::strcmp(st, "0") != 0) {
+        for (Slot* sl : ctx->slots) {
+            const int rc = power_on_selftest(sl);
+            if (rc) {
+                sbft_gv_destroy(ctx);
+                return rc;
+            }
+        }
+    }
     *out = ctx;
     return SBFT_GV_OK;
 }
@@ -700,11 +773,6 @@ int for_each_device(size_t m, F&& f) {
         if (r) return r;
     return SBFT_GV_OK;
 }
-
-#define HIPCHK(x)                                   \
-    do {                                            \
-        if ((x) != hipSuccess) return SBFT_GV_EDEVICE; \
-    } while (0)
 
 // Enqueue verify of tuples [c.begin, c.begin+c.count) on c.slot. Layout of the slot
 // buffer: digest | r | s | qx | qy | ok, each array 256-byte aligned.

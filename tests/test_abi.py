@@ -5,6 +5,7 @@ import glob
 import os
 import re
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -51,6 +52,7 @@ def test_strerror_and_no_gpu_failure_is_loud():
     from smartbft_amd import gpuverify
     lib = gpuverify.load_library()
     assert lib.sbft_gv_strerror(-2) == b"no usable GPU"
+    assert lib.sbft_gv_strerror(-6) == b"device failed the known-answer self-test"
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present: the no-GPU error path is not reachable")
@@ -102,3 +104,27 @@ def test_go_binding_uses_only_declared_symbols():
               "RequestsFromProposal", "AuxiliaryData", "Sign", "SignProposal", "VerifyConsenterSigs"]:
         assert re.search(r"func \(\w+ \*(Verifier|Signer)\) %s\(" % m, go), m
     assert "elided" not in go
+
+
+def test_power_on_selftest_vectors_match_fixtures():
+    """The engine's init-time known-answer records (smartbft_amd/csrc/p256_post_vectors.inc,
+    tools/gen_post_vectors.py) are fixture records with the fixtures' verdicts, and its SHA-256
+    answers are hashlib's: a stale or hand-edited table would make every context refuse to start."""
+    import hashlib
+    import re
+    text = open(os.path.join(ROOT, "smartbft_amd", "csrc", "p256_post_vectors.inc")).read()
+    body = text[text.index("kPostVectors"):text.index("};")]
+    recs = [bytes(int(x, 16) for x in m.split(",")) for m in re.findall(r"\{([0-9a-fx,]+)\}", body)]
+    raw = np.fromfile(os.path.join(ROOT, "tests", "golden", "p256_vectors.bin"), dtype=np.uint8).reshape(-1, 162)
+    fixtures = {bytes(r[:160]): int(r[160]) for r in raw}
+    assert len(recs) == int(re.search(r"SBFT_POST_N (\d+)", text).group(1)) >= 64
+    for r in recs:
+        assert len(r) == 161 and fixtures[r[:160]] == r[160]
+    cats = set(int(r[161]) for r in raw if bytes(r[:160]) in {x[:160] for x in recs})
+    assert len(cats) == 18  # every category, the exceptional ones included
+    blob = bytes(int(x, 16) for x in re.findall(r"0x([0-9a-f]{2})", text[text.index("kPostShaBlob"):text.index("kPostShaOff")]))
+    off = [int(x) for x in re.search(r"kPostShaOff\[SBFT_POST_SHA_N\] = \{([^}]*)\}", text).group(1).split(",")]
+    ln = [int(x) for x in re.search(r"kPostShaLen\[SBFT_POST_SHA_N\] = \{([^}]*)\}", text).group(1).split(",")]
+    dig = text[text.index("kPostShaDigest"):]
+    digs = [bytes(int(x, 16) for x in m.split(",")) for m in re.findall(r"\{([0-9a-fx,]+)\}", dig)]
+    assert [hashlib.sha256(blob[o:o + n]).digest() for o, n in zip(off, ln)] == digs
