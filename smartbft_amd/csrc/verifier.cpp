@@ -31,6 +31,7 @@
 
 #include <climits>
 #include <linux/futex.h>
+#include <sched.h>
 #include <sys/prctl.h>
 #include <sys/random.h>
 #include <sys/syscall.h>
@@ -555,6 +556,7 @@ struct sbft_verifier {
         std::chrono::steady_clock::time_point t_open;  // the leader's arrival
         std::condition_variable cv;                    // wakes the leader when the batch fills
         DoneFlag done;                                 // wakes the followers when the results are published
+        DoneFlag ready;  // the batch is closed and its launch under way (pre-wake, see consenter_coalesced)
     };
     std::mutex cs_mu;
     std::shared_ptr<CsBatch> cs_open;
@@ -1136,8 +1138,25 @@ static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const 
             }
         }
     }
-    if (!leader) batch->done.wait(0);  // the batch is one launch away: sleep at once
+    static const bool prewake = [] {
+        const char* e = getenv("SBFT_CS_PREWAKE");
+        return !e || std::strcmp(e, "0") != 0;
+    }();
+    if (!leader) {
+        if (prewake) {
+            // Sleep until the leader closes the batch (the arrivals still to come need the
+            // cores), then wait out the launch awake: the leader wakes the followers (a tree)
+            // right before it stages and launches, so their wake-ups overlap the ~50 us the GPU
+            // takes instead of following it. Bounded: a long batch sleeps again.
+            batch->ready.wait(0);
+            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(400);
+            while (!batch->done.v.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < until)
+                sched_yield();
+        }
+        batch->done.wait(0);  // the batch is one launch away: sleep at once
+    }
     if (leader) {
+        if (prewake) batch->ready.set();
         static const bool trace = getenv("SBFT_CS_TRACE") != nullptr;  // diagnostics
         const auto tc = std::chrono::steady_clock::now();
         // closed: nobody else touches the entries until done is published
