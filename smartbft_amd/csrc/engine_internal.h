@@ -11,12 +11,13 @@ struct sbft_gv_ctx;
 
 // Framed hash + verify of one payload (sbft_gv_sha256_verify_p256_framed) with the host-side
 // parse overlapped with the payload's H2D copy: the copy does not need the offsets, so
-// `prepare` runs on the engine's helper thread while the caller's thread copies the payload
-// to the device. prepare fills off / len (one entry per framed message) and returns 0, or a
-// nonzero code that is returned unchanged (nothing is launched). ok receives one verdict per
-// message. Batches of min_split or more messages on a multi-device context fall back to the
+// The engine's helper thread copies the payload to the device while `prepare` runs on the
+// caller's thread. prepare fills off / len (one entry per framed message) and returns 0, or a
+// nonzero code that is returned unchanged (nothing is launched). `during` (optional) runs on
+// the caller's thread once the hash and verify launches are queued, before the call waits for
+// them. ok receives one verdict per message. Batches of min_split or more messages on a multi-device context fall back to the
 // split path after the parse.
 int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, int32_t sig_rel,
                               int32_t pub_rel,
                               const std::function<int(std::vector<uint64_t>&, std::vector<uint32_t>&)>& prepare,
-                              std::vector<uint8_t>& ok);
+                              std::vector<uint8_t>& ok, const std::function<void()>& during = nullptr);

@@ -1131,7 +1131,7 @@ int sbft_gv_sha256_verify_p256_framed(sbft_gv_ctx* ctx, const uint8_t* blob, siz
 int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, int32_t sig_rel,
                               int32_t pub_rel,
                               const std::function<int(std::vector<uint64_t>&, std::vector<uint32_t>&)>& prepare,
-                              std::vector<uint8_t>& ok) {
+                              std::vector<uint8_t>& ok, const std::function<void()>& during) {
     if (!ctx || (!blob && blob_len)) return SBFT_GV_EINVAL;
     // this thread's scratch, bound to references: a lambda running on the helper thread must
     // see these objects, not the helper's own thread_local instances
@@ -1186,6 +1186,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     if (len.size() != n || n > 0xffffffffu) return SBFT_GV_EINVAL;
     if (n >= ctx->min_split && ctx->slots.size() > 1) {  // large: the multi-device split path
         lk.unlock();
+        if (during) during();
         return sbft_gv_sha256_verify_p256_framed(ctx, blob, blob_len, off.data(), len.data(), n, sig_rel, pub_rel,
                                                  ok.data());
     }
@@ -1215,6 +1216,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
                                 sl->stream, nullptr, nullptr, ctx->lanes_for(n)))
         return SBFT_GV_ELAUNCH;
     HIPCHK(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, sl->stream));
+    if (during) during();  // the caller's host work that does not need the verdicts, under the launch
     HIPCHK(hipStreamSynchronize(sl->stream));
     return SBFT_GV_OK;
 }

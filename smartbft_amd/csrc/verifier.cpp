@@ -448,8 +448,9 @@ bool write_info(char*& w, char* end, const Req::Str& cid, const Req::Str& id) {
 
 // VerifyProposal's result: the first request with a 0 verdict fails the whole proposal (with
 // its index and ids in the message), else the RequestInfos in payload order.
+// infos == nullptr: the records were already written (info_rc is how that went)
 int finish_proposal(const std::vector<Req>& reqs, const std::vector<uint8_t>& ok, char* infos, size_t infos_cap,
-                    size_t* count, int64_t* bad_index, char* err, size_t err_cap) {
+                    size_t* count, int64_t* bad_index, char* err, size_t err_cap, int info_rc = 0) {
     const size_t n = reqs.size();
     if (ok.size() != n) return SBFT_GV_EINVAL;
     for (size_t i = 0; i < n; ++i)
@@ -459,10 +460,14 @@ int finish_proposal(const std::vector<Req>& reqs, const std::vector<uint8_t>& ok
                     reqs[i].client_id.p, reqs[i].req_id.n, reqs[i].req_id.p);
             return SBFT_V_EVERIFY;
         }
-    char* w = infos;
-    char* end = infos + infos_cap;
-    for (auto& q : reqs)
-        if (!write_info(w, end, q.client_id, q.req_id)) return SBFT_V_ESPACE;
+    if (infos) {
+        char* w = infos;
+        char* end = infos + infos_cap;
+        for (auto& q : reqs)
+            if (!write_info(w, end, q.client_id, q.req_id)) return SBFT_V_ESPACE;
+    } else if (info_rc) {
+        return info_rc;
+    }
     *count = n;
     return 0;
 }
@@ -1004,13 +1009,25 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
         registered = v->clients.count != 0;
     }
     if (v->ctx && !registered) {
-        // no registered client keys: one framed launch, the parse overlapped with the payload copy
-        const int rc = sbft_gv_framed_overlapped(v->ctx, p->payload, p->payload_len, 0, -64, prepare, ok);
+        // no registered client keys: one framed launch, the parse overlapped with the payload
+        // copy, and the RequestInfo records written while the GPU verifies (they are returned
+        // only if every request passes)
+        int info_rc = 0;
+        auto during = [&] {
+            char* w = infos;
+            char* end = infos + infos_cap;
+            for (auto& q : reqs)
+                if (!write_info(w, end, q.client_id, q.req_id)) {
+                    info_rc = SBFT_V_ESPACE;
+                    return;
+                }
+        };
+        const int rc = sbft_gv_framed_overlapped(v->ctx, p->payload, p->payload_len, 0, -64, prepare, ok, during);
         if (rc) {
             if (rc != SBFT_V_EFORMAT) put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
             return rc;
         }
-        return finish_proposal(reqs, ok, infos, infos_cap, count, bad_index, err, err_cap);
+        return finish_proposal(reqs, ok, nullptr, 0, count, bad_index, err, err_cap, info_rc);
     }
     std::vector<uint64_t>& off = scr.off;
     std::vector<uint32_t>& len = scr.len;
