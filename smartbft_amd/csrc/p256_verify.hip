@@ -17,6 +17,7 @@
 //
 // Inputs: SoA, 32-byte big-endian fields. Output: one verdict byte per tuple.
 #include <cstdio>
+#include <cstdlib>
 
 #include "p256_f29.hpp"
 #include "p256_inv.hpp"
@@ -810,13 +811,21 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
                                                           const uint8_t* __restrict__ qyy,
                                                           uint8_t* __restrict__ ok, uint32_t n,
                                                           uint32_t* __restrict__ work, sinv_ws ws,
-                                                          const uint4* __restrict__ gcomb) {
+                                                          const uint4* __restrict__ gcomb, int spread) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     inv::stage_divstep_table(dtab);  // ends with a barrier
 
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool active = gid < n;
-    const uint32_t idx = active ? gid : (n - 1);
+    // this lane's tuple: 256 per workgroup, or (spread) the grid is a whole number of resident
+    // rounds and workgroup b takes tuples [b n / G, (b + 1) n / G) (sbft_launch_p256_verify)
+    uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, end = n;
+    if (spread) {
+        const uint32_t lo = (uint32_t)((uint64_t)blockIdx.x * n / gridDim.x);
+        end = (uint32_t)((uint64_t)(blockIdx.x + 1) * n / gridDim.x);
+        gid = lo + threadIdx.x;
+        if (lo + (threadIdx.x & ~63u) >= end) return;  // a wave with no tuple (no barrier follows)
+    }
+    const bool active = gid < end;
+    const uint32_t idx = active ? gid : (end - 1);
 
     const fe e_raw = load_be32(digest + 32ull * idx);
     const fe r = load_be32(rr + 32ull * idx);
@@ -1263,6 +1272,13 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
     do {                \
     } while (0)
 #endif
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
     if (hipMemsetAsync(d_work, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     SBFT_STEP("memset");
     if (lanes < 2) {  // the small-batch kernels invert s themselves
@@ -1283,21 +1299,27 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
             hipLaunchKernelGGL(sbft::p256_verify_small_kernel<4>, dim3(sblocks), dim3(64), 0, stream, d_digest,
                                d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb);
     } else {
-        hipLaunchKernelGGL(sbft::p256_verify_kernel, dim3(blocks), dim3(threads), 0, stream, d_digest, d_r,
-                           d_s, d_qx, d_qy, d_ok, n, d_work, ws, (const uint4*)d_gcomb);
+        // Waves are issue-bound at 4 per SIMD, and all take the same time. When the last
+        // resident round would be mostly full, a whole number of rounds with the tuples spread
+        // evenly over the workgroups (a few idle lanes per wave) finishes sooner than the partial
+        // round (tools/ladder_ceiling: 1M tuples 12.94 -> 12.82 ms); a round less than ~80% full
+        // is cheaper as it is (its SIMDs run 3 waves faster than 4).
+        const unsigned slots = (unsigned)SBFT_VERIFY_WAVES * (unsigned)cus;  // resident workgroups
+        const unsigned last = blocks % slots;
+        static const bool spread_on = [] {  // SBFT_VERIFY_SPREAD=0: A/B measurement only
+            const char* e = getenv("SBFT_VERIFY_SPREAD");
+            return !e || e[0] != '0';
+        }();
+        const bool spread = spread_on && blocks > slots && last != 0 && 5u * last >= 4u * slots;
+        const unsigned grid = spread ? (blocks / slots + 1) * slots : blocks;
+        hipLaunchKernelGGL(sbft::p256_verify_kernel, dim3(grid), dim3(threads), 0, stream, d_digest, d_r, d_s,
+                           d_qx, d_qy, d_ok, n, d_work, ws, (const uint4*)d_gcomb, spread ? 1 : 0);
     }
     if (ev1 && hipEventRecord(ev1, stream) != hipSuccess) return -1;
     SBFT_STEP("verify");
     // The flagged count is known only on the device: size the grid for the worst case (every
     // tuple exceptional, e.g. a batch of crafted R = infinity signatures), capped at one
     // resident round of the chip; blocks past the count exit at once.
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
     const unsigned fix_cap = 8u * (unsigned)cus;
     const unsigned fix_blocks = blocks < fix_cap ? blocks : fix_cap;
     hipLaunchKernelGGL(sbft::p256_verify_fixup_kernel, dim3(fix_blocks), dim3(threads), 0, stream,

@@ -234,6 +234,27 @@ def test_bench_workload_properties(gpu):
     assert np.array_equal(oracle.verify_batch(*f), ok[:3000].cpu().numpy())
 
 
+@pytest.mark.parametrize("n", [262_145, 786_432, 900_000, 1_000_000])
+def test_throughput_grid_shapes(gpu, n):
+    """The throughput launch at sizes past one resident round: a partial last round launched
+    as is (262,145; 900,000: last round < 80% full), exactly whole rounds (786,432), and a
+    mostly full last round, which the launch turns into whole rounds with the tuples spread
+    evenly over the workgroups (1,000,000: 3,907 -> 4,096 workgroups of ~244 tuples). Verdicts
+    = the workload's construction on every tuple, an oracle sample at workgroup edges."""
+    import torch
+    from smartbft_amd.workload import make_workload
+    wl = make_workload(gpu, n, start=9000 + n % 1000)
+    ok = torch.empty(wl.n, dtype=torch.uint8, device="cuda:0")
+    gpu.verify_dev(wl.digest, wl.r, wl.s, wl.qx, wl.qy, ok)
+    torch.cuda.synchronize()
+    assert torch.equal(ok, (~wl.corrupted).to(torch.uint8))
+    g = 4096 if n == 1_000_000 else 0  # the spread grid's workgroup edges: b n / 4096
+    edges = sorted({e for b in (1, 2, 1000, 4095) for e in ((b * n // g) - 1, b * n // g)} if g else {255, 256, n - 1})
+    edges = [e for e in edges if 0 <= e < n]
+    f = [x[edges] for x in wl.host_fields()]
+    assert np.array_equal(oracle.verify_batch(*f), ok.cpu().numpy()[edges])
+
+
 # ---- every verify kernel at every size: the one-lane throughput kernel and the small-batch
 # latency kernel with two and four lanes per tuple (p256_verify_small_kernel<2|4>, forced on
 # for big batches too)
