@@ -9,7 +9,7 @@ def main(path, kernel, top=8):
     import re as _re
     m = _re.search(r"\n(" + _re.escape(kernel) + r"\w*):", s)  # kernel = a mangled-name prefix
     i = m.start()
-    j = s.index("s_endpgm", i)
+    j = s.index(".Lfunc_end", i)  # not the first s_endpgm: a kernel may exit early
     body = s[i:j]
     parts = re.split(r"\n(\.LBB\d+_\d+):", body)
     blocks = [("entry", parts[0])] + [(parts[k], parts[k + 1]) for k in range(1, len(parts), 2)]
