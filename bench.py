@@ -39,8 +39,9 @@ VALU_ISSUE_PEAK_T = 39.3  # 1,024 SIMDs x 64 lanes / 4 cycles x 2.4 GHz (64-bit 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5,
+                    help="untimed steps: the first full-size dispatches after start-up run ~15%% slower")
     ap.add_argument("--n", type=int, default=1_000_000, help="tuples per GPU")
     ap.add_argument("--cpu-sample", type=int, default=131072)
     ap.add_argument("--cpu-threads", type=int, default=0,

@@ -2,7 +2,8 @@
 profiles/pmc_verify_latest.json (read by bench.py for roofline.traffic).
 
 Each counter comes from its own pass (gpurun_out/pmc_*/run_counter_collection.csv). Values are
-averaged over the kernel's dispatches. FETCH_SIZE / WRITE_SIZE are in KiB."""
+averaged over the kernel's full-size dispatches (the largest grid; the engine's init self-test
+launches it on 72 tuples). FETCH_SIZE / WRITE_SIZE are in KiB."""
 import csv
 import glob
 import json
@@ -16,16 +17,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main(src=os.path.join(ROOT, "gpurun_out"), dst=os.path.join(ROOT, "profiles", "pmc_verify_latest.json"),
          kernel="sbft::p256_verify_kernel", n=1_000_000):
     per = defaultdict(lambda: defaultdict(float))  # counter -> dispatch -> value
+    rows = []
     for f in glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv")):
-        for row in csv.DictReader(open(f)):
-            if not row["Kernel_Name"].startswith(kernel + "("):
-                continue
+        rows += [(f, r) for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith(kernel + "(")]
+    # only the full-size launches: the engine's init self-test dispatches the kernel on 72 tuples
+    grid = max((int(r["Grid_Size"]) for _, r in rows), default=0)
+    for f, row in rows:
+        if int(row["Grid_Size"]) == grid:
             per[row["Counter_Name"]][(f, row["Dispatch_Id"])] += float(row["Counter_Value"])
     raw = {c: sum(d.values()) / len(d) for c, d in per.items() if d}
     if not raw:
         sys.exit(f"no {kernel} dispatches under {src}/pmc_*")
     out = {"kernel": kernel, "n": n, "source": "rocprofv3 --pmc, separate passes (gpurun_out/pmc_*), "
-           "mean over the kernel's dispatches", "counters_raw": raw}
+           "mean over the kernel's full-size dispatches (grid %d)" % grid, "counters_raw": raw}
     if "SQ_INSTS_VALU" in raw and "SQ_WAVES" in raw:
         out["valu_instructions_per_verify"] = raw["SQ_INSTS_VALU"] * 64 / n
     if "FETCH_SIZE" in raw and "WRITE_SIZE" in raw:
