@@ -353,6 +353,11 @@ struct Slot {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// hash batches of at least this many messages (and no caller order) are taken longest first
+// (sbft_launch_sha256_lpt_order: three small kernels, ~tens of us, against a tail of up to
+// milliseconds when long messages are drawn last)
+constexpr size_t kShaLptMin = 65536;
+
 // signing batches up to this size take the wavefront-per-signature kernel (defined with the
 // registered-key code below, which owns G's comb table)
 constexpr size_t kSignWaveMax = 4096;
@@ -695,10 +700,18 @@ int sbft_gv_sha256_dev(sbft_gv_ctx* ctx, int device, const void* d_blob, const v
     if (!sl) return SBFT_GV_ENODEV;
     if (n == 0) return SBFT_GV_OK;
     if (hipSetDevice(device) != hipSuccess) return SBFT_GV_EDEVICE;
-    uint32_t* ctr = sl->stream_workspace((hipStream_t)stream, 256);  // the stream's work counter
-    if (!ctr) return SBFT_GV_ENOMEM;
+    // the stream's workspace: work counter | longest-first sort scratch | order
+    const bool lpt = !d_order && n >= kShaLptMin;
+    const size_t o_ws = 256, o_ord = 256 + align_up(sbft_sha256_lpt_ws_bytes(), 256);
+    uint32_t* ws = sl->stream_workspace((hipStream_t)stream, lpt ? o_ord + 4 * n : 256);
+    if (!ws) return SBFT_GV_ENOMEM;
+    uint32_t* ord = (uint32_t*)((uint8_t*)ws + o_ord);
+    if (lpt && sbft_launch_sha256_lpt_order((const uint32_t*)d_len, (uint32_t)n, (uint32_t*)((uint8_t*)ws + o_ws),
+                                            ord, (hipStream_t)stream))
+        return SBFT_GV_ELAUNCH;
     return sbft_launch_sha256((const uint8_t*)d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len,
-                              (const uint32_t*)d_order, (uint8_t*)d_dig, (uint32_t)n, ctr, (hipStream_t)stream)
+                              lpt ? ord : (const uint32_t*)d_order, (uint8_t*)d_dig, (uint32_t)n, ws,
+                              (hipStream_t)stream)
                ? SBFT_GV_ELAUNCH
                : SBFT_GV_OK;
 }
@@ -936,8 +949,11 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
     const size_t fd = align_up(32 * c.count, 256);
     const bool verify = ok_out != nullptr;
     // blob | off | len | work counter | digests [| r | s | qx | qy | ok | verify workspace]
+    // [| longest-first sort scratch | order]
+    const bool lpt = c.count >= kShaLptMin;
+    const size_t f_lpt = lpt ? align_up(sbft_sha256_lpt_ws_bytes(), 256) + align_up(4 * c.count, 256) : 0;
     const size_t need = fb + fo + fl + 256 + fd +
-                        (verify ? 4 * fd + align_up(c.count, 256) + sbft_verify_work_bytes(c.count) : 0);
+                        (verify ? 4 * fd + align_up(c.count, 256) + sbft_verify_work_bytes(c.count) : 0) + f_lpt;
     HIPCHK(hipSetDevice(sl->device));
     int rc = sl->reserve(need);
     if (rc) return rc;
@@ -947,7 +963,14 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
     HIPCHK(hipMemcpyAsync(d_off, rebased.data(), 8 * c.count, hipMemcpyHostToDevice, sl->stream));
     HIPCHK(hipMemcpyAsync(d_len, len + c.begin, 4 * c.count, hipMemcpyHostToDevice, sl->stream));
     // `rebased` is owned by the caller until the stream is synchronised
-    if (sbft_launch_sha256(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len, nullptr, d_dig,
+    uint32_t* ord = nullptr;
+    if (lpt) {
+        uint8_t* w = b + need - f_lpt;
+        ord = (uint32_t*)(w + align_up(sbft_sha256_lpt_ws_bytes(), 256));
+        if (sbft_launch_sha256_lpt_order((const uint32_t*)d_len, (uint32_t)c.count, (uint32_t*)w, ord, sl->stream))
+            return SBFT_GV_ELAUNCH;
+    }
+    if (sbft_launch_sha256(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len, ord, d_dig,
                            (uint32_t)c.count, (uint32_t*)d_ctr, sl->stream))
         return SBFT_GV_ELAUNCH;
     if (verify) {

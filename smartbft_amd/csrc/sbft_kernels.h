@@ -37,6 +37,12 @@ int sbft_launch_gcomb_build(void* d_table, hipStream_t stream);
 // device u32 of scratch private to the stream (zeroed by the launch).
 int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
                        const uint32_t* d_order, uint8_t* d_dig, uint32_t n, uint32_t* d_ctr, hipStream_t stream);
+// Longest-first message order for sbft_launch_sha256 (d_order): a counting sort of the lengths
+// over 128 length classes. d_ws: sbft_sha256_lpt_ws_bytes() of device scratch private to the
+// stream; d_order: n u32 indices. Worth it for large batches of unequal lengths (config 5).
+size_t sbft_sha256_lpt_ws_bytes(void);
+int sbft_launch_sha256_lpt_order(const uint32_t* d_len, uint32_t n, uint32_t* d_ws, uint32_t* d_order,
+                                 hipStream_t stream);
 // SoA verify inputs (32-byte fields, 16-B aligned outputs) gathered from framed messages in
 // the blob: r || s at off[k] + len[k] + sig_rel, x || y at off[k] + len[k] + pub_rel (the
 // caller has bounds-checked both against the blob).

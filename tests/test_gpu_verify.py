@@ -154,6 +154,34 @@ def test_sha256_dev_explicit_order(gpu):
         assert np.array_equal(d_dig.cpu().numpy(), exp)
 
 
+@pytest.mark.parametrize("n", [65_535, 65_536, 100_003])
+def test_sha256_longest_first_batches(gpu, n):
+    """Batches of >= 65,536 messages (no caller order) are hashed longest first: a device-side
+    counting sort of the lengths into 128 classes picks the order (sha256.hip). Digests land at
+    their own index on the device entry and the host entry, for lengths spanning empty, one-
+    block, padding-edge and multi-KiB messages at unaligned offsets, on both sides of the cut-in."""
+    import torch
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 1500, size=n).astype(np.uint32)
+    lens[:: 97] = rng.integers(4000, 9000, size=len(lens[:: 97]))  # a spread of long messages
+    lens[1::1009] = 0
+    lens[2::1013] = 55
+    lens[3::1019] = 64
+    gaps = rng.integers(0, 4, size=n).astype(np.uint64)
+    off = (np.cumsum(lens.astype(np.uint64) + gaps) - lens).astype(np.uint64)
+    total = int(off[-1] + lens[-1])
+    blob = rng.integers(0, 256, size=total + 256, dtype=np.uint8)  # SBFT_GV_SHA_BLOB_PAD
+    exp = oracle.sha256_batch(blob, off, lens)
+    got = gpu.sha256(blob[:total], off, lens)
+    assert np.array_equal(got, exp)
+    dev = torch.device("cuda:0")
+    d_dig = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    gpu.sha256_dev(torch.from_numpy(blob).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
+                   torch.from_numpy(lens.astype(np.int32)).to(dev), d_dig)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_dig.cpu().numpy(), exp)
+
+
 def test_fused_hash_then_verify(gpu):
     rng = np.random.default_rng(9)
     n = 600
