@@ -326,7 +326,7 @@ def sha_roofline(gbs: float) -> dict:
     return out
 
 
-def sha_config5(gv, dev, n_msgs: int, e2e_msgs: int = 65536):
+def sha_config5(gv, dev, n_msgs: int, e2e_msgs: int = 262144):
     """BASELINE config 5 on one GPU: requests with payload lengths uniform in [1 KiB, 64 KiB]
     (seeded; 2M per GPU = the 16M of config 5 over 8 GPUs), each signed under its own key,
     ~10% corrupted (smartbft_amd/workload.py make_config5).
@@ -334,7 +334,9 @@ def sha_config5(gv, dev, n_msgs: int, e2e_msgs: int = 65536):
       - hash + verify: sbft_gv_sha256_verify_p256_dev, digests never leave the GPU (kernel
         time of the SHA + verify launches); parity: verdict == not corrupted, every request;
       - streamed end to end from host memory: sbft_gv_sha256_verify_p256_stream on the first
-        e2e_msgs requests (~2 GB), from pageable and from page-locked memory (PCIe included);
+        e2e_msgs requests (~8.7 GB: the pipeline's fixed ramp -- the first window's copy, the
+        last window's serial hashing -- is ~15% of a 2 GB sample and ~4% of this one; config 5's
+        530 GB amortises it fully), from pageable and from page-locked memory (PCIe included);
         verdicts equal the device-resident ones."""
     import hashlib
     from smartbft_amd import PinnedArray
