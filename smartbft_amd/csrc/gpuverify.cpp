@@ -207,6 +207,33 @@ struct Slot {
             cap = 0;
         }
     };
+    // mapped, coherent host memory the VerifyProposal launches read their message offsets and
+    // lengths from (sbft_gv_framed_overlapped; no copy, caller holds mu)
+    uint8_t* vmap = nullptr;
+    uint8_t* vmap_dev = nullptr;
+    size_t vmap_cap = 0;
+    int reserve_vmap(size_t bytes) {
+        if (bytes <= vmap_cap) return SBFT_GV_OK;
+        if (vmap) {
+            (void)hipStreamSynchronize(stream);  // the last launches that read it have drained
+            (void)hipHostFree(vmap);
+        }
+        vmap = vmap_dev = nullptr;
+        vmap_cap = 0;
+        size_t want = std::max(bytes, (size_t)1 << 18);
+        want = (want + 4095) & ~(size_t)4095;
+        if (hipHostMalloc((void**)&vmap, want, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+            vmap = nullptr;
+            return SBFT_GV_ENOMEM;
+        }
+        if (hipHostGetDevicePointer((void**)&vmap_dev, vmap, 0) != hipSuccess) {
+            (void)hipHostFree(vmap);
+            vmap = nullptr;
+            return SBFT_GV_EDEVICE;
+        }
+        vmap_cap = want;
+        return SBFT_GV_OK;
+    }
     static constexpr int kZcLanes = 4;
     ZcLane zcl[kZcLanes];
     std::atomic<uint32_t> zc_rr{0};
@@ -548,6 +575,7 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
         for (void* t : s->retired) (void)hipFree(t);
         if (s->pin) (void)hipHostFree(s->pin);
         for (auto& z : s->zcl) z.release();
+        if (s->vmap) (void)hipHostFree(s->vmap);
         if (s->gcomb) (void)hipFree(s->gcomb);
         for (auto& kv : s->ws) {
             (void)hipStreamSynchronize(kv.first);
@@ -1219,24 +1247,31 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         for (int32_t rel : {sig_rel, pub_rel})
             if (end + rel < 0 || (uint64_t)(end + rel) + 64 > blob_len) return SBFT_GV_EINVAL;
     }
-    // off | len | hash counter | digests | r | s | qx | qy | ok | verify workspace
+    // Device: hash counter (256) | verify workspace | digests | r | s | qx | qy | ok. The
+    // offsets and lengths stay in mapped host memory that the gather and hash kernels read
+    // over PCIe, and the gather launch (first on the stream) zeroes both counters: no copy and
+    // no memset launch between the parse and the hash (a pageable copy each and two memsets
+    // cost ~40 us of the ~1 ms call, one pinned copy still ~25 us with its engine hand-off).
     const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256), fd = align_up(32 * n, 256);
-    rc = sl->reserve(fo + fl + 256 + 5 * fd + align_up(n, 256) + sbft_verify_work_bytes(n));
+    const size_t fw = align_up(sbft_verify_work_bytes(n), 256);
+    rc = sl->reserve(256 + fw + 5 * fd + align_up(n, 256));
+    if (!rc) rc = sl->reserve_vmap(fo + fl);
     if (rc) return rc;
     uint8_t* b = sl->dbuf;
-    uint8_t *d_off = b, *d_len = b + fo, *d_ctr = d_len + fl, *d_dig = d_ctr + 256, *v = d_dig + fd;
+    uint8_t *d_ctr = b, *d_work = d_ctr + 256, *d_dig = d_work + fw;
+    uint8_t* v = d_dig + fd;
     uint8_t* d_ok = v + 4 * fd;
-    uint32_t* work = (uint32_t*)(d_ok + align_up(n, 256));
     const void* gcomb = sl->gcomb_table();
     if (!gcomb) return SBFT_GV_ENOMEM;
-    HIPCHK(hipMemcpyAsync(d_off, off.data(), 8 * n, hipMemcpyHostToDevice, sl->stream));
-    HIPCHK(hipMemcpyAsync(d_len, len.data(), 4 * n, hipMemcpyHostToDevice, sl->stream));
-    if (sbft_launch_sha256(sl->bbuf, (const uint64_t*)d_off, (const uint32_t*)d_len, nullptr, d_dig, (uint32_t)n,
-                           (uint32_t*)d_ctr, sl->stream) ||
-        sbft_launch_gather_framed(sl->bbuf, (const uint64_t*)d_off, (const uint32_t*)d_len, (uint32_t)n, sig_rel,
-                                  pub_rel, v, v + fd, v + 2 * fd, v + 3 * fd, sl->stream) ||
-        sbft_launch_p256_verify(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_ok, (uint32_t)n, work, gcomb,
-                                sl->stream, nullptr, nullptr, ctx->lanes_for(n)))
+    std::memcpy(sl->vmap, off.data(), 8 * n);
+    std::memcpy(sl->vmap + fo, len.data(), 4 * n);
+    const uint64_t* d_off = (const uint64_t*)sl->vmap_dev;
+    const uint32_t* d_len = (const uint32_t*)(sl->vmap_dev + fo);
+    if (sbft_launch_gather_framed(sl->bbuf, d_off, d_len, (uint32_t)n, sig_rel, pub_rel, v, v + fd, v + 2 * fd,
+                                  v + 3 * fd, sl->stream, (uint32_t*)d_ctr, (uint32_t*)d_work) ||
+        sbft_launch_sha256(sl->bbuf, d_off, d_len, nullptr, d_dig, (uint32_t)n, (uint32_t*)d_ctr, sl->stream, 1) ||
+        sbft_launch_p256_verify(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_ok, (uint32_t)n, (uint32_t*)d_work, gcomb,
+                                sl->stream, nullptr, nullptr, ctx->lanes_for(n), 1))
         return SBFT_GV_ELAUNCH;
     HIPCHK(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, sl->stream));
     if (during) during();  // the caller's host work that does not need the verdicts, under the launch

@@ -1249,7 +1249,7 @@ __global__ __launch_bounds__(256) void p256_verify_keyed_lanes_kernel(const uint
 extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                        const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
                                        uint32_t n, uint32_t* d_work, const void* d_gcomb, hipStream_t stream,
-                                       hipEvent_t ev0, hipEvent_t ev1, int lanes) {
+                                       hipEvent_t ev0, hipEvent_t ev1, int lanes, int work_zeroed) {
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned blocks = (n + threads - 1) / threads;
@@ -1279,7 +1279,7 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
     }
-    if (hipMemsetAsync(d_work, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
+    if (!work_zeroed && hipMemsetAsync(d_work, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     SBFT_STEP("memset");
     if (lanes < 2) {  // the small-batch kernels invert s themselves
         const unsigned groups = (n + SBFT_SINV_GROUP - 1) / SBFT_SINV_GROUP;  // <= blocks: fits tot / kb

@@ -27,7 +27,8 @@ extern "C" {
 int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                             const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok, uint32_t n,
                             uint32_t* d_work, const void* d_gcomb, hipStream_t stream,
-                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int lanes = 1);
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int lanes = 1,
+                            int work_zeroed = 0);  // 1: the caller has zeroed d_work's first word
 size_t sbft_gcomb_table_bytes(void);
 int sbft_launch_gcomb_build(void* d_table, hipStream_t stream);
 // SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable
@@ -36,7 +37,8 @@ int sbft_launch_gcomb_build(void* d_table, hipStream_t stream);
 // NULL = index order, which keeps each wavefront's streams adjacent in memory). d_ctr: one
 // device u32 of scratch private to the stream (zeroed by the launch).
 int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
-                       const uint32_t* d_order, uint8_t* d_dig, uint32_t n, uint32_t* d_ctr, hipStream_t stream);
+                       const uint32_t* d_order, uint8_t* d_dig, uint32_t n, uint32_t* d_ctr, hipStream_t stream,
+                       int ctr_zeroed = 0);  // 1: the caller has zeroed *d_ctr (no memset launch)
 // Longest-first message order for sbft_launch_sha256 (d_order): a counting sort of the lengths
 // over 128 length classes. d_ws: sbft_sha256_lpt_ws_bytes() of device scratch private to the
 // stream; d_order: n u32 indices. Worth it for large batches of unequal lengths (config 5).
@@ -46,9 +48,12 @@ int sbft_launch_sha256_lpt_order(const uint32_t* d_len, uint32_t n, uint32_t* d_
 // SoA verify inputs (32-byte fields, 16-B aligned outputs) gathered from framed messages in
 // the blob: r || s at off[k] + len[k] + sig_rel, x || y at off[k] + len[k] + pub_rel (the
 // caller has bounds-checked both against the blob).
+// zero0 / zero1 (may be NULL): device u32s the launch sets to 0 (the counters of the hash and
+// verify launches that follow on the stream, so they need no memset launches of their own).
 int sbft_launch_gather_framed(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len, uint32_t n,
                               int32_t sig_rel, int32_t pub_rel, uint8_t* d_r, uint8_t* d_s, uint8_t* d_qx,
-                              uint8_t* d_qy, hipStream_t stream);
+                              uint8_t* d_qy, hipStream_t stream, uint32_t* zero0 = nullptr,
+                              uint32_t* zero1 = nullptr);
 // Key derivation + ECDSA sign with caller nonces: Q = d*G, (r, s); status 1 = ok.
 int sbft_launch_p256_sign(const uint8_t* d_d, const uint8_t* d_k, const uint8_t* d_e, uint8_t* d_qx,
                           uint8_t* d_qy, uint8_t* d_r, uint8_t* d_s, uint8_t* d_status, uint32_t n,

@@ -348,8 +348,13 @@ __global__ __launch_bounds__(256) void gather_framed_kernel(const uint8_t* __res
                                                             const uint32_t* __restrict__ len, uint32_t n,
                                                             int32_t sig_rel, int32_t pub_rel,
                                                             uint8_t* __restrict__ r, uint8_t* __restrict__ s,
-                                                            uint8_t* __restrict__ qx, uint8_t* __restrict__ qy) {
+                                                            uint8_t* __restrict__ qx, uint8_t* __restrict__ qy,
+                                                            uint32_t* zero0, uint32_t* zero1) {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid == 0) {
+        if (zero0) *zero0 = 0;
+        if (zero1) *zero1 = 0;
+    }
     if (gid >= 4u * n) return;
     const uint32_t k = gid >> 2, f = gid & 3u;
     const int64_t end = (int64_t)(off[k] + len[k]);
@@ -462,17 +467,18 @@ extern "C" int sbft_launch_sha256_lpt_order(const uint32_t* d_len, uint32_t n, u
 
 extern "C" int sbft_launch_gather_framed(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
                                          uint32_t n, int32_t sig_rel, int32_t pub_rel, uint8_t* d_r, uint8_t* d_s,
-                                         uint8_t* d_qx, uint8_t* d_qy, hipStream_t stream) {
+                                         uint8_t* d_qx, uint8_t* d_qy, hipStream_t stream, uint32_t* zero0,
+                                         uint32_t* zero1) {
     if (n == 0) return 0;
     const unsigned blocks = (unsigned)((4ull * n + 255) / 256);
     hipLaunchKernelGGL(sbft::gather_framed_kernel, dim3(blocks), dim3(256), 0, stream, d_blob, d_off, d_len, n,
-                       sig_rel, pub_rel, d_r, d_s, d_qx, d_qy);
+                       sig_rel, pub_rel, d_r, d_s, d_qx, d_qy, zero0, zero1);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
                                   const uint32_t* d_order, uint8_t* d_dig, uint32_t n, uint32_t* d_ctr,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, int ctr_zeroed) {
     if (n == 0) return 0;
     static int cus = 0;
     if (!cus) {
@@ -483,7 +489,7 @@ extern "C" int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, 
     }
     const unsigned threads = 256;
     const unsigned need = (n + threads - 1) / threads;
-    if (hipMemsetAsync(d_ctr, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
+    if (!ctr_zeroed && hipMemsetAsync(d_ctr, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     static int variant = -1;
     if (variant < 0) {
         // A/B measurement only: 0 the per-lane-load kernel; else the LDS-staged kernel with
