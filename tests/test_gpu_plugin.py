@@ -415,3 +415,43 @@ def test_consenter_sig_coalescer_concurrent_callers(gpu):
         v.VerifyConsenterSig(votes[0], blocks[0])
     assert v.consenter_stats() == (l1 + 2, c1 + 2)
     v.close()
+
+
+def test_consenter_batches_concurrent_on_zero_copy_lanes(gpu):
+    """Small keyed batches take one of four zero-copy lanes (own stream, mapped buffer, lock)
+    instead of the device lock, so concurrent quorum checks run side by side. 12 threads x 6
+    uncoalesced batches each (more callers than lanes: some wait for a lane), every batch with
+    its own proposal and a different bad signature: each caller gets exactly its statuses."""
+    import threading
+    nodes = [plugin.Signer(gpu, i, _priv(("zl", i))) for i in range(1, 18)]
+    v = plugin.Verifier(gpu, 1)
+    for s in nodes:
+        v.add_consenter(s.id, s.public_key())
+    T, R = 12, 6
+    props = [plugin.Proposal(b"zl-block-%d" % k * 20, b"h", b"m", 1) for k in range(T * R)]
+    jobs = []
+    for k, p in enumerate(props):
+        sigs = [n.SignProposal(p, b"x") for n in nodes]
+        bad = k % len(sigs)
+        sigs[bad] = plugin.Signature(sigs[bad].ID, sigs[(bad + 1) % len(sigs)].Value, sigs[bad].Msg)
+        want = [0] * len(sigs)
+        want[bad] = plugin.EVERIFY
+        jobs.append((sigs, p, want))
+    errors = []
+    start = threading.Barrier(T)
+
+    def worker(t):
+        start.wait()
+        for r in range(R):
+            sigs, p, want = jobs[t * R + r]
+            got = v.VerifyConsenterSigs(sigs, p)
+            if got != want:
+                errors.append((t, r, got, want))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(120)
+    assert not errors, errors[:3]
+    v.close()
