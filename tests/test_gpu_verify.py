@@ -154,7 +154,7 @@ def test_sha256_dev_explicit_order(gpu):
         assert np.array_equal(d_dig.cpu().numpy(), exp)
 
 
-@pytest.mark.parametrize("n", [65_535, 65_536, 100_003])
+@pytest.mark.parametrize("n", [65_535, 65_536, 100_003, 70_001])
 def test_sha256_longest_first_batches(gpu, n):
     """Batches of >= 65,536 messages (no caller order) are hashed longest first: a device-side
     counting sort of the lengths into 128 classes picks the order (sha256.hip). Digests land at
@@ -167,6 +167,9 @@ def test_sha256_longest_first_batches(gpu, n):
     lens[1::1009] = 0
     lens[2::1013] = 55
     lens[3::1019] = 64
+    if n == 70_001:  # messages past 64 KiB take the eighth-octave classes; one length for many
+        lens[5::2003] = rng.integers(65_000, 600_000, size=len(lens[5::2003]))
+        lens[6::7] = 777
     gaps = rng.integers(0, 4, size=n).astype(np.uint64)
     off = (np.cumsum(lens.astype(np.uint64) + gaps) - lens).astype(np.uint64)
     total = int(off[-1] + lens[-1])
