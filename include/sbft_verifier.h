@@ -81,7 +81,8 @@ void sbft_verifier_set_verification_sequence(sbft_verifier* v, uint64_t seq);
 /* api.Verifier.VerifyProposal (dependencies.go:56-57; called view.go:555): one fused GPU
  * launch (SHA-256 of every request body + P-256 verify). On success writes *count RequestInfo
  * pairs into infos as "client_id\0id\0" records (infos_cap bytes); bad_index (may be NULL)
- * receives the first failing request index on SBFT_V_EVERIFY. */
+ * receives the first failing request index on SBFT_V_EVERIFY. On failure *count is 0 and the
+ * contents of infos are unspecified (the records are written while the GPU verifies). */
 int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char* infos,
                                   size_t infos_cap, size_t* count, int64_t* bad_index, char* err,
                                   size_t err_cap);
