@@ -365,6 +365,7 @@ struct Slot {
         stage.clear();
     }
 
+    uint64_t dgen = 0;  // dbuf allocations so far (a new one may reuse the old address)
     int reserve(size_t bytes) {
         if (bytes <= dcap) return SBFT_GV_OK;
         if (dbuf) (void)hipFree(dbuf);
@@ -374,6 +375,7 @@ struct Slot {
         want = (want + 4095) & ~(size_t)4095;
         if (hipMalloc(&dbuf, want) != hipSuccess) return SBFT_GV_ENOMEM;
         dcap = want;
+        ++dgen;
         return SBFT_GV_OK;
     }
 };
@@ -940,6 +942,16 @@ int enqueue_verify_piped(const Chunk& c, const uint8_t* digest, const uint8_t* r
     return rc;
 }
 
+// Framed verify batches on the small-batch kernels hash inside the verify launch
+// (sbft_launch_p256_verify_framed). SBFT_VP_FUSED=0: gather + hash + verify kernels (A/B only).
+bool framed_fused_on() {
+    static const bool on = [] {
+        const char* e = getenv("SBFT_VP_FUSED");
+        return !e || e[0] != '0';
+    }();
+    return on;
+}
+
 // Hash (and optionally verify) messages [c.begin, +c.count). Offsets are rebased to the
 // chunk's first message so each device receives only its slice of the blob.
 // framed: verify inputs are gathered on the device from the blob itself (r || s at message
@@ -991,17 +1003,30 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
     HIPCHK(hipMemcpyAsync(d_off, rebased.data(), 8 * c.count, hipMemcpyHostToDevice, sl->stream));
     HIPCHK(hipMemcpyAsync(d_len, len + c.begin, 4 * c.count, hipMemcpyHostToDevice, sl->stream));
     // `rebased` is owned by the caller until the stream is synchronised
+    const bool fused = fr.on && verify && !dig_out && c.lanes >= 2 && framed_fused_on();
     uint32_t* ord = nullptr;
-    if (lpt) {
+    if (lpt && !fused) {
         uint8_t* w = b + need - f_lpt;
         ord = (uint32_t*)(w + align_up(sbft_sha256_lpt_ws_bytes(), 256));
         if (sbft_launch_sha256_lpt_order((const uint32_t*)d_len, (uint32_t)c.count, (uint32_t*)w, ord, sl->stream))
             return SBFT_GV_ELAUNCH;
     }
-    if (sbft_launch_sha256(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len, ord, d_dig,
-                           (uint32_t)c.count, (uint32_t*)d_ctr, sl->stream))
+    if (!fused && sbft_launch_sha256(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len, ord, d_dig,
+                                     (uint32_t)c.count, (uint32_t*)d_ctr, sl->stream))
         return SBFT_GV_ELAUNCH;
-    if (verify) {
+    if (fused) {
+        uint8_t* v = d_dig + fd;
+        uint8_t* d_ok = v + 4 * fd;
+        uint32_t* work = (uint32_t*)(d_ok + align_up(c.count, 256));
+        const void* gcomb = sl->gcomb_table();
+        if (!gcomb) return SBFT_GV_ENOMEM;
+        if (hipMemsetAsync(work, 0, sizeof(uint32_t), sl->stream) != hipSuccess ||
+            sbft_launch_p256_verify_framed(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len,
+                                           (uint32_t)c.count, fr.sig_rel, fr.pub_rel, d_dig, v, v + fd, v + 2 * fd,
+                                           v + 3 * fd, d_ok, work, gcomb, sl->stream, c.lanes))
+            return SBFT_GV_ELAUNCH;
+        HIPCHK(hipMemcpyAsync(ok_out + c.begin, d_ok, c.count, hipMemcpyDeviceToHost, sl->stream));
+    } else if (verify) {
         uint8_t* v = d_dig + fd;
         if (fr.on) {
             if (sbft_launch_gather_framed(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len,
@@ -1205,6 +1230,13 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     // the caller's core, whose caches typically hold it; the copy streams it from anywhere
     hipError_t ce = hipSuccess;
     const int dev = sl->device;
+    // the fused launch's fixup counter (d_work's first word, at a fixed offset of the device
+    // buffer): cleared ahead of the payload copy, so no fill sits between the parse and the
+    // verify launch (cleared again below only if the buffer is reallocated)
+    uint8_t* const pre_dbuf = sl->dbuf;
+    const uint64_t pre_gen = sl->dgen;
+    if (pre_dbuf && hipMemsetAsync(pre_dbuf + 256, 0, sizeof(uint32_t), sl->stream) != hipSuccess)
+        return SBFT_GV_EDEVICE;
     auto copy = [&] {
         if (blob_len && (ce = hipSetDevice(dev)) == hipSuccess)
             ce = hipMemcpyAsync(sl->bbuf, blob, blob_len, hipMemcpyHostToDevice, sl->stream);
@@ -1215,8 +1247,17 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     const int prc = prepare(off, len);
     const auto t2 = TC::now();
     if (async) ctx->helper.wait();
-    const int sync_rc = hipStreamSynchronize(sl->stream) == hipSuccess && ce == hipSuccess ? SBFT_GV_OK
-                                                                                           : SBFT_GV_EDEVICE;
+    // No stream synchronisation here: the launches below queue behind the payload copy on the
+    // same stream, so the verify starts as the DMA ends instead of one host round trip later
+    // (a pageable copy returns once its source is staged: the caller's buffer is free). A DMA
+    // fault surfaces at the closing synchronisation. SBFT_VP_SYNC=1: wait here (A/B only).
+    static const bool sync_after_copy = [] {
+        const char* e = getenv("SBFT_VP_SYNC");
+        return e && e[0] == '1';
+    }();
+    const int sync_rc = (!sync_after_copy || hipStreamSynchronize(sl->stream) == hipSuccess) && ce == hipSuccess
+                            ? SBFT_GV_OK
+                            : SBFT_GV_EDEVICE;
     const auto t3 = TC::now();
     struct Tr {
         bool on;
@@ -1267,12 +1308,24 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     std::memcpy(sl->vmap + fo, len.data(), 4 * n);
     const uint64_t* d_off = (const uint64_t*)sl->vmap_dev;
     const uint32_t* d_len = (const uint32_t*)(sl->vmap_dev + fo);
-    if (sbft_launch_gather_framed(sl->bbuf, d_off, d_len, (uint32_t)n, sig_rel, pub_rel, v, v + fd, v + 2 * fd,
-                                  v + 3 * fd, sl->stream, (uint32_t*)d_ctr, (uint32_t*)d_work) ||
-        sbft_launch_sha256(sl->bbuf, d_off, d_len, nullptr, d_dig, (uint32_t)n, (uint32_t*)d_ctr, sl->stream, 1) ||
-        sbft_launch_p256_verify(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_ok, (uint32_t)n, (uint32_t*)d_work, gcomb,
-                                sl->stream, nullptr, nullptr, ctx->lanes_for(n), 1))
+    // Small batches (lanes 2 / 4) hash inside the verify launch, on a second wavefront per
+    // workgroup that runs while the first builds its Q tables: no gather or hash kernel in
+    // front (~37 us of a 10k-tuple call).
+    const int lanes = ctx->lanes_for(n);
+    if (framed_fused_on() && lanes >= 2) {
+        if (((!pre_dbuf || sl->dgen != pre_gen) &&
+             hipMemsetAsync(d_work, 0, sizeof(uint32_t), sl->stream) != hipSuccess) ||
+            sbft_launch_p256_verify_framed(sl->bbuf, d_off, d_len, (uint32_t)n, sig_rel, pub_rel, d_dig, v, v + fd,
+                                           v + 2 * fd, v + 3 * fd, d_ok, (uint32_t*)d_work, gcomb, sl->stream, lanes))
+            return SBFT_GV_ELAUNCH;
+    } else if (sbft_launch_gather_framed(sl->bbuf, d_off, d_len, (uint32_t)n, sig_rel, pub_rel, v, v + fd,
+                                         v + 2 * fd, v + 3 * fd, sl->stream, (uint32_t*)d_ctr, (uint32_t*)d_work) ||
+               sbft_launch_sha256(sl->bbuf, d_off, d_len, nullptr, d_dig, (uint32_t)n, (uint32_t*)d_ctr, sl->stream,
+                                  1) ||
+               sbft_launch_p256_verify(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_ok, (uint32_t)n,
+                                       (uint32_t*)d_work, gcomb, sl->stream, nullptr, nullptr, lanes, 1)) {
         return SBFT_GV_ELAUNCH;
+    }
     HIPCHK(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, sl->stream));
     if (during) during();  // the caller's host work that does not need the verdicts, under the launch
     HIPCHK(hipStreamSynchronize(sl->stream));

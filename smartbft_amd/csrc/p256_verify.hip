@@ -23,6 +23,7 @@
 #include "p256_inv.hpp"
 #include "p256_point.hpp"
 #include "sbft_kernels.h"
+#include "sha256_dev.hpp"
 
 namespace sbft {
 
@@ -890,23 +891,81 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
 // Setup (checks, Q table, scalars) and the final comparison run redundantly on all lanes of a
 // tuple. The Q table lives in LDS (one copy per tuple). One wavefront per workgroup spreads a
 // small batch over as many CUs as possible.
-template <int LPT>
-__global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __restrict__ digest,
-                                                               const uint8_t* __restrict__ rr,
-                                                               const uint8_t* __restrict__ ss,
-                                                               const uint8_t* __restrict__ qxx,
-                                                               const uint8_t* __restrict__ qyy,
-                                                               uint8_t* __restrict__ ok, uint32_t n,
-                                                               uint32_t* __restrict__ work,
-                                                               const uint4* __restrict__ gcomb) {
+//
+// FRAMED (sbft_launch_p256_verify_framed): the tuples come straight from a framed payload, and
+// each workgroup has a second wavefront that hashes the tuples' messages (one lane per message)
+// while the first builds its Q tables; the digests meet the scalars in LDS at the table
+// barrier. r, s and Q are read from the payload in place (unaligned). No gather or hash
+// kernel runs in front: the batch's serial hashing hides under the table build. A tuple that
+// needs the exact fixup has its five fields written to the SoA rows the fixup kernel reads.
+struct FramedIn {
+    const uint8_t* blob;
+    const uint64_t* off;
+    const uint32_t* len;
+    int32_t sig_rel, pub_rel;
+    uint8_t *dig, *r, *s, *qx, *qy;  // SoA rows for the fixup kernel (flagged tuples only)
+};
+
+// 32 big-endian bytes at any byte address -> 8 little-endian limbs (reads up to 3 bytes past)
+SBFT_DEV fe load_be32_any(const uint8_t* p) {
+    typedef const __attribute__((address_space(1))) uint32_t gu32;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    gu32* base = (gu32*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t raw[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) raw[i] = base[i];
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[7 - i] = __builtin_bswap32(__builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh));
+    return r;
+}
+
+template <int LPT, bool FRAMED = false>
+__global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(const uint8_t* __restrict__ digest,
+                                                                             const uint8_t* __restrict__ rr,
+                                                                             const uint8_t* __restrict__ ss,
+                                                                             const uint8_t* __restrict__ qxx,
+                                                                             const uint8_t* __restrict__ qyy,
+                                                                             uint8_t* __restrict__ ok, uint32_t n,
+                                                                             uint32_t* __restrict__ work,
+                                                                             const uint4* __restrict__ gcomb,
+                                                                             FramedIn fr) {
     static_assert(LPT == 2 || LPT == 4, "two or four lanes per tuple");
     constexpr bool kQuad = LPT == 4;
-    constexpr int kTuples = 64 / LPT;  // tuples per 64-lane workgroup
+    constexpr int kTuples = 64 / LPT;  // tuples per 64-lane verify wavefront
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     // [entry][x limbs 0..8, y limbs 0..8][tuple]: the lanes of a tuple read the same word, the
     // tuples of the wave consecutive words
     __shared__ u32 qtab[kQTab * 18 * kTuples];
+    __shared__ u32 edig[FRAMED ? 8 * kTuples : 1];  // FRAMED: the hash wave's digests [word][tuple]
     inv::stage_divstep_table(dtab);  // ends with a barrier
+
+    if constexpr (FRAMED) {
+        if (threadIdx.x >= 64) {  // the hash wavefront (wave-uniform branch)
+            const uint32_t lane = threadIdx.x - 64, th = blockIdx.x * kTuples + lane;
+            if (lane < (uint32_t)kTuples && th < n) {
+                const uint8_t* msg = fr.blob + fr.off[th];
+                const uint32_t L = fr.len[th], nb = sha256_nblocks(L);
+                uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+                uint32_t w[16];
+                for (uint32_t b = 0; b < nb; ++b) {
+                    sha256_block_at(msg, L, b, w);
+                    compress(h, w);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) edig[k * kTuples + lane] = h[k];
+            }
+            // the verify wavefront's barriers: the Q table's, and the quad's two comb stagings
+            __syncthreads();
+            if constexpr (kQuad) {
+                __syncthreads();
+                __syncthreads();
+            }
+            return;
+        }
+    }
 
     const int pr = threadIdx.x / LPT;
     const bool odd = (threadIdx.x & 1) != 0;
@@ -915,11 +974,20 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
     const bool active = t < n;
     const uint32_t idx = active ? t : (n - 1);
 
-    const fe e_raw = load_be32(digest + 32ull * idx);
-    const fe r = load_be32(rr + 32ull * idx);
-    const fe s = load_be32(ss + 32ull * idx);
-    const fe qx = load_be32(qxx + 32ull * idx);
-    const fe qy = load_be32(qyy + 32ull * idx);
+    fe e_raw, r, s, qx, qy;
+    if constexpr (FRAMED) {
+        const uint8_t* end = fr.blob + fr.off[idx] + fr.len[idx];
+        r = load_be32_any(end + fr.sig_rel);
+        s = load_be32_any(end + fr.sig_rel + 32);
+        qx = load_be32_any(end + fr.pub_rel);
+        qy = load_be32_any(end + fr.pub_rel + 32);
+    } else {
+        e_raw = load_be32(digest + 32ull * idx);
+        r = load_be32(rr + 32ull * idx);
+        s = load_be32(ss + 32ull * idx);
+        qx = load_be32(qxx + 32ull * idx);
+        qy = load_be32(qyy + 32ull * idx);
+    }
     const bool valid = verify_inputs_valid(r, s, qx, qy);
     // The table's one inversion mod p (even lane) and s^-1 mod n (odd lane) run as one safegcd
     // instruction stream; no launch-wide s^-1 batching kernels in front of this one.
@@ -959,6 +1027,10 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
             }
     }
     __syncthreads();
+    if constexpr (FRAMED) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e_raw.v[7 - k] = edig[k * kTuples + pr];
+    }
     fe u1, u2;
     bool neg1, neg2;
     {
@@ -1091,6 +1163,13 @@ __global__ __launch_bounds__(64) void p256_verify_small_kernel(const uint8_t* __
     const bool accept = verify_final(acc, r, exc);
     if (active && (threadIdx.x % LPT) == 0) {
         if (exc && valid) {
+            if constexpr (FRAMED) {  // the fixup kernel's inputs
+                store_be32(fr.dig + 32ull * t, e_raw);
+                store_be32(fr.r + 32ull * t, r);
+                store_be32(fr.s + 32ull * t, s);
+                store_be32(fr.qx + 32ull * t, qx);
+                store_be32(fr.qy + 32ull * t, qy);
+            }
             const uint32_t slot = atomicAdd(work, 1u);
             work[1 + slot] = t;
         } else {
@@ -1294,10 +1373,10 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
         const unsigned tpw = 64 / lanes, sblocks = (n + tpw - 1) / tpw;
         if (lanes == 2)
             hipLaunchKernelGGL(sbft::p256_verify_small_kernel<2>, dim3(sblocks), dim3(64), 0, stream, d_digest,
-                               d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb);
+                               d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, sbft::FramedIn{});
         else
             hipLaunchKernelGGL(sbft::p256_verify_small_kernel<4>, dim3(sblocks), dim3(64), 0, stream, d_digest,
-                               d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb);
+                               d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, sbft::FramedIn{});
     } else {
         // Waves are issue-bound at 4 per SIMD, and all take the same time. When the last
         // resident round would be mostly full, a whole number of rounds with the tuples spread
@@ -1346,5 +1425,36 @@ extern "C" int sbft_launch_gcomb_build(void* d_table, hipStream_t stream) {
     const unsigned total = SBFT_GCOMB_WINDOWS * SBFT_GCOMB_ENTRIES + 1;
     hipLaunchKernelGGL(sbft::p256_gcomb_build_kernel, dim3((total + 255) / 256), dim3(256), 0, stream,
                        (uint4*)d_table);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Framed tuples on the small-batch kernels (lanes 2 or 4): hash, field reads and verify in one
+// launch (p256_verify_small_kernel<LPT, true>), then the fixup. The SoA rows (32 B per tuple
+// each) are written only for the rare tuples the fixup takes; d_work's counter must be zero.
+extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
+                                              uint32_t n, int32_t sig_rel, int32_t pub_rel, uint8_t* d_dig,
+                                              uint8_t* d_r, uint8_t* d_s, uint8_t* d_qx, uint8_t* d_qy,
+                                              uint8_t* d_ok, uint32_t* d_work, const void* d_gcomb,
+                                              hipStream_t stream, int lanes) {
+    if (n == 0) return 0;
+    if (lanes != 2 && lanes != 4) return -1;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, pub_rel, d_dig, d_r, d_s, d_qx, d_qy};
+    const unsigned tpw = 64 / (unsigned)lanes, sblocks = (n + tpw - 1) / tpw;
+    if (lanes == 2)
+        hipLaunchKernelGGL((sbft::p256_verify_small_kernel<2, true>), dim3(sblocks), dim3(128), 0, stream, d_dig,
+                           d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
+    else
+        hipLaunchKernelGGL((sbft::p256_verify_small_kernel<4, true>), dim3(sblocks), dim3(128), 0, stream, d_dig,
+                           d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
+    const unsigned blocks = (n + 255) / 256, fix_cap = 8u * (unsigned)cus;
+    hipLaunchKernelGGL(sbft::p256_verify_fixup_kernel, dim3(blocks < fix_cap ? blocks : fix_cap), dim3(256), 0,
+                       stream, d_dig, d_r, d_s, d_qx, d_qy, d_ok, (const uint32_t*)d_work);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -29,6 +29,15 @@ int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const u
                             uint32_t* d_work, const void* d_gcomb, hipStream_t stream,
                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int lanes = 1,
                             int work_zeroed = 0);  // 1: the caller has zeroed d_work's first word
+// Framed tuples (message k = blob[off[k], off[k]+len[k]), r||s at its end + sig_rel, Qx||Qy at
+// its end + pub_rel; the blob readable SBFT_GV_SHA_BLOB_PAD bytes past its end) on the
+// small-batch kernel, lanes 2 or 4: SHA-256 and verify in one launch, then the fixup. d_dig ..
+// d_qy: 32n-byte rows each (written only for tuples the fixup recomputes). d_work's first word
+// must be zero (sbft_launch_gather_framed's zero0 can clear it).
+int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len, uint32_t n,
+                                   int32_t sig_rel, int32_t pub_rel, uint8_t* d_dig, uint8_t* d_r, uint8_t* d_s,
+                                   uint8_t* d_qx, uint8_t* d_qy, uint8_t* d_ok, uint32_t* d_work,
+                                   const void* d_gcomb, hipStream_t stream, int lanes);
 size_t sbft_gcomb_table_bytes(void);
 int sbft_launch_gcomb_build(void* d_table, hipStream_t stream);
 // SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable

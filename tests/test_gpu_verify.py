@@ -395,6 +395,53 @@ def test_framed_hash_then_verify(mode):
     gv.close()
 
 
+@pytest.mark.parametrize("mode", list(KERNEL_OPTS))
+def test_framed_exceptional_tuples(mode):
+    """Framed tuples whose Shamir sum meets an exceptional addition, through the fused
+    hash-and-verify launch (pair, quad) and the three-kernel chain (lane): the verify kernel
+    writes the flagged tuples' fields out for the fix-up kernel. With u1 = e/s, u2 = r/s:
+    Q = -(e/r) G makes R = u1 G + u2 Q infinity (reject); Q = (e/r) G with s = 2e/k and
+    r = x(kG) makes u2 Q = u1 G, a doubling, and the signature valid. Verdicts equal the oracle's."""
+    import torch
+    from smartbft_amd import GpuVerifier
+    assert torch.cuda.is_available(), "gpu-marked test needs a visible MI355X"
+    gv = GpuVerifier(**KERNEL_OPTS[mode])
+    rng = np.random.default_rng(77)
+    n, N = 160, oracle.N
+    parts, off, lens, exp = [], [], [], []
+    pos = 1
+    for i in range(n):
+        msg = rng.bytes(int(rng.integers(0, 200)))
+        e = int.from_bytes(hashlib.sha256(msg).digest(), "big") % N
+        k = int.from_bytes(rng.bytes(32), "big") % N or 1
+        if i % 4 == 0:  # R = infinity
+            r = int.from_bytes(rng.bytes(32), "big") % N or 1
+            s = int.from_bytes(rng.bytes(32), "big") % N or 1
+            q = oracle.pubkey((-e * pow(r, -1, N)) % N or 1)
+        elif i % 4 == 1:  # u2 Q = u1 G: the doubling case, a valid signature
+            r = int.from_bytes(oracle.pubkey(k)[0], "big") % N
+            s = (2 * e * pow(k, -1, N)) % N or 1
+            q = oracle.pubkey((e * pow(r, -1, N)) % N or 1)
+        else:  # ordinary signatures
+            d = int.from_bytes(rng.bytes(32), "big") % N or 1
+            q = oracle.pubkey(d)
+            rb, sb = oracle.sign(d, k, hashlib.sha256(msg).digest())
+            r, s = int.from_bytes(rb, "big"), int.from_bytes(sb, "big")
+        sig = r.to_bytes(32, "big") + s.to_bytes(32, "big")
+        cols = (hashlib.sha256(msg).digest(), sig[:32], sig[32:], q[0], q[1])
+        exp.append(oracle.verify_batch(*[np.frombuffer(x, dtype=np.uint8).reshape(1, 32) for x in cols])[0])
+        off.append(pos)
+        lens.append(len(msg))
+        parts.append(msg + sig + q[0] + q[1])  # the key follows the signature: Q depends on e
+        pos += len(msg) + 128
+    exp = np.array(exp, dtype=np.uint8)
+    blob = np.frombuffer(b"\0" + b"".join(parts), dtype=np.uint8)
+    got = gv.sha256_verify_framed(blob, np.array(off), np.array(lens), 0, 64)
+    assert np.array_equal(got, exp)
+    assert exp[1::4].all() and not exp[0::4].any()
+    gv.close()
+
+
 def test_pinned_inputs_pipelined_host_verify(gpu):
     """sbft_gv_verify_p256 with all five inputs in sbft_gv_host_alloc memory takes the
     copy/compute pipeline (a 65,536 then 262,144-tuple sub-batches on a copy stream + events,
