@@ -17,7 +17,11 @@ struct sbft_gv_ctx;
 // the caller's thread once the hash and verify launches are queued, before the call waits for
 // them. ok receives one verdict per message. Batches of min_split or more messages on a multi-device context fall back to the
 // split path after the parse.
+// kid (optional): registered key ids (sbft_gv_register_keys), read after prepare returns. If
+// prepare left one nonzero id per message there (and the batch is large enough for the
+// four-lane keyed kernel), the batch is verified against those keys' comb tables instead.
 int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, int32_t sig_rel,
                               int32_t pub_rel,
                               const std::function<int(std::vector<uint64_t>&, std::vector<uint32_t>&)>& prepare,
-                              std::vector<uint8_t>& ok, const std::function<void()>& during = nullptr);
+                              std::vector<uint8_t>& ok, const std::function<void()>& during = nullptr,
+                              const std::vector<uint32_t>* kid = nullptr);

@@ -1204,10 +1204,15 @@ int sbft_gv_sha256_verify_p256_framed(sbft_gv_ctx* ctx, const uint8_t* blob, siz
 
 }  // extern "C"
 
+namespace {
+int ensure_tables(Slot* sl, size_t upto);
+}  // namespace
+
 int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, int32_t sig_rel,
                               int32_t pub_rel,
                               const std::function<int(std::vector<uint64_t>&, std::vector<uint32_t>&)>& prepare,
-                              std::vector<uint8_t>& ok, const std::function<void()>& during) {
+                              std::vector<uint8_t>& ok, const std::function<void()>& during,
+                              const std::vector<uint32_t>* kid) {
     if (!ctx || (!blob && blob_len)) return SBFT_GV_EINVAL;
     // this thread's scratch, bound to references: a lambda running on the helper thread must
     // see these objects, not the helper's own thread_local instances
@@ -1287,6 +1292,30 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         const int64_t end = (int64_t)(off[k] + len[k]);
         for (int32_t rel : {sig_rel, pub_rel})
             if (end + rel < 0 || (uint64_t)(end + rel) + 64 > blob_len) return SBFT_GV_EINVAL;
+    }
+    // Every request signed by a registered client key (kid[k] != 0 for all k, filled by
+    // prepare): the keyed four-lane kernel over the clients' comb tables, hashing on a fifth
+    // wavefront per workgroup and reading r || s from the payload; key ids beside the offsets
+    // in mapped host memory. Smaller batches go through the caller's other paths.
+    if (kid && kid->size() == n && n >= ctx->keyed_lanes_min) {
+        const uint32_t nkeys = (uint32_t)ctx->nkeys.load();
+        const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256);
+        rc = ensure_tables(sl, nkeys);
+        if (!rc) rc = sl->reserve(align_up(n, 256));
+        if (!rc) rc = sl->reserve_vmap(fo + 2 * fl);
+        if (rc) return rc;
+        std::memcpy(sl->vmap, off.data(), 8 * n);
+        std::memcpy(sl->vmap + fo, len.data(), 4 * n);
+        std::memcpy(sl->vmap + fo + fl, kid->data(), 4 * n);
+        const uint8_t* vd = sl->vmap_dev;
+        if (sbft_launch_p256_verify_keyed_framed(sl->bbuf, (const uint64_t*)vd, (const uint32_t*)(vd + fo), sig_rel,
+                                                 (const uint32_t*)(vd + fo + fl), (const void* const*)sl->d_keytab,
+                                                 nkeys, sl->dbuf, (uint32_t)n, sl->stream))
+            return SBFT_GV_ELAUNCH;
+        HIPCHK(hipMemcpyAsync(ok.data(), sl->dbuf, n, hipMemcpyDeviceToHost, sl->stream));
+        if (during) during();
+        HIPCHK(hipStreamSynchronize(sl->stream));
+        return SBFT_GV_OK;
     }
     // Device: hash counter (256) | verify workspace | digests | r | s | qx | qy | ok. The
     // offsets and lengths stay in mapped host memory that the gather and hash kernels read

@@ -1214,21 +1214,51 @@ SBFT_DEV void quad_combine(jp29& acc, bool& inf) {
     inf = inf && oinf;
 }
 
-__global__ __launch_bounds__(256) void p256_verify_keyed_lanes_kernel(const uint8_t* __restrict__ digest,
-                                                                      const uint8_t* __restrict__ rr,
-                                                                      const uint8_t* __restrict__ ss,
-                                                                      const uint32_t* __restrict__ key,
-                                                                      const uint4* const* __restrict__ keytab,
-                                                                      uint32_t nkeys, uint8_t* __restrict__ ok,
-                                                                      uint32_t n) {
+// FRAMED (sbft_launch_p256_verify_keyed_framed): the signatures' bodies lie in a payload
+// (fr.blob/off/len, r || s at the body's end + fr.sig_rel); a fifth wavefront per workgroup
+// hashes the workgroup's 64 bodies into LDS while the four verify wavefronts invert s, and
+// the digests are picked up after that barrier. No hash kernel in front.
+template <bool FRAMED = false>
+__global__ __launch_bounds__(FRAMED ? 320 : 256) void p256_verify_keyed_lanes_kernel(
+    const uint8_t* __restrict__ digest, const uint8_t* __restrict__ rr, const uint8_t* __restrict__ ss,
+    const uint32_t* __restrict__ key, const uint4* const* __restrict__ keytab, uint32_t nkeys,
+    uint8_t* __restrict__ ok, uint32_t n, FramedIn fr) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    __shared__ u32 edig[FRAMED ? 8 * 64 : 1];  // FRAMED: [word][signature of the workgroup]
     inv::stage_divstep_table(dtab);  // ends with a barrier
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if constexpr (FRAMED) {
+        if (threadIdx.x >= 256) {  // the hash wavefront
+            const uint32_t lane = threadIdx.x - 256, th = blockIdx.x * 64 + lane;
+            if (th < n) {
+                const uint8_t* msg = fr.blob + fr.off[th];
+                const uint32_t L = fr.len[th], nb = sha256_nblocks(L);
+                uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+                uint32_t w[16];
+                for (uint32_t b = 0; b < nb; ++b) {
+                    sha256_block_at(msg, L, b, w);
+                    compress(h, w);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) edig[k * 64 + lane] = h[k];
+            }
+            __syncthreads();  // the verify wavefronts' digest barrier
+            return;
+        }
+    }
+    const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
     const uint32_t t = gid >> 2, j = gid & 3u;
     const bool active = t < n;
     const uint32_t idx = active ? t : n - 1;
-    const fe r = load_be32(rr + 32ull * idx);
-    const fe s = load_be32(ss + 32ull * idx);
+    fe r, s;
+    if constexpr (FRAMED) {
+        const uint8_t* sig = fr.blob + fr.off[idx] + fr.len[idx] + fr.sig_rel;
+        r = load_be32_any(sig);
+        s = load_be32_any(sig + 32);
+    } else {
+        r = load_be32(rr + 32ull * idx);
+        s = load_be32(ss + 32ull * idx);
+    }
     const uint32_t kid = key[idx];
     const bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
                        kid >= 1 && kid < nkeys && keytab[kid] != nullptr;
@@ -1245,7 +1275,16 @@ __global__ __launch_bounds__(256) void p256_verify_keyed_lanes_kernel(const uint
         inv::inv_mod(w.v, sv.v, dtab, false, rn.v);
     }
     fe e, u;
-    fn_canon(e, load_be32(digest + 32ull * idx));
+    if constexpr (FRAMED) {
+        __syncthreads();  // the hash wavefront's digests
+        fe d;
+        const uint32_t sl = threadIdx.x >> 2;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d.v[7 - k] = edig[k * 64 + sl];
+        fn_canon(e, d);
+    } else {
+        fn_canon(e, load_be32(digest + 32ull * idx));
+    }
     fn_mul(u, j < 2 ? e : r, w);  // u1 = e s^-1 (j < 2) or u2 = r s^-1 (plain)
     fn_canon(u, u);
     const uint4* tab = keytab[j < 2 ? 0u : (valid ? kid : 0u)];
@@ -1414,8 +1453,20 @@ extern "C" int sbft_launch_p256_verify_keyed_lanes(const uint8_t* d_digest, cons
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned kblocks = (unsigned)((4ull * n + threads - 1) / threads);
-    hipLaunchKernelGGL(sbft::p256_verify_keyed_lanes_kernel, dim3(kblocks), dim3(threads), 0, stream, d_digest, d_r,
-                       d_s, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n);
+    hipLaunchKernelGGL(sbft::p256_verify_keyed_lanes_kernel<false>, dim3(kblocks), dim3(threads), 0, stream, d_digest,
+                       d_r, d_s, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n, sbft::FramedIn{});
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int sbft_launch_p256_verify_keyed_framed(const uint8_t* d_blob, const uint64_t* d_off,
+                                                    const uint32_t* d_len, int32_t sig_rel, const uint32_t* d_key,
+                                                    const void* const* d_keytab, uint32_t nkeys, uint8_t* d_ok,
+                                                    uint32_t n, hipStream_t stream) {
+    if (n == 0) return 0;
+    const unsigned kblocks = (unsigned)((n + 63) / 64);  // 64 signatures per workgroup
+    const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipLaunchKernelGGL(sbft::p256_verify_keyed_lanes_kernel<true>, dim3(kblocks), dim3(320), 0, stream, nullptr,
+                       nullptr, nullptr, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n, fr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -93,6 +93,11 @@ int sbft_launch_comb_build(const uint8_t* d_qx, const uint8_t* d_qy, void* d_tab
 int sbft_launch_p256_verify_keyed_lanes(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                         const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
                                         uint8_t* d_ok, uint32_t n, hipStream_t stream);
+// The same over framed signatures (r || s at body end + sig_rel in d_blob; the blob readable
+// SBFT_GV_SHA_BLOB_PAD bytes past its end): the bodies are hashed inside the launch.
+int sbft_launch_p256_verify_keyed_framed(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
+                                         int32_t sig_rel, const uint32_t* d_key, const void* const* d_keytab,
+                                         uint32_t nkeys, uint8_t* d_ok, uint32_t n, hipStream_t stream);
 int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint8_t* d_blob, const uint64_t* d_off,
                                   const uint32_t* d_len, const uint8_t* d_r, const uint8_t* d_s,
                                   const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,

@@ -314,6 +314,7 @@ struct ProposalScratch {
     std::vector<Req> reqs;
     std::vector<uint64_t> off;
     std::vector<uint32_t> len;
+    std::vector<uint32_t> kid;  // registered client key ids (VerifyProposal with clients registered)
     std::vector<uint8_t> ok;
 };
 ProposalScratch& proposal_scratch() {
@@ -1008,87 +1009,51 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
         std::shared_lock<std::shared_mutex> g(v->clients_mu);
         registered = v->clients.count != 0;
     }
-    if (v->ctx && !registered) {
-        // no registered client keys: one framed launch, the parse overlapped with the payload
-        // copy, and the RequestInfo records written while the GPU verifies (they are returned
-        // only if every request passes)
-        int info_rc = 0;
-        auto during = [&] {
-            char* w = infos;
-            char* end = infos + infos_cap;
-            for (auto& q : reqs)
-                if (!write_info(w, end, q.client_id, q.req_id)) {
-                    info_rc = SBFT_V_ESPACE;
-                    return;
-                }
-        };
-        const int rc = sbft_gv_framed_overlapped(v->ctx, p->payload, p->payload_len, 0, -64, prepare, ok, during);
-        if (rc) {
-            if (rc != SBFT_V_EFORMAT) put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
-            return rc;
-        }
-        return finish_proposal(reqs, ok, nullptr, 0, count, bad_index, err, err_cap, info_rc);
-    }
-    std::vector<uint64_t>& off = scr.off;
-    std::vector<uint32_t>& len = scr.len;
-    if (int prc = prepare(off, len)) return prc;
-    const size_t n = reqs.size();
-    ok.assign(n, 0);
-    if (n && !v->ctx) {
+    if (!v->ctx) {
+        if (int prc = prepare(scr.off, scr.len)) return prc;
+        ok.clear();
+        if (reqs.empty()) return finish_proposal(reqs, ok, infos, infos_cap, count, bad_index, err, err_cap);
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(SBFT_GV_ENODEV));
         return SBFT_GV_ENODEV;
     }
-    // requests whose key is a registered client key take the keyed launch (comb tables, no
-    // doublings); the rest the generic fused launch. The request bodies are hashed where they
-    // lie in the payload either way.
-    std::vector<uint32_t> kid;
-    size_t nk = 0;
-    {
+    // One framed launch, the parse overlapped with the payload copy, and the RequestInfo
+    // records written while the GPU verifies (they are returned only if every request passes).
+    // With client keys registered, the parse also looks every request's key up: if all are
+    // registered, the batch takes the keyed launch over their comb tables (no doublings);
+    // otherwise the generic launch verifies every request (the same verdicts).
+    std::vector<uint32_t>& kid = scr.kid;
+    kid.clear();
+    auto prepare_keyed = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
+        if (int prc = prepare(off, len)) return prc;
+        const size_t n = reqs.size();
+        kid.resize(n);
         std::shared_lock<std::shared_mutex> g(v->clients_mu);
-        if (v->clients.count) {
-            kid.resize(n);
-            for (size_t i = 0; i < n; ++i) nk += (kid[i] = v->clients.find(reqs[i].pub + 1)) != 0;
-        }
-    }
-    int rc = 0;
-    if (n && nk == 0) {  // the tuples are gathered on the device from the payload itself
-        rc = sbft_gv_sha256_verify_p256_framed(v->ctx, p->payload, p->payload_len, off.data(), len.data(), n,
-                                               0, -64, ok.data());
-    } else if (n) {
-        std::vector<size_t> wk, wg;
-        wk.reserve(nk);
-        wg.reserve(n - nk);
-        for (size_t i = 0; i < n; ++i) (kid[i] ? wk : wg).push_back(i);
-        auto pick64 = [](const std::vector<uint64_t>& a, const std::vector<size_t>& w) {
-            std::vector<uint64_t> o(w.size());
-            for (size_t i = 0; i < w.size(); ++i) o[i] = a[w[i]];
-            return o;
-        };
-        auto pick32 = [](const std::vector<uint32_t>& a, const std::vector<size_t>& w) {
-            std::vector<uint32_t> o(w.size());
-            for (size_t i = 0; i < w.size(); ++i) o[i] = a[w[i]];
-            return o;
-        };
-        std::vector<uint8_t> rk(32 * wk.size()), sk(32 * wk.size());
-        for (size_t i = 0; i < wk.size(); ++i) {
-            std::memcpy(&rk[32 * i], reqs[wk[i]].sig, 32);
-            std::memcpy(&sk[32 * i], reqs[wk[i]].sig + 32, 32);
-        }
-        std::vector<uint8_t> okk(wk.size()), okg(wg.size());
-        rc = sbft_gv_sha256_verify_p256_keyed(v->ctx, p->payload, p->payload_len, pick64(off, wk).data(),
-                                              pick32(len, wk).data(), rk.data(), sk.data(), pick32(kid, wk).data(),
-                                              wk.size(), okk.data());
-        if (!rc && !wg.empty())
-            rc = sbft_gv_sha256_verify_p256_framed(v->ctx, p->payload, p->payload_len, pick64(off, wg).data(),
-                                                   pick32(len, wg).data(), wg.size(), 0, -64, okg.data());
-        for (size_t i = 0; i < wk.size(); ++i) ok[wk[i]] = okk[i];
-        for (size_t i = 0; i < wg.size(); ++i) ok[wg[i]] = okg[i];
-    }
+        for (size_t i = 0; i < n; ++i)
+            if (!(kid[i] = v->clients.find(reqs[i].pub + 1))) {
+                kid.clear();
+                break;
+            }
+        return 0;
+    };
+    int info_rc = 0;
+    auto during = [&] {
+        char* w = infos;
+        char* end = infos + infos_cap;
+        for (auto& q : reqs)
+            if (!write_info(w, end, q.client_id, q.req_id)) {
+                info_rc = SBFT_V_ESPACE;
+                return;
+            }
+    };
+    const int rc = registered ? sbft_gv_framed_overlapped(v->ctx, p->payload, p->payload_len, 0, -64, prepare_keyed,
+                                                          ok, during, &kid)
+                              : sbft_gv_framed_overlapped(v->ctx, p->payload, p->payload_len, 0, -64, prepare, ok,
+                                                          during);
     if (rc) {
-        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+        if (rc != SBFT_V_EFORMAT) put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
         return rc;
     }
-    return finish_proposal(reqs, ok, infos, infos_cap, count, bad_index, err, err_cap);
+    return finish_proposal(reqs, ok, nullptr, 0, count, bad_index, err, err_cap, info_rc);
 }
 
 int sbft_verifier_verify_request(sbft_verifier* v, const uint8_t* req, size_t len, char* info, size_t info_cap,

@@ -327,6 +327,17 @@ def test_verify_proposal_registered_clients(gpu, net):
     assert ei.value.index == 46
     v.add_clients([c.public_key() for c in clients])  # all registered (re-registering is a no-op)
     assert v.VerifyProposal(p) == generic
+    # >= 1,025 requests, every key registered: the keyed four-lane launch over the payload
+    # (bodies hashed on a fifth wavefront, r || s read in place), against the generic verifier
+    g = plugin.Verifier(gpu, 3)
+    big, _ = _proposal(clients, 1100)
+    assert v.VerifyProposal(big) == g.VerifyProposal(big)
+    for t in (0, 1037, 1099):
+        bad, _ = _proposal(clients, 1100, tamper=t)
+        with pytest.raises(plugin.VerifyError) as ei:
+            v.VerifyProposal(bad)
+        assert ei.value.index == t and "has an invalid signature" in str(ei.value)
+    g.close()
     v.close()
 
 
