@@ -68,9 +68,10 @@ void sbft_verifier_free(sbft_verifier* v);
  * Returns a negative SBFT_GV_E* only on an engine failure; an invalid point is stored and
  * every signature under it is rejected. */
 int sbft_verifier_add_consenter(sbft_verifier* v, uint64_t id, const uint8_t pubkey65[65]);
-/* Client-key registry (optional): requests signed by a registered key are verified by
- * VerifyProposal against that key's precomputed comb tables (the keyed
- * launch: no doublings, one wavefront per signature), the others by the generic launch.
+/* Client-key registry (optional): a proposal whose requests are all signed by registered keys
+ * (and that holds at least 1,025 of them) is verified by VerifyProposal against those keys'
+ * precomputed comb tables (the keyed launch: no doublings, four lanes per signature); any
+ * other proposal by the generic launch. Verdicts are the same either way.
  * pubkeys65: n x 65 bytes SEC1 uncompressed; keys that are not valid points are ignored.
  * Registration builds 512 KiB of tables per key per device (10,000 clients = 5 GB). */
 int sbft_verifier_add_clients(sbft_verifier* v, const uint8_t* pubkeys65, size_t n);

@@ -309,8 +309,9 @@ def test_request_batcher_coalesces_concurrent_callers(net):
 # ---- client-key registry: VerifyProposal on the keyed launch ------------------------------
 def test_verify_proposal_registered_clients(gpu, net):
     """With the clients' keys registered (sbft_verifier_add_clients), VerifyProposal verifies
-    their requests on the comb-table launch: same RequestInfos, same rejection (index and text)
-    as the generic path; a mix of registered and unregistered clients is split over both."""
+    a proposal whose keys are all registered on the comb-table launch (>= 1,025 requests): same
+    RequestInfos, same rejection (index and text) as the generic path; a proposal mixing
+    registered and unregistered clients, or a small one, takes the generic launch."""
     _, nodes, clients = net
     v = plugin.Verifier(gpu, 3)
     p, reqs = _proposal(clients, 120)
