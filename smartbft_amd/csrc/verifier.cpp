@@ -493,6 +493,15 @@ struct KeyMap {
             if (std::memcmp(keys[i].data(), k, 64) == 0) return ids[i];
         }
     }
+    // the slot find(k) probes first: fetched ahead while earlier lookups run (a 10k-key table
+    // is ~2 MB, mostly outside L2, and the lookups are otherwise serial misses)
+    void prefetch(const uint8_t* k) const {
+        if (ids.empty()) return;
+        const size_t i = hash(k) & (ids.size() - 1);
+        __builtin_prefetch(&ids[i]);
+        __builtin_prefetch(keys[i].data());
+        __builtin_prefetch(keys[i].data() + 63);
+    }
     void put(const uint8_t* k, uint32_t id) {
         if (2 * (count + 1) > ids.size()) {
             KeyMap bigger;
@@ -1028,11 +1037,15 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
         const size_t n = reqs.size();
         kid.resize(n);
         std::shared_lock<std::shared_mutex> g(v->clients_mu);
-        for (size_t i = 0; i < n; ++i)
+        constexpr size_t kAhead = 8;
+        for (size_t i = 0; i < n && i < kAhead; ++i) v->clients.prefetch(reqs[i].pub + 1);
+        for (size_t i = 0; i < n; ++i) {
+            if (i + kAhead < n) v->clients.prefetch(reqs[i + kAhead].pub + 1);
             if (!(kid[i] = v->clients.find(reqs[i].pub + 1))) {
                 kid.clear();
                 break;
             }
+        }
         return 0;
     };
     int info_rc = 0;
