@@ -391,7 +391,10 @@ bool parse_request(const uint8_t* d, size_t len, size_t base, Req& out) {
     return true;
 }
 
-bool parse_payload(const uint8_t* p, size_t len, std::vector<Req>& out) {
+// on_req(i) runs as soon as request i is parsed (its memory accesses then overlap the walk's
+// dependent loads)
+template <class F>
+bool parse_payload(const uint8_t* p, size_t len, std::vector<Req>& out, F&& on_req) {
     Reader r{p, len};
     uint32_t count;
     if (!r.u32(count)) return false;
@@ -405,8 +408,12 @@ bool parse_payload(const uint8_t* p, size_t len, std::vector<Req>& out) {
         const size_t at = r.pos;
         if (!r.take(l, q)) return false;
         if (!parse_request(q, l, at, out[i])) return false;
+        on_req(i);
     }
     return r.pos == len;
+}
+bool parse_payload(const uint8_t* p, size_t len, std::vector<Req>& out) {
+    return parse_payload(p, len, out, [](uint32_t) {});
 }
 
 struct Msg {
@@ -993,8 +1000,8 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     std::vector<Req>& reqs = scr.reqs;
     std::vector<uint8_t>& ok = scr.ok;
     // parse + per-request format checks -> the body offsets / lengths of the framed requests
-    auto prepare = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
-        if (!parse_payload(p->payload, p->payload_len, reqs)) {
+    auto prepare_cb = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len, auto&& on_req) -> int {
+        if (!parse_payload(p->payload, p->payload_len, reqs, on_req)) {
             put_err(err, err_cap, "malformed proposal payload");
             return SBFT_V_EFORMAT;
         }
@@ -1012,6 +1019,9 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
             len[i] = (uint32_t)reqs[i].body_len;
         }
         return 0;
+    };
+    auto prepare = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
+        return prepare_cb(off, len, [](uint32_t) {});
     };
     bool registered;
     {
@@ -1033,19 +1043,23 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     std::vector<uint32_t>& kid = scr.kid;
     kid.clear();
     auto prepare_keyed = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
-        if (int prc = prepare(off, len)) return prc;
-        const size_t n = reqs.size();
-        kid.resize(n);
+        // the key lookups ride along the parse: request i's map slot is prefetched as soon as
+        // it is parsed, and looked up kAhead requests later
+        constexpr uint32_t kAhead = 8;
+        bool all = true;
         std::shared_lock<std::shared_mutex> g(v->clients_mu);
-        constexpr size_t kAhead = 8;
-        for (size_t i = 0; i < n && i < kAhead; ++i) v->clients.prefetch(reqs[i].pub + 1);
-        for (size_t i = 0; i < n; ++i) {
-            if (i + kAhead < n) v->clients.prefetch(reqs[i + kAhead].pub + 1);
-            if (!(kid[i] = v->clients.find(reqs[i].pub + 1))) {
-                kid.clear();
-                break;
-            }
-        }
+        auto look = [&](uint32_t i) {
+            if (all && !(kid[i] = v->clients.find(reqs[i].pub + 1))) all = false;
+        };
+        const int prc = prepare_cb(off, len, [&](uint32_t i) {
+            if (i == 0) kid.resize(reqs.size());
+            v->clients.prefetch(reqs[i].pub + 1);
+            if (i >= kAhead) look(i - kAhead);
+        });
+        if (prc) return prc;
+        const uint32_t n = (uint32_t)reqs.size();
+        for (uint32_t i = n > kAhead ? n - kAhead : 0; i < n; ++i) look(i);
+        if (!all) kid.clear();
         return 0;
     };
     int info_rc = 0;
