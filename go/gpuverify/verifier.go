@@ -119,8 +119,9 @@ func (v *Verifier) AddConsenter(id uint64, pubkey65 []byte) error {
 	return nil
 }
 
-// AddClients registers client keys (65-byte SEC1 each, concatenated): their requests are
-// verified against precomputed comb tables (512 KiB per key and device).
+// AddClients registers client keys (65-byte SEC1 each, concatenated): a proposal whose
+// requests are all signed by registered keys (at least 1,025 of them) is verified against
+// their precomputed comb tables (512 KiB per key and device); others take the generic launch.
 func (v *Verifier) AddClients(pubkeys65 []byte) error {
 	if len(pubkeys65)%65 != 0 {
 		return errors.New("gpuverify: client keys must be 65-byte SEC1 records")
