@@ -57,13 +57,24 @@ typedef struct sbft_gv_opts {
     int32_t quad_max;       /* ... and of at most this many, its four-lane form (the u1*G comb on
                                lanes 2-3; measured no faster than the pair form, so off by default);
                                0 = default SBFT_GV_QUAD_MAX_DEFAULT, < 0 = never */
-    uint64_t reserved[3];
+    uint32_t slots_per_device; /* engine slots per selected device (0 = 1). Each slot owns a stream,
+                                  staging, G's comb table and the registered-key tables, and takes
+                                  one share of a split batch, exactly as a separate GPU would: with
+                                  k > 1 the multi-device split (shares, offset rebasing, verdict
+                                  placement, per-device host workers) runs on a single GPU. For
+                                  testing the split; a deployment leaves it 0. The environment
+                                  variable SBFT_GV_SLOTS_PER_DEVICE overrides it. */
+    uint32_t reserved32;
+    uint64_t reserved[2];
 } sbft_gv_opts;
 
 #define SBFT_GV_PAIR_MAX_DEFAULT 32768u
 /* The device-resident hash entry points (sbft_gv_sha256_dev, sbft_gv_sha256_verify_p256_dev)
- * read up to this many bytes past the end of a message (the hash kernel moves whole 16-B
- * pieces of whole steps into LDS): the blob must stay readable that far past its last message. */
+ * read no byte outside the 16-byte-aligned granules that hold message bytes (the hash kernel
+ * moves whole 16-B pieces into LDS and clamps every piece past a message's last granule onto
+ * it), so a blob sized exactly to its messages is safe. The host-buffer entry points stage the
+ * blob with this much slack, which the hash-measurement variants selected by SBFT_SHA_VARIANT
+ * (per-lane 68-byte block loads) need. */
 #define SBFT_GV_SHA_BLOB_PAD 256u
 #define SBFT_GV_QUAD_MAX_DEFAULT 0u
 
@@ -72,6 +83,8 @@ typedef struct sbft_gv_opts {
  * Verifier to consensus.Consensus.Verifier (pkg/consensus/consensus.go:36). */
 int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out);
 void sbft_gv_destroy(sbft_gv_ctx* ctx);
+/* Number of engine slots: the selected devices times slots_per_device. A host-buffer batch is
+ * split over this many shares. */
 int sbft_gv_device_count(const sbft_gv_ctx* ctx);
 /* The host-side batch split every host-buffer call uses (no GPU; pure arithmetic, exported so
  * the split is testable without devices): a batch of n >= min_split (0 = 65536) tuples on

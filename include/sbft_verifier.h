@@ -172,12 +172,15 @@ void sbft_compute_quorum(uint64_t n, int* q, int* f);
 int sbft_verify_prev_commit_signatures(sbft_verifier* v, const sbft_signature* sigs, size_t n,
                                        const sbft_proposal* prev, uint64_t curr_vseq, int* skipped,
                                        char* err, size_t err_cap);
-/* View.processCommits + voteVerifier.verifyVote (view.go:519-551, 820-849) with one GPU launch
- * per batch of arrived votes: votes whose digest differs from the proposal's are dropped
- * ("Got wrong digest at processCommits"), duplicates by signer are ignored (voteSet.registerVote,
- * util.go:123-136), the rest are verified together; valid_idx receives the indices of valid
- * votes in arrival order, at most `need` (= quorum - 1). log receives one line per rejected
- * vote ("Couldn't verify <id>'s signature: <reason>", view.go:840). */
+/* View.processCommits + voteVerifier.verifyVote (view.go:519-551, 820-849) with the batch hook
+ * of go/patches/internal_bft_commits.patch: votes are taken in arrival order; votes whose digest
+ * differs from the proposal's are dropped ("Got wrong digest at processCommits"), duplicates by
+ * signer are ignored (voteSet.registerVote, util.go:123-136); once the valid votes so far plus
+ * the pending ones can complete the quorum, the pending ones are verified in one GPU launch,
+ * and after an invalid vote the next arrivals form the next batch. Collection stops at `need`
+ * (= quorum - 1) valid votes: later votes are not verified. valid_idx receives the indices of
+ * the collected votes, log one line per rejected vote ("Couldn't verify <id>'s signature:
+ * <reason>", view.go:840). If the votes run out first, the pending ones are verified anyway. */
 int sbft_collect_commits(sbft_verifier* v, const sbft_signature* votes, const char* const* vote_digests,
                          size_t n, const sbft_proposal* p, size_t need, size_t* valid_idx,
                          size_t* n_valid, char* log, size_t log_cap);

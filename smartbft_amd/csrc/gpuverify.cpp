@@ -18,6 +18,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -91,6 +92,59 @@ struct Helper {
         }
         cv.notify_one();
         if (th.joinable()) th.join();
+    }
+};
+
+// Persistent host workers that drive the shares of a split batch: share i >= 1 of every call
+// runs on worker i (started on first use, kept for the context's life), share 0 on the
+// calling thread. A worker job only enqueues on, and synchronises, its own slot; it never waits
+// for another worker, so concurrent split calls queue per worker and cannot deadlock.
+struct Workers {
+    struct W {
+        std::mutex mu;
+        std::condition_variable cv;
+        std::vector<std::function<void()>> q;
+        std::thread th;
+        bool stop = false;
+        void loop() {
+            for (;;) {
+                std::vector<std::function<void()>> jobs;
+                {
+                    std::unique_lock<std::mutex> g(mu);
+                    cv.wait(g, [&] { return stop || !q.empty(); });
+                    if (q.empty()) return;  // stop, nothing left
+                    jobs.swap(q);
+                }
+                for (auto& f : jobs) f();
+            }
+        }
+    };
+    std::mutex mu;  // guards w's growth
+    std::vector<std::unique_ptr<W>> w;
+    void post(size_t i, std::function<void()> f) {
+        W* x;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            while (w.size() <= i) w.emplace_back(new W());
+            x = w[i].get();
+            std::lock_guard<std::mutex> gx(x->mu);
+            if (!x->th.joinable()) x->th = std::thread([x] { x->loop(); });
+        }
+        {
+            std::lock_guard<std::mutex> gx(x->mu);
+            x->q.push_back(std::move(f));
+        }
+        x->cv.notify_one();
+    }
+    ~Workers() {
+        for (auto& x : w) {
+            {
+                std::lock_guard<std::mutex> g(x->mu);
+                x->stop = true;
+            }
+            x->cv.notify_one();
+            if (x->th.joinable()) x->th.join();
+        }
     }
 };
 
@@ -392,6 +446,8 @@ constexpr size_t kShaLptMin = 65536;
 constexpr size_t kSignWaveMax = 4096;
 int sign_wave(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_t* digest, size_t n, uint8_t* qx,
               uint8_t* qy, uint8_t* r, uint8_t* s, uint8_t* status);
+// registered-key tables [0, upto) on a slot's device (defined with the registered-key code)
+int ensure_tables(Slot* sl, size_t upto);
 
 
 }  // namespace
@@ -430,7 +486,8 @@ struct sbft_gv_ctx {
     };
     std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_index;
     std::atomic<uint32_t> nkeys{1};
-    Helper helper;  // host work overlapped with a caller's copies (sbft_gv_framed_overlapped)
+    Helper helper;    // host work overlapped with a caller's copies (sbft_gv_framed_overlapped)
+    Workers workers;  // host threads driving shares 1.. of a split batch (for_each_device)
 };
 
 // the generator G, x || y big-endian (key id 0)
@@ -530,16 +587,26 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     if (opts && opts->quad_max) ctx->quad_max = opts->quad_max < 0 ? 0u : (uint32_t)opts->quad_max;
     if (const char* e = getenv("SBFT_KEYED_ZC_MAX")) ctx->keyed_zc_max = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("SBFT_KEYED_LANES_MIN")) ctx->keyed_lanes_min = (size_t)strtoull(e, nullptr, 10);
+    // slots per device (sbft_gv_opts.slots_per_device, SBFT_GV_SLOTS_PER_DEVICE): > 1 runs the
+    // multi-device split on one GPU, each slot standing in for a device of its own
+    uint32_t spd = opts && opts->slots_per_device ? opts->slots_per_device : 1u;
+    if (const char* e = getenv("SBFT_GV_SLOTS_PER_DEVICE")) spd = (uint32_t)strtoul(e, nullptr, 10);
+    if (spd == 0 || spd > 64) {
+        delete ctx;
+        return SBFT_GV_EINVAL;
+    }
     for (int d = 0; d < ndev && d < 32; ++d) {
         if (!(mask & (1u << d))) continue;
-        auto* s = new Slot();
-        s->device = d;
-        if (hipSetDevice(d) != hipSuccess ||
-            hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
-            delete s;
-            continue;
+        for (uint32_t k = 0; k < spd; ++k) {
+            auto* s = new Slot();
+            s->device = d;
+            if (hipSetDevice(d) != hipSuccess ||
+                hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+                delete s;
+                break;
+            }
+            ctx->slots.push_back(s);
         }
-        ctx->slots.push_back(s);
     }
     if (ctx->slots.empty()) {
         delete ctx;
@@ -800,18 +867,28 @@ std::vector<Chunk> plan(sbft_gv_ctx* ctx, size_t n) {
     return out;
 }
 
-// Run f(i) for i in [0, m): i = 0 on the calling thread, the others on threads of their own
-// (one per device chunk), so each device's pageable H2D copies and its synchronisation are
+// Run f(i) for i in [0, m): i = 0 on the calling thread, the others on the context's persistent
+// workers (worker i drives share i), so each device's pageable H2D copies and its synchronisation are
 // driven independently instead of one device after another. Returns the first non-zero rc.
 template <class F>
-int for_each_device(size_t m, F&& f) {
+int for_each_device(sbft_gv_ctx* ctx, size_t m, F&& f) {
     if (m == 1) return f((size_t)0);
     std::vector<int> rc(m, SBFT_GV_OK);
-    std::vector<std::thread> th;
-    th.reserve(m - 1);
-    for (size_t i = 1; i < m; ++i) th.emplace_back([&, i] { rc[i] = f(i); });
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t left = m - 1;
+    for (size_t i = 1; i < m; ++i)
+        ctx->workers.post(i, [&, i] {
+            const int r = f(i);
+            std::lock_guard<std::mutex> g(mu);
+            rc[i] = r;
+            if (--left == 0) cv.notify_one();
+        });
     rc[0] = f((size_t)0);
-    for (auto& t : th) t.join();
+    {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return left == 0; });
+    }
     for (int r : rc)
         if (r) return r;
     return SBFT_GV_OK;
@@ -956,9 +1033,16 @@ bool framed_fused_on() {
 // chunk's first message so each device receives only its slice of the blob.
 // framed: verify inputs are gathered on the device from the blob itself (r || s at message
 // end + sig_rel, x || y at message end + pub_rel) instead of copied from r, s, qx, qy.
+// kid (optional): registered client key id per message (all non-zero); a share of at least
+// keyed_min messages then takes the keyed launch over the clients' comb tables
+// (sbft_launch_p256_verify_keyed_framed, hash on a fifth wavefront), as the one-slot
+// VerifyProposal path does.
 struct Framing {
     bool on = false;
     int32_t sig_rel = 0, pub_rel = 0;
+    const uint32_t* kid = nullptr;
+    uint32_t nkeys = 0;
+    size_t keyed_min = 0;
 };
 int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uint64_t* off,
                  const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint8_t* qx,
@@ -988,6 +1072,26 @@ int enqueue_hash(const Chunk& c, const uint8_t* blob, size_t blob_len, const uin
     const size_t fo = align_up(8 * c.count, 256), fl = align_up(4 * c.count, 256);
     const size_t fd = align_up(32 * c.count, 256);
     const bool verify = ok_out != nullptr;
+    if (fr.on && verify && fr.kid && fr.keyed_min && c.count >= fr.keyed_min) {
+        // registered clients: blob | off | len | key ids | ok (caller holds sl->mu)
+        HIPCHK(hipSetDevice(sl->device));
+        const size_t fk = align_up(4 * c.count, 256);
+        int rc = ensure_tables(sl, fr.nkeys);
+        if (!rc) rc = sl->reserve(fb + fo + fl + fk + align_up(c.count, 256));
+        if (rc) return rc;
+        uint8_t* b = sl->dbuf;
+        uint8_t *d_blob = b, *d_off = b + fb, *d_len = d_off + fo, *d_kid = d_len + fl, *d_ok = d_kid + fk;
+        HIPCHK(hipMemcpyAsync(d_blob, blob + lo, span, hipMemcpyHostToDevice, sl->stream));
+        HIPCHK(hipMemcpyAsync(d_off, rebased.data(), 8 * c.count, hipMemcpyHostToDevice, sl->stream));
+        HIPCHK(hipMemcpyAsync(d_len, len + c.begin, 4 * c.count, hipMemcpyHostToDevice, sl->stream));
+        HIPCHK(hipMemcpyAsync(d_kid, fr.kid + c.begin, 4 * c.count, hipMemcpyHostToDevice, sl->stream));
+        if (sbft_launch_p256_verify_keyed_framed(d_blob, (const uint64_t*)d_off, (const uint32_t*)d_len, fr.sig_rel,
+                                                 (const uint32_t*)d_kid, (const void* const*)sl->d_keytab, fr.nkeys,
+                                                 d_ok, (uint32_t)c.count, sl->stream))
+            return SBFT_GV_ELAUNCH;
+        HIPCHK(hipMemcpyAsync(ok_out + c.begin, d_ok, c.count, hipMemcpyDeviceToHost, sl->stream));
+        return SBFT_GV_OK;
+    }
     // blob | off | len | work counter | digests [| r | s | qx | qy | ok | verify workspace]
     // [| longest-first sort scratch | order]
     const bool lpt = c.count >= kShaLptMin;
@@ -1098,7 +1202,7 @@ int enqueue_selftest(const Chunk& c, int op, const uint8_t* a, const uint8_t* b,
 template <class F>
 int run_chunks(sbft_gv_ctx* ctx, size_t n, F&& enqueue) {
     std::vector<Chunk> chunks = plan(ctx, n);
-    return for_each_device(chunks.size(), [&](size_t i) {
+    return for_each_device(ctx, chunks.size(), [&](size_t i) {
         const Chunk& c = chunks[i];
         std::lock_guard<std::mutex> lk(c.slot->mu);
         int rc = enqueue(c, i);
@@ -1204,10 +1308,6 @@ int sbft_gv_sha256_verify_p256_framed(sbft_gv_ctx* ctx, const uint8_t* blob, siz
 
 }  // extern "C"
 
-namespace {
-int ensure_tables(Slot* sl, size_t upto);
-}  // namespace
-
 int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob_len, int32_t sig_rel,
                               int32_t pub_rel,
                               const std::function<int(std::vector<uint64_t>&, std::vector<uint32_t>&)>& prepare,
@@ -1264,6 +1364,17 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
                             ? SBFT_GV_OK
                             : SBFT_GV_EDEVICE;
     const auto t3 = TC::now();
+    // From here the payload copy may still be in flight (possibly a DMA from the caller's
+    // page-locked buffer): every return drains this slot's stream first, so the caller's buffer
+    // is free and a copy fault is reported by this call, not by the slot's next user. (The
+    // launch paths end in a synchronisation of their own and disarm it.)
+    struct Drain {
+        hipStream_t st;
+        bool armed;
+        ~Drain() {
+            if (armed) (void)hipStreamSynchronize(st);
+        }
+    } drain{sl->stream, true};
     struct Tr {
         bool on;
         TC::time_point a, b, c, d;
@@ -1282,10 +1393,25 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     if (n == 0) return SBFT_GV_OK;
     if (len.size() != n || n > 0xffffffffu) return SBFT_GV_EINVAL;
     if (n >= ctx->min_split && ctx->slots.size() > 1) {  // large: the multi-device split path
+        // each share copies its own slice of the payload: this slot's copy is not used
+        drain.armed = false;
+        if (hipStreamSynchronize(sl->stream) != hipSuccess) return SBFT_GV_EDEVICE;
         lk.unlock();
         if (during) during();
-        return sbft_gv_sha256_verify_p256_framed(ctx, blob, blob_len, off.data(), len.data(), n, sig_rel, pub_rel,
-                                                 ok.data());
+        Framing fr;
+        fr.on = true;
+        fr.sig_rel = sig_rel;
+        fr.pub_rel = pub_rel;
+        if (kid && kid->size() == n) {
+            fr.kid = kid->data();
+            fr.nkeys = (uint32_t)ctx->nkeys.load();
+            fr.keyed_min = ctx->keyed_lanes_min;
+        }
+        std::vector<std::vector<uint64_t>> rebased(ctx->slots.size() + 1);
+        return run_chunks(ctx, n, [&](const Chunk& c, size_t i) {
+            return enqueue_hash(c, blob, blob_len, off.data(), len.data(), nullptr, nullptr, nullptr, nullptr,
+                                ok.data(), nullptr, rebased[i], fr);
+        });
     }
     for (size_t k = 0; k < n; ++k) {
         if (off[k] + len[k] > blob_len || off[k] + len[k] < off[k]) return SBFT_GV_EINVAL;
@@ -1297,7 +1423,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     // prepare): the keyed four-lane kernel over the clients' comb tables, hashing on a fifth
     // wavefront per workgroup and reading r || s from the payload; key ids beside the offsets
     // in mapped host memory. Smaller batches go through the caller's other paths.
-    if (kid && kid->size() == n && n >= ctx->keyed_lanes_min) {
+    if (kid && kid->size() == n && ctx->keyed_lanes_min && n >= ctx->keyed_lanes_min) {
         const uint32_t nkeys = (uint32_t)ctx->nkeys.load();
         const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256);
         rc = ensure_tables(sl, nkeys);
@@ -1315,6 +1441,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         HIPCHK(hipMemcpyAsync(ok.data(), sl->dbuf, n, hipMemcpyDeviceToHost, sl->stream));
         if (during) during();
         HIPCHK(hipStreamSynchronize(sl->stream));
+        drain.armed = false;
         return SBFT_GV_OK;
     }
     // Device: hash counter (256) | verify workspace | digests | r | s | qx | qy | ok. The
@@ -1358,6 +1485,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     HIPCHK(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, sl->stream));
     if (during) during();  // the caller's host work that does not need the verdicts, under the launch
     HIPCHK(hipStreamSynchronize(sl->stream));
+    drain.armed = false;
     return SBFT_GV_OK;
 }
 
@@ -1772,7 +1900,7 @@ int run_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* blob, size
               uint8_t* ok_out) {
     const uint32_t nkeys = (uint32_t)ctx->nkeys.load();  // published keys
     std::vector<Chunk> chunks = plan(ctx, n);
-    return for_each_device(chunks.size(), [&](size_t i) {
+    return for_each_device(ctx, chunks.size(), [&](size_t i) {
         Chunk& c = chunks[i];
         if (c.count <= ctx->keyed_zc_max) {
             // zero-copy: the slot lock only for the tables, then a lane of its own
@@ -1884,9 +2012,16 @@ int sbft_gv_register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy
             std::lock_guard<std::mutex> lk(sl->mu);
             if (sl->comb.size() > before) {
                 (void)hipSetDevice(sl->device);
-                (void)hipFree(sl->comb_alloc.back());
+                (void)hipStreamSynchronize(sl->stream);
+                void* block = sl->comb_alloc.back();
+                // a slot that had no table yet built [0, upto) in this block, G's included:
+                // forget them all, so G's table is rebuilt on next use instead of pointing
+                // at freed memory
+                const bool holds_g = !sl->comb.empty() && sl->comb[0] == block;
+                (void)hipFree(block);
                 sl->comb_alloc.pop_back();
-                sl->comb.resize(before);
+                if (holds_g) sl->comb.clear();
+                else sl->comb.resize(before);
             }
         }
         for (size_t id = before; id < upto; ++id) ctx->key_index.erase(ctx->keys[id]);

@@ -158,18 +158,37 @@ struct ShaQueue {
     }
 };
 
-// One step's DMA: slot s = m * 64 + lane fetches its P pieces from chunk[m] of its owner lane.
+// The last 16-B granule a fetch for a message may touch: the one holding its last byte (for an
+// empty message the byte before it, or the blob's first granule). Pieces past it are clamped
+// onto it, so the DMA never reads beyond the granules that hold message bytes: no blob padding
+// is needed, and a blob sized exactly to its messages cannot fault. (The bytes past a message's
+// end are masked off by the tail code either way.)
+__device__ __forceinline__ uint64_t sha_last_granule(uint64_t base, uint32_t ml, uint64_t blob0) {
+    const uint64_t last = ml ? base + ml - 1 : (base > blob0 ? base - 1 : base);
+    return last & ~(uint64_t)15;
+}
+
+// One step's DMA: slot s = m * 64 + lane fetches its P pieces from chunk[m] of its owner lane,
+// none past the slot's limit granule lim[m]. The owner packs its chunk address, moved two
+// granules down, with d' = 2 + (granules from the chunk to the limit, at least -1: a step
+// starts at most 8 bytes past its message's end) saturated to 15 into one 64-bit value; piece j
+// then reads granule min(j + 2, d') of that base: one and, one min and one add per piece.
 template <int C, int M>
-__device__ __forceinline__ void sha_lds_fetch(uint8_t* buf, const uint64_t (&chunk)[M], uint32_t lane) {
+__device__ __forceinline__ void sha_lds_fetch(uint8_t* buf, const uint64_t (&chunk)[M], const uint64_t (&lim)[M],
+                                              uint32_t lane) {
     typedef __attribute__((address_space(3))) void* lptr;
     typedef __attribute__((address_space(1))) void* gptr;
     constexpr int P = 4 * C + 1;
+    static_assert(P + 1 <= 15, "the piece index + 2 must fit the 4-bit limit field");
     uint32_t alo[M], ahi[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
         const uint64_t a = chunk[m] & ~(uint64_t)15;
-        alo[m] = (uint32_t)a;
-        ahi[m] = (uint32_t)(a >> 32);
+        const int64_t dg = ((int64_t)lim[m] - (int64_t)a) >> 4;
+        const uint32_t dp = dg >= 13 ? 15u : dg <= -2 ? 0u : (uint32_t)(dg + 2);
+        const uint64_t ab = (a - 32) | dp;
+        alo[m] = (uint32_t)ab;
+        ahi[m] = (uint32_t)(ab >> 32);
     }
 #pragma unroll
     for (int i = 0; i < M * P; ++i) {
@@ -185,7 +204,8 @@ __device__ __forceinline__ void sha_lds_fetch(uint8_t* buf, const uint64_t (&chu
                 hi = h;
             }
         }
-        const uint64_t src = (((uint64_t)hi << 32) | lo) + 16u * piece;
+        const uint32_t pe = min(piece + 2u, lo & 15u);
+        const uint64_t src = (((uint64_t)hi << 32) | (lo & ~15u)) + 16u * pe;
         __builtin_amdgcn_global_load_lds((gptr)(uintptr_t)src, (lptr)(buf + i * 1024), 16, 0, 0);
     }
 }
@@ -217,7 +237,7 @@ __global__ __launch_bounds__(256) void sha256_lds_kernel(const uint8_t* __restri
     // this lane's M current messages: index, length, blocks, next block, start address, state
     bool act[M];
     uint32_t mi[M], ml[M], nb[M], b[M];
-    uint64_t base[M], pf[M];
+    uint64_t base[M], pf[M], pl[M];
     uint32_t h[M][8];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -233,8 +253,9 @@ __global__ __launch_bounds__(256) void sha256_lds_kernel(const uint8_t* __restri
         }
         sha_init(h[m]);
         pf[m] = base[m];
+        pl[m] = sha_last_granule(base[m], ml[m], blob0);
     }
-    sha_lds_fetch<C, M>(wbuf, pf, lane);
+    sha_lds_fetch<C, M>(wbuf, pf, pl, lane);
     for (uint32_t t = 0;; ++t) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step t's rows have landed
         bool any = false;
@@ -254,16 +275,19 @@ __global__ __launch_bounds__(256) void sha256_lds_kernel(const uint8_t* __restri
             nmi[m] = nml[m] = 0;
             nbase[m] = blob0;
             pf[m] = blob0;
+            pl[m] = blob0 & ~(uint64_t)15;
             if (fin[m] && nidx[m] < n) {
                 nmi[m] = order ? order[nidx[m]] : nidx[m];
                 nml[m] = len[nmi[m]];
                 nbase[m] += off[nmi[m]];
                 pf[m] = nbase[m];
+                pl[m] = sha_last_granule(nbase[m], nml[m], blob0);
             } else if (act[m] && !fin[m]) {
                 pf[m] = base[m] + 64ull * (b[m] + C);
+                pl[m] = sha_last_granule(base[m], ml[m], blob0);
             }
         }
-        if (DB) sha_lds_fetch<C, M>(wbuf + ((t + 1u) & 1u) * L::BUF, pf, lane);
+        if (DB) sha_lds_fetch<C, M>(wbuf + ((t + 1u) & 1u) * L::BUF, pf, pl, lane);
 #pragma unroll
         for (int j = 0; j < C; ++j) {
             uint32_t w[M][16];
@@ -316,7 +340,7 @@ __global__ __launch_bounds__(256) void sha256_lds_kernel(const uint8_t* __restri
             for (int m = 0; m < M; ++m) any_live = any_live || live[m];
             if (any_live) compress_multi<M>(h, w, live);
         }
-        if (!DB) sha_lds_fetch<C, M>(wbuf, pf, lane);  // the step's reads are consumed: refill in place
+        if (!DB) sha_lds_fetch<C, M>(wbuf, pf, pl, lane);  // the step's reads are consumed: refill in place
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             if (fin[m]) {

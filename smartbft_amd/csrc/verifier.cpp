@@ -1328,30 +1328,43 @@ int sbft_collect_commits(sbft_verifier* v, const sbft_signature* votes, const ch
     char expected[65];
     v->digest_of(p, expected);
     std::string lg;
-    std::vector<size_t> cand;
-    std::vector<sbft_signature> batch;
+    std::vector<size_t> pend;  // arrived, pre-checked votes not verified yet (in arrival order)
     std::unordered_map<uint64_t, bool> seen;
-    for (size_t i = 0; i < n; ++i) {
-        if (seen.count(votes[i].id)) continue;  // voteSet.registerVote: one vote per signer
+    // one batch call over the pending votes, as go/patches/internal_bft_commits.patch does
+    auto run = [&]() -> int {
+        std::vector<sbft_signature> batch;
+        batch.reserve(pend.size());
+        for (size_t i : pend) batch.push_back(votes[i]);
+        std::vector<int32_t> st(batch.size());
+        std::vector<std::string> why;
+        const int rc = v->consenter_batch(batch.data(), batch.size(), p, st.data(), &why);
+        if (rc) return rc;
+        for (size_t k = 0; k < batch.size(); ++k) {
+            if (st[k]) {
+                lg += "Couldn't verify " + std::to_string(batch[k].id) + "'s signature: " + why[k] + "\n";
+                continue;
+            }
+            if (*n_valid < need) valid_idx[(*n_valid)++] = pend[k];
+        }
+        pend.clear();
+        return 0;
+    };
+    for (size_t i = 0; i < n && *n_valid < need; ++i) {  // the quorum complete: the loop returns
+        if (seen.count(votes[i].id)) continue;             // voteSet.registerVote: one vote per signer
         seen[votes[i].id] = true;
         if (!vote_digests[i] || std::strcmp(vote_digests[i], expected) != 0) {
             lg += "Got wrong digest at processCommits\n";
             continue;
         }
-        cand.push_back(i);
-        batch.push_back(votes[i]);
+        pend.push_back(i);
+        // enough arrived to complete the quorum if all are valid: verify them as one batch
+        if (*n_valid + pend.size() >= need)
+            if (const int rc = run()) return rc;
     }
-    std::vector<int32_t> st(batch.size());
-    std::vector<std::string> why;
-    const int rc = v->consenter_batch(batch.data(), batch.size(), p, st.data(), &why);
-    if (rc) return rc;
-    for (size_t k = 0; k < batch.size(); ++k) {
-        if (st[k]) {
-            lg += "Couldn't verify " + std::to_string(batch[k].id) + "'s signature: " + why[k] + "\n";
-            continue;
-        }
-        if (*n_valid < need) valid_idx[(*n_valid)++] = cand[k];
-    }
+    // arrivals ended with the quorum still short (the library would keep waiting): verify what
+    // arrived, so every rejected vote is logged
+    if (!pend.empty())
+        if (const int rc = run()) return rc;
     if (log && log_cap) {
         const size_t m = std::min(log_cap - 1, lg.size());
         std::memcpy(log, lg.data(), m);
@@ -1589,6 +1602,9 @@ static int presign_refill(sbft_signer* s, size_t m) {
     std::memset(kk.data(), 0, kk.size());
     std::memset(dd.data(), 0, dd.size());
     if (rc) return rc;
+    // no growth inside the loop: a reallocation would free a buffer still holding
+    // pre-signatures (any one reveals d = B / (A r))
+    s->pool.reserve(s->pool.size() + m);
     for (size_t i = 0; i < m; ++i) {
         if (!st[2 * i] || !st[2 * i + 1]) continue;  // s came out 0 for this nonce: skip it
         sbft_signer::Presig p;
@@ -1609,8 +1625,12 @@ static int presign_refill(sbft_signer* s, size_t m) {
         sbft::modn::add_mod(p.a, s1, neg);
         std::memcpy(p.b, s0, sizeof s0);
         s->pool.push_back(p);
+        explicit_bzero(&p, sizeof p);
+        explicit_bzero(s0, sizeof s0);
+        explicit_bzero(s1, sizeof s1);
+        explicit_bzero(neg, sizeof neg);
     }
-    std::memset(sv.data(), 0, sv.size());
+    explicit_bzero(sv.data(), sv.size());
     return 0;
 }
 
@@ -1671,7 +1691,9 @@ int sbft_signer_sign(sbft_signer* s, const uint8_t* data, size_t len, uint8_t si
                 std::memcpy(sig64, p.r, 32);
                 sbft::modn::to_be32(sig64 + 32, sg);
             }
-            std::memset(&p, 0, sizeof p);
+            explicit_bzero(&p, sizeof p);
+            explicit_bzero(t, sizeof t);
+            explicit_bzero(sg, sizeof sg);
             if (zero) continue;  // s = 0: take the next nonce
             return 0;
         }

@@ -37,7 +37,8 @@ class GpuVerifyError(RuntimeError):
 class Opts(ctypes.Structure):
     _fields_ = [("device_mask", ctypes.c_uint32), ("min_split", ctypes.c_uint32),
                 ("pair_max", ctypes.c_int32), ("quad_max", ctypes.c_int32),
-                ("reserved", ctypes.c_uint64 * 3)]
+                ("slots_per_device", ctypes.c_uint32), ("reserved32", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint64 * 2)]
 
 
 _LIB = None
@@ -205,12 +206,15 @@ class GpuVerifier:
     """One sbft_gv_ctx. Host-array calls are synchronous; *_dev calls take torch tensors
     (device-resident) and enqueue on the given (or current) stream."""
 
-    def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0, quad_max: int = 0):
+    def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0, quad_max: int = 0,
+                 slots_per_device: int = 0):
         """pair_max / quad_max: per-device batches of at most this many tuples run the latency
-        kernel with two / four lanes per tuple (0 = library default, negative = never)."""
+        kernel with two / four lanes per tuple (0 = library default, negative = never).
+        slots_per_device > 1: that many engine slots per GPU, each taking a share of a split
+        batch as a separate device would (runs the multi-device split on one GPU)."""
         self.L = load_library()
         ctx = _vp()
-        opts = Opts(device_mask, min_split, pair_max, quad_max)
+        opts = Opts(device_mask, min_split, pair_max, quad_max, slots_per_device)
         rc = self.L.sbft_gv_init(ctypes.byref(opts), ctypes.byref(ctx))
         if rc:
             raise GpuVerifyError(f"sbft_gv_init: {self.L.sbft_gv_strerror(rc).decode()} ({rc})")
@@ -388,6 +392,10 @@ class GpuVerifier:
         n = d_ok.numel()
         if d_off.dtype not in (torch.int64, torch.uint64) or d_len.dtype not in (torch.int32, torch.uint32):
             raise ValueError("offsets must be 64-bit and lengths 32-bit integers")
+        if d_blob.dtype != torch.uint8 or not d_blob.is_contiguous() or not d_blob.is_cuda:
+            raise ValueError("blob: expected a contiguous uint8 device tensor")
+        if n and int((d_off.to(torch.int64) + d_len.to(torch.int64)).max()) > d_blob.numel():
+            raise ValueError("a message extends past the end of the blob")
         p = [_dev(t, 32 * n, w) for t, w in ((d_r, "r"), (d_s, "s"), (d_qx, "qx"), (d_qy, "qy"))]
         self._check(self.L.sbft_gv_sha256_verify_p256_dev(
             self.ctx, d_ok.device.index, d_blob.data_ptr(), _dev(d_off, n, "offsets", d_off.dtype),
@@ -406,7 +414,8 @@ class GpuVerifier:
 
     def sha256_dev(self, d_blob, d_off, d_len, d_dig, stream=None, d_order=None):
         """d_off int64/uint64 offsets, d_len int32 lengths, d_order (optional) int32 permutation;
-        the blob must be readable 128 bytes past its last message (the hash kernel's over-read)."""
+        the hash kernel reads nothing outside the 16-byte granules holding message bytes, so
+        the blob needs no padding; offsets + lengths are checked against its size here."""
         import torch
         n = d_off.numel()
         if d_blob.dtype != torch.uint8 or not d_blob.is_contiguous() or not d_blob.is_cuda:
@@ -414,6 +423,8 @@ class GpuVerifier:
         if d_off.dtype not in (torch.int64, torch.uint64):
             raise ValueError(f"offsets: expected 64-bit integers, got {d_off.dtype}")
         p_off = _dev(d_off, n, "offsets", d_off.dtype)
+        if n and int((d_off.to(torch.int64) + d_len.to(torch.int64)).max()) > d_blob.numel():
+            raise ValueError("a message extends past the end of the blob")
         p_len = _dev(d_len, n, "lengths", d_len.dtype if d_len.dtype in (torch.int32, torch.uint32) else torch.int32)
         p_ord = _dev(d_order, n, "order", d_order.dtype if d_order.dtype in (torch.int32, torch.uint32)
                      else torch.int32) if d_order is not None else None
