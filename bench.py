@@ -64,6 +64,11 @@ def parse():
                          "(sbft_gv_opts.slots_per_device), each with its own N-tuple workload and stream, "
                          "standing in for K GPUs (the step launches all K; the host-buffer rate splits "
                          "one call over the K slots). Not a scaling measurement: K slots share one GPU")
+    ap.add_argument("--split", type=int, default=1,
+                    help="A/B tool: cut each device's step into S equal sub-batches (contiguous slices)")
+    ap.add_argument("--split-streams", type=int, default=1,
+                    help="A/B tool: run the sub-batches over this many streams, forked from and joined "
+                         "back into the step's stream every step")
     return ap.parse_args()
 
 
@@ -509,9 +514,28 @@ def main():
     wl, ok, stream = wls[0], oks[0], streams[0]
     rehearsal = slots > 1
 
+    S, SS = max(1, args.split), max(1, args.split_streams)
+    subs = [[torch.cuda.Stream(device=torch.device(f"cuda:{d}")) for _ in range(SS - 1)] for d in lanes]
+
     def step():
-        for w, o, st, d in zip(wls, oks, streams, lanes):  # asynchronous: every device runs concurrently
-            gv.verify_dev(w.digest, w.r, w.s, w.qx, w.qy, o, st)
+        for j, (w, o, st, d) in enumerate(zip(wls, oks, streams, lanes)):  # asynchronous: every device runs concurrently
+            if S == 1:
+                gv.verify_dev(w.digest, w.r, w.s, w.qx, w.qy, o, st)
+                continue
+            # A/B: S sub-batches over SS streams, forked from st and joined back into it
+            fork = torch.cuda.Event()
+            fork.record(st)
+            pool = [st] + subs[j]
+            for x in subs[j]:
+                x.wait_event(fork)
+            for i in range(S):
+                lo, hi = n * i // S, n * (i + 1) // S
+                gv.verify_dev(w.digest[lo:hi], w.r[lo:hi], w.s[lo:hi], w.qx[lo:hi], w.qy[lo:hi], o[lo:hi],
+                              pool[i % SS])
+            for x in subs[j]:
+                ev = torch.cuda.Event()
+                ev.record(x)
+                st.wait_event(ev)
 
     def sync_all():
         for d in devs:
@@ -550,14 +574,14 @@ def main():
     avg_step_gpu_ms = sum(step_ms) / len(step_ms)
     launches, kern_total_ms = gv.kernel_time()
     gv.kernel_timing(False)
-    assert launches == args.steps * len(lanes), (launches, args.steps)
+    assert launches == args.steps * len(lanes) * S, (launches, args.steps)
     avg_kern_s = kern_total_ms / launches / 1e3
     n_gpus = world * len(devs)
 
     if rank == 0:
         total = n * world * len(lanes) * args.steps
         value = total / elapsed
-        achieved_t = n * PRODUCTS_PER_VERIFY / avg_kern_s / 1e12
+        achieved_t = n / S * PRODUCTS_PER_VERIFY / avg_kern_s / 1e12
         traffic = None
         instr_per_verify = None
         if os.path.exists(args.traffic_file):

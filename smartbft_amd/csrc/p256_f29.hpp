@@ -266,6 +266,58 @@ SBFT_DEV void f29_normalize(f29& r, const f29& a) {
     r = t;
 }
 
+// ---------------------------------------------------------------- exact zero tests mod p
+// Common tail: limbs 0..7 in [0, 2^29), limb 8 signed, |x| < 2^258. The bits at 2^256 and up,
+// h = limb8 >> 24 (|h| <= 4), are folded with 2^256 = 2^224 - 2^192 - 2^96 + 1 (mod p):
+// y = (x mod 2^256) + h (2^224 - 2^192 - 2^96 + 1) lies in (-p, 2p), so after one carry pass
+// x == 0 (mod p) iff y's limbs are all 0 or are p's.
+SBFT_DEV bool f29_zero_tail(const u32 (&a)[9]) {
+    const i32 h = (i32)a[8] >> 24;
+    i32 v[9];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (i32)a[i];
+    v[8] = (i32)(a[8] & 0x00FFFFFFu);
+    v[7] += h * (1 << 21);
+    v[6] -= h * (1 << 18);
+    v[3] -= h * (1 << 9);
+    v[0] += h;
+    i32 c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const i32 x = v[i] + c;
+        v[i] = x & (i32)F29_MASK;
+        c = x >> 29;
+    }
+    v[8] += c;
+    constexpr u32 P29[9] = {0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x000001ffu, 0u, 0u, 0x00040000u, 0x1fe00000u,
+                            0x00ffffffu};
+    u32 z = 0, q = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        z |= (u32)v[i];
+        q |= (u32)v[i] ^ P29[i];
+    }
+    return z == 0 || q == 0;
+}
+// x == 0 (mod p) for x in normal form (an f29_mul / f29_sqr output): exact, ~50 VALU
+// instructions, no multiplication (f29_canon_plain costs a product and a subtraction loop).
+SBFT_DEV bool f29_zero_mod_p(const f29& a) { return f29_zero_tail(a.v); }
+// The same for any x with |limb| < 2^31 and |x| < 2^260 (normalised and carried first).
+SBFT_DEV bool f29_zero_mod_p_any(const f29& a) {
+    f29 t;
+    f29_normalize(t, a);  // limbs 0..7 in (-2^26, 2^29 + 2^26), limb 8 in [0, 2^24), |x| < 2^257
+    u32 v[9];
+    i32 c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const i32 x = (i32)t.v[i] + c;
+        v[i] = (u32)x & F29_MASK;
+        c = x >> 29;
+    }
+    v[8] = t.v[8] + (u32)c;
+    return f29_zero_tail(v);
+}
+
 // ---------------------------------------------------------------- points
 struct jp29 {
     f29 x, y, z;
@@ -489,6 +541,42 @@ SBFT_DEV void p29_add_jac_lean(jp29& acc, const jp29& b) {
 SBFT_DEV void p29_add_aff_lean(jp29& acc, const f29& x2, const f29& y2) {
     if (SBFT_F29_IL & 4) p29_add_aff_lean_i(acc, x2, y2);
     else p29_add_aff_lean_s(acc, x2, y2);
+}
+
+// ---------------------------------------------------------------- exceptional additions
+// The lean mixed addition has no case analysis: for acc == +-P (H == 0) it returns Z3 = 0.
+// In the verify ladders this can happen only at additions an attacker can aim at (the last
+// addition of the u2 Q ladder, any comb addition of u1 G on top of u2 Q, see p256_verify.hip),
+// and a crafted request must not cost more than an honest one (a rejected proposal triggers
+// complain + sync, view.go:386-393). So after those additions:
+//   hz = Z3 == 0 (exact; Z3 = Z1 H with Z1 != 0, so H == 0): then X3 = r^2, and r == 0 (the
+//   addend equals acc: the result is 2P, a doubling of the affine addend) iff X3 == 0, else the
+//   addend is -acc and the result is infinity (flag inf);
+//   inf (acc was infinity): the result is the addend itself.
+// The repair runs in a wave-uniform branch taken only when some lane of the wave needs it, so
+// an honest batch pays the ~50-instruction zero test per addition. reload(x, y) re-materialises
+// the addend (from the table or the comb in memory) instead of keeping it live across the
+// addition; dbl(p) doubles in place (the kernel's doubling: one lane or a lane pair).
+template <class Dbl, class Reload>
+SBFT_DEV void add_aff_fix(jp29& acc, bool& inf, Dbl dbl, Reload reload) {
+    const bool hz = !inf && f29_zero_mod_p(acc.z);
+    if (__builtin_expect(__any(hz || inf), 0)) {
+        f29 x2, y2;
+        reload(x2, y2);
+        const bool twice = hz && f29_zero_mod_p_any(acc.x);
+        jp29 d;
+        d.x = x2;
+        d.y = y2;
+        d.z = f29_const(C29_ONE);
+        dbl(d);
+        if (twice) acc = d;
+        if (inf) {
+            acc.x = x2;
+            acc.y = y2;
+            acc.z = f29_const(C29_ONE);
+        }
+        inf = hz && !twice;
+    }
 }
 
 // ---------------------------------------------------------------- lane pairs (latency kernel)
@@ -783,11 +871,12 @@ SBFT_DEV fe f29_canon_plain(const f29& a) {
     return lo;
 }
 
-// The lean additions leave Z = 0 from the first exceptional case on (P + P, P + (-P),
-// R = infinity), so Z == 0 (mod p) flags the tuple for the general path (exc). Otherwise
-// x(R) mod n == r is checked projectively: X == r Z^2 or, when r + n < p, X == (r + n) Z^2.
+// Exceptional additions done in place (add_aff_careful below) leave R = infinity as the
+// caller's flag; a lean addition that met one anyway leaves Z = 0 from there on, so
+// Z == 0 (mod p) flags the tuple for the general path (exc). Otherwise x(R) mod n == r is
+// checked projectively: X == r Z^2 or, when r + n < p, X == (r + n) Z^2. acc.z in normal form.
 SBFT_DEV bool verify_final(const jp29& acc, const fe& rv, bool& exc) {
-    exc = fe_is_zero_raw(f29_canon_plain(acc.z));
+    exc = f29_zero_mod_p(acc.z);
     const f29 r2 = f29_const(C29_R2);
     f29 z2, lhs, rm;
     f29_sqr(z2, acc.z);

@@ -721,12 +721,25 @@ SBFT_DEV int q_digit(const fe& k2, int i) {
 // PINGPONG (latency kernel): two entry buffers in fixed registers, loop unrolled by two, so
 // that the next entry's loads are never waited on to shuffle registers (at one wave per SIMD
 // the rotated one-buffer loop exposed an HBM round trip per addition).
-template <bool PINGPONG = false, class AddAff>
-SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __restrict__ gcomb, AddAff add) {
+// fix(reload) runs after every addition (add_aff_fix: the comb's points are added on top of
+// u2 Q, so with a crafted Q any of them can meet acc == +-entry); reload(x, y) reloads the entry
+// just added.
+template <bool PINGPONG = false, class AddAff, class Fix>
+SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __restrict__ gcomb, AddAff add,
+                           Fix fix) {
     constexpr int T = kGK + 1;  // entries summed
     fe k1 = u1;
     uint4 cur[5], nxt[5];
     int dneg_cur = 0, dneg_nxt = 0;
+    auto entry_xy = [neg1](const uint4* e, int dn, f29& gx, f29& gy) {
+        const u32* w = reinterpret_cast<const u32*>(e);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            gx.v[k] = w[k];
+            gy.v[k] = w[10 + k];
+        }
+        if ((dn != 0) != neg1) f29_neg(gy, gy);
+    };
     // digit i of u1 -> (entry pointer, negative?)
     auto digit = [&](int i, const uint4*& ptr, int& neg) {
         if (i < kGK) {
@@ -746,38 +759,39 @@ SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __re
     };
     const uint4* ptr;
     if (PINGPONG) {
-        auto add_entry = [&](const uint4 (&en)[5], int dn) {
+        const uint4 *pc = nullptr, *pn = nullptr;  // the buffers' entry addresses (for the reload)
+        auto add_entry = [&](const uint4 (&en)[5], int dn, const uint4* src) {
             f29 gx, gy;
-            const u32* w = reinterpret_cast<const u32*>(en);
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                gx.v[k] = w[k];
-                gy.v[k] = w[10 + k];
-            }
-            if ((dn != 0) != neg1) f29_neg(gy, gy);
+            entry_xy(en, dn, gx, gy);
             add(acc, gx, gy);
+            fix([&](f29& x, f29& y) { entry_xy(src, dn, x, y); });
         };
         digit(0, ptr, dneg_cur);
+        pc = ptr;
 #pragma unroll
         for (int k = 0; k < 5; ++k) cur[k] = ptr[k];
         int i = 0;
 #pragma unroll 1
         for (; i + 1 < T; i += 2) {
             digit(i + 1, ptr, dneg_nxt);
+            pn = ptr;
 #pragma unroll
             for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
-            add_entry(cur, dneg_cur);
+            add_entry(cur, dneg_cur, pc);
             if (i + 2 < T) {
                 digit(i + 2, ptr, dneg_cur);
+                pc = ptr;
 #pragma unroll
                 for (int k = 0; k < 5; ++k) cur[k] = ptr[k];
             }
-            add_entry(nxt, dneg_nxt);
+            add_entry(nxt, dneg_nxt, pn);
         }
-        if (i < T) add_entry(cur, dneg_cur);  // odd entry count: the last one
+        if (i < T) add_entry(cur, dneg_cur, pc);  // odd entry count: the last one
         return;
     }
+    const uint4 *pc = nullptr, *pn = nullptr;
     digit(0, ptr, dneg_nxt);
+    pn = ptr;
 #pragma unroll
     for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
 #pragma unroll 1
@@ -785,20 +799,18 @@ SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __re
 #pragma unroll
         for (int k = 0; k < 5; ++k) cur[k] = nxt[k];
         dneg_cur = dneg_nxt;
+        pc = pn;
         if (i + 1 < T) {
             digit(i + 1, ptr, dneg_nxt);
+            pn = ptr;
 #pragma unroll
             for (int k = 0; k < 5; ++k) nxt[k] = ptr[k];
         }
         f29 gx, gy;
-        const u32* w = reinterpret_cast<const u32*>(cur);
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            gx.v[k] = w[k];
-            gy.v[k] = w[10 + k];
-        }
-        if ((dneg_cur != 0) != neg1) f29_neg(gy, gy);
+        entry_xy(cur, dneg_cur, gx, gy);
         add(acc, gx, gy);
+        const int dn = dneg_cur;
+        fix([&](f29& x, f29& y) { entry_xy(pc, dn, x, y); });
     }
 }
 
@@ -850,24 +862,39 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     acc.y = ty[0];
     acc.z = f29_const(C29_ONE);
     if (neg2) f29_neg(acc.y, acc.y);
-    // the accumulator starts at +-Q (the 2^(wK) term of u2)
+    // the accumulator starts at +-Q (the 2^(wK) term of u2). With odd digits the partial scalar
+    // m of the ladder is odd and 16 m > |d| until the last digit, where 16 m = n + d is possible
+    // (u2 = n - 2|d|, P + P): only the last addition can be exceptional (add_aff_fix).
     const fe k2 = u2;
-#pragma unroll 1
-    for (int i = kQDigits - 1; i >= 0; --i) {
-#pragma unroll kDblUnroll
-        for (int d = 0; d < kQWin; ++d) p29_dbl(acc, acc);
+    bool inf = false;  // acc is the point at infinity (add_aff_fix)
+    auto dbl1 = [](jp29& p) { p29_dbl(p, p); };
+    auto entry = [&](int i, f29& x2, f29& y2) __attribute__((always_inline)) {
         const int d2 = q_digit(k2, i);
         const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
-        const f29 x2 = tx[m2];
-        f29 y2 = ty[m2];
+        x2 = tx[m2];
+        y2 = ty[m2];
         if ((d2 < 0) != neg2) f29_neg(y2, y2);
+    };
+    auto digit_step = [&](int i) __attribute__((always_inline)) {
+#pragma unroll kDblUnroll
+        for (int d = 0; d < kQWin; ++d) p29_dbl(acc, acc);
+        f29 x2, y2;
+        entry(i, x2, y2);
         p29_add_aff_lean(acc, x2, y2);
-    }
-    comb_add_u1g(acc, u1, neg1, gcomb,
-                 [](jp29& a, const f29& x, const f29& y) { p29_add_aff_lean(a, x, y); });
+    };
+#pragma unroll 1
+    for (int i = kQDigits - 1; i >= 1; --i) digit_step(i);
+    digit_step(0);  // the last digit, peeled: the fix's state stays out of the loop
+    add_aff_fix(acc, inf, dbl1, [&](f29& x2, f29& y2) { entry(0, x2, y2); });
+    comb_add_u1g(acc, u1, neg1, gcomb, [](jp29& a, const f29& x, const f29& y) { p29_add_aff_lean(a, x, y); },
+                 [&](auto reload) { add_aff_fix(acc, inf, dbl1, reload); });
 
     bool exc;
-    const bool accept = verify_final(acc, load_be32(rr + 32ull * idx), exc);  // r reloaded
+    bool accept = verify_final(acc, load_be32(rr + 32ull * idx), exc);  // r reloaded
+    if (inf) {  // R = infinity: rejected (Go's Verify), not an exceptional tuple
+        accept = false;
+        exc = false;
+    }
     if (active) {
         if (exc && valid) {
             const uint32_t slot = atomicAdd(work, 1u);
@@ -1101,6 +1128,8 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
             }
     }
     const fe k2 = u2;
+    bool inf = false;  // acc is the point at infinity (add_aff_fix; the pair form only)
+    auto dblp = [odd](jp29& p) { p29_dbl_pair(p, p, odd); };
 #ifndef SBFT_PAIR_LADDER_DIGITS  // development: time the phases (tools/pair_probe.py --no-check)
 #define SBFT_PAIR_LADDER_DIGITS kQDigits
 #endif
@@ -1119,13 +1148,16 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
         }
         const int d2 = q_digit(k2, i);
         const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
-        f29 x2, y2;
+        auto entry = [&](f29& x, f29& y) {
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            x2.v[k] = qtab[(m2 * 18 + k) * kTuples + pr];
-            y2.v[k] = qtab[(m2 * 18 + 9 + k) * kTuples + pr];
-        }
-        if ((d2 < 0) != neg2) f29_neg(y2, y2);
+            for (int k = 0; k < 9; ++k) {
+                x.v[k] = qtab[(m2 * 18 + k) * kTuples + pr];
+                y.v[k] = qtab[(m2 * 18 + 9 + k) * kTuples + pr];
+            }
+            if ((d2 < 0) != neg2) f29_neg(y, y);
+        };
+        f29 x2, y2;
+        entry(x2, y2);
         if constexpr (kQuad) {
             // comb lanes: entry j + 1 while j + 1 <= K, then their accumulator is final
             const int ce = j + 1 <= kGK ? j + 1 : kGK;
@@ -1140,6 +1172,7 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
             if (!comb_role || j + 1 <= kGK) acc = tt;
         } else {
             p29_add_aff_pair(acc, x2, y2, odd);
+            if (i == 0) add_aff_fix(acc, inf, dblp, entry);  // the ladder's only exceptional spot
         }
     }
     if constexpr (kQuad) {
@@ -1155,12 +1188,17 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
     } else {
 #ifndef SBFT_PAIR_NO_COMB
         comb_add_u1g<true>(acc, u1, neg1, gcomb,
-                           [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); });
+                           [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); },
+                           [&](auto reload) { add_aff_fix(acc, inf, dblp, reload); });
 #endif
     }
 
     bool exc;
-    const bool accept = verify_final(acc, r, exc);
+    bool accept = verify_final(acc, r, exc);
+    if (inf) {  // R = infinity: rejected, not an exceptional tuple
+        accept = false;
+        exc = false;
+    }
     if (active && (threadIdx.x % LPT) == 0) {
         if (exc && valid) {
             if constexpr (FRAMED) {  // the fixup kernel's inputs
