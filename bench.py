@@ -166,6 +166,39 @@ def cpu_baseline(wl, sample: int, threads: int):
     return base, port, ok_cpu
 
 
+def pipelined(gv, wl, dev, steps: int, streams: int = 4):
+    """Sustained rate with several batches in flight: the same 1M device-resident tuples cut into
+    `streams` contiguous sub-batches, each verified over and over on a stream of its own with no
+    join between passes (a serving loop with that many launches in flight). A single launch ends
+    with a tail (the last resident round's waves finish at different times, then the fix-up and
+    s^-1 kernels run on an idle GPU); here other streams' work fills it. Reported beside
+    `value` (one launch per step, steps serialised on one stream), never as it."""
+    n = wl.n
+    sts = [torch.cuda.Stream(device=dev) for _ in range(streams)]
+    oks = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(streams)]
+
+    def run(k):
+        for i, st in enumerate(sts):
+            lo, hi = n * i // streams, n * (i + 1) // streams
+            for _ in range(k):
+                gv.verify_dev(wl.digest[lo:hi], wl.r[lo:hi], wl.s[lo:hi], wl.qx[lo:hi], wl.qy[lo:hi], oks[i][lo:hi], st)
+
+    run(2)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    want = (~wl.corrupted).to(torch.uint8)
+    mism = 0
+    for i in range(streams):
+        lo, hi = n * i // streams, n * (i + 1) // streams
+        mism += int((oks[i][lo:hi] != want[lo:hi]).sum())
+    return {"value": round(n * steps / dt, 1), "unit": "verifies/s", "streams": streams, "passes": steps,
+            "ms_per_pass": round(dt / steps * 1e3, 4), "mismatches": mism,
+            "path": f"sbft_gv_verify_p256_dev, {streams} streams x {n // streams} tuples, no join between passes"}
+
+
 def host_path(gv, wls, dev, reps: int = 3):
     """PCIe-inclusive rate of the host-buffer C ABI (sbft_gv_verify_p256: the call a cgo
     plugin makes with Go-heap tuples): H2D of 160 B/tuple + verify pipeline + D2H of verdicts,
@@ -313,6 +346,14 @@ def latency_configs(gv, calls: int):
     # the unmodified library: 66 goroutines (view.go:537-541), one VerifyConsenterSig each
     # (:834), released together per decision (tools/latency_harness quorum-gpu); stock = one
     # launch per call, coalesced = sbft_verifier_coalesce_consenter_sigs(66, 50 us)
+    # the patched processCommits (go/patches/internal_bft_commits.patch): 67 votes arrive per
+    # decision, the collector verifies them in one call once 66 can complete the quorum (a
+    # second call after a bad vote); latency = release -> 66 valid votes
+    hook = _harness("quorum-hook", 67, 66, calls)
+    if hook:
+        assert hook["wrong_verdicts"] == 0
+        out["commit_quorum_n100_hook"] = dict(hook, path="sbft_verifier_verify_consenter_sigs from the collector "
+                                                         "as votes arrive (processCommits batch hook)")
     stock = _harness("quorum-gpu", 66, calls, 0, 0)
     coal = _harness("quorum-gpu", 66, calls, 66, 50)
     if stock and coal:
@@ -441,10 +482,16 @@ def adversarial(gv, dev):
     cats = _json.load(open(os.path.join(ROOT, "tests", "golden", "p256_categories.json")))["categories"]
     sel = np.isin(raw[:, 161], [cats.index("r_infinity"), cats.index("shamir_exceptional")])
     base = raw[sel]
-    out = {"base_vectors": int(len(base)), "base_accepts": int(base[:, 160].sum())}
+    # crafted tuples (tests/golden/p256_crafted.bin, data): keys chosen so that the comb or the
+    # ladder's last addition meets acc == +-addend at a chosen step -- what a client controlling
+    # its own Q, r, s can aim at
+    crafted = np.fromfile(os.path.join(ROOT, "tests", "golden", "p256_crafted.bin"), dtype=np.uint8).reshape(-1, 162)
+    out = {"base_vectors": int(len(base)), "base_accepts": int(base[:, 160].sum()),
+           "crafted_vectors": int(len(crafted))}
     stream = torch.cuda.current_stream(dev)
-    for n in (10_000, 1_000_000):
-        t = np.resize(base, (n, 162))
+    for name, src, n in (("all_exceptional", base, 10_000), ("all_exceptional", base, 1_000_000),
+                         ("crafted_collisions", crafted, 10_000), ("crafted_collisions", crafted, 1_000_000)):
+        t = np.resize(src, (n, 162))
         f = [torch.from_numpy(np.ascontiguousarray(t[:, 32 * k:32 * k + 32])).to(dev) for k in range(5)]
         ok = torch.empty(n, dtype=torch.uint8, device=dev)
         run = lambda: gv.verify_dev(*f, ok, stream)
@@ -457,7 +504,7 @@ def adversarial(gv, dev):
         e1.record(stream)
         torch.cuda.synchronize(dev)
         ms = e0.elapsed_time(e1) / reps
-        out[f"all_exceptional_{n}"] = {"ms": round(ms, 3), "verifies_per_s": round(n / ms * 1e3, 1),
+        out[f"{name}_{n}"] = {"ms": round(ms, 3), "verifies_per_s": round(n / ms * 1e3, 1),
                                        "mismatches": int((ok.cpu().numpy() != t[:, 160]).sum())}
     return out
 
@@ -660,6 +707,8 @@ def main():
             rec["cpu_oracle"] = port
             rec["parity"]["oracle_sample_mismatches"] = int(
                 (ok[:len(ok_cpu)].cpu().numpy() != ok_cpu).sum())
+        if n_gpus == 1 and not rehearsal and S == 1:
+            rec["pipelined"] = pipelined(gv, wl, dev, args.steps)
         if world == 1 and not args.no_host_path:
             rec["host_buffer_path"] = host_path(gv, wls, dev)
         if n_gpus == 1 and not rehearsal and not args.no_sha:
@@ -683,6 +732,10 @@ def main():
                     lat["commit_quorum_n100_concurrent_singles"]["cpu_openssl"] = qc
                     lat["commit_quorum_n100_concurrent_singles"]["speedup_p50_vs_cpu"] = round(
                         qc["p50_ms"] / lat["commit_quorum_n100_concurrent_singles"]["coalesced"]["p50_ms"], 1)
+                if qc and "commit_quorum_n100_hook" in lat:
+                    h = lat["commit_quorum_n100_hook"]
+                    h["speedup_p50_vs_cpu"] = round(qc["p50_ms"] / h["p50_ms"], 1)
+                    h["speedup_p99_vs_cpu"] = round(qc["p99_ms"] / h["p99_ms"], 1)
             rec["latency"] = lat
         print(json.dumps(rec), flush=True)
     if world > 1:

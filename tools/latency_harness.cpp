@@ -12,6 +12,8 @@
 //       SBFT_V_EVERIFY with the reference's text, everyone else 0.
 //   quorum-batch VOTES DECISIONS
 //       the batch hook: one sbft_verifier_verify_consenter_sigs call per decision.
+//   quorum-hook VOTERS NEED DECISIONS
+//       the processCommits batch hook with arriving votes (go/patches/internal_bft_commits.patch).
 //   sign CALLS
 //       one signature at a time from one thread: sbft_signer_sign (RFC 6979, and with the
 //       pre-signature pool of 1,024) vs OpenSSL ECDSA_do_sign.
@@ -249,6 +251,131 @@ static int quorum_gpu(int callers, int decisions, int cmax, int cwait) {
     return wrong.load() ? 2 : 0;
 }
 
+// quorum-hook VOTERS NEED DECISIONS: the patched processCommits (go/patches/internal_bft_commits.patch):
+// VOTERS threads deliver one commit vote each per decision, released together (the votes of a
+// decision arriving from the network); the collector (this thread, the View goroutine) takes
+// them in arrival order and, as soon as the valid votes so far plus the pending ones can complete
+// the quorum, verifies the pending ones with ONE sbft_verifier_verify_consenter_sigs call; after a
+// bad vote the votes that arrived meanwhile form the next call. Latency = release -> NEED valid
+// votes collected. Every 10th decision carries one bad vote (voter 7), so VOTERS = NEED + 1 lets
+// the spare vote complete that quorum, as a 67th replica's vote would at n = 100.
+static int quorum_hook(int voters, int need, int decisions) {
+    sbft_gv_ctx* ctx = nullptr;
+    if (sbft_gv_init(nullptr, &ctx)) {
+        std::fprintf(stderr, "no GPU\n");
+        return 1;
+    }
+    sbft_verifier* v = sbft_verifier_new(ctx, 1);
+    std::vector<sbft_signer*> signers;
+    for (int i = 1; i <= voters + 1; ++i) {
+        uint8_t d[32], pub[65];
+        priv_of(1000 + i, d);
+        signers.push_back(sbft_signer_new(ctx, i, d));
+        sbft_signer_public_key(signers.back(), pub);
+        sbft_verifier_add_consenter(v, i, pub);
+    }
+    const int NB = 8;
+    std::vector<std::string> payloads(NB);
+    std::vector<sbft_proposal> props(NB);
+    std::vector<std::vector<std::vector<uint8_t>>> msgs(NB), vals(NB), bads(NB);
+    for (int b = 0; b < NB; ++b) {
+        payloads[b] = std::string(1300, 'a' + b);
+        props[b] = sbft_proposal{(const uint8_t*)payloads[b].data(), payloads[b].size(), (const uint8_t*)"h", 1,
+                                 (const uint8_t*)"m", 1, 1};
+        for (int i = 0; i < voters; ++i) {
+            std::vector<uint8_t> m(256), sig(64);
+            size_t ml = 0;
+            sbft_signer_sign_proposal(signers[i + 1], &props[b], nullptr, 0, m.data(), m.size(), &ml, sig.data());
+            m.resize(ml);
+            msgs[b].push_back(m);
+            vals[b].push_back(sig);
+            sig[40] ^= 1;
+            bads[b].push_back(sig);
+        }
+    }
+    std::unique_ptr<std::atomic<int>[]> order(new std::atomic<int>[voters]);
+    std::atomic<int> arrived{0}, gen{-1};
+    std::atomic<bool> stop{false};
+    std::vector<std::thread> th;
+    for (int i = 0; i < voters; ++i)
+        th.emplace_back([&, i] {
+            int seen = -1;
+            for (;;) {
+                int g;
+                bool slept = false;
+                while ((g = gen.load(std::memory_order_acquire)) == seen && !stop.load()) {
+                    futex(&gen, FUTEX_WAIT_PRIVATE, seen);
+                    slept = true;
+                }
+                if (slept) futex(&gen, FUTEX_WAKE_PRIVATE, 2);  // the release is a wake-up tree
+                if (stop.load()) return;
+                seen = g;
+                const int k = arrived.fetch_add(1, std::memory_order_acq_rel);
+                order[k].store(i + 1, std::memory_order_release);
+            }
+        });
+    std::vector<double> t;
+    int wrong = 0, launches = 0;
+    std::vector<sbft_signature> batch;
+    std::vector<int> who;
+    std::vector<int32_t> st;
+    for (int g = -5; g < decisions; ++g) {
+        const int b = (g + 80) % NB;
+        const bool bad_dec = g % 10 == 9;
+        for (int k = 0; k < voters; ++k) order[k].store(0, std::memory_order_relaxed);
+        arrived.store(0, std::memory_order_release);
+        const auto t0 = Clock::now();
+        gen.store(g + 5, std::memory_order_release);
+        futex(&gen, FUTEX_WAKE_PRIVATE, 2);
+        int valid = 0, consumed = 0;
+        while (valid < need) {
+            const int a = arrived.load(std::memory_order_acquire);
+            if (a == consumed || valid + (a - consumed) < need) {
+                if (a == voters) break;  // every vote is in and the quorum is still short
+                __builtin_ia32_pause();
+                continue;
+            }
+            batch.clear();
+            who.clear();
+            for (int k = consumed; k < a; ++k) {
+                int i;
+                while ((i = order[k].load(std::memory_order_acquire)) == 0) __builtin_ia32_pause();
+                --i;
+                const auto& val = (bad_dec && i == 7) ? bads[b][i] : vals[b][i];
+                batch.push_back(sbft_signature{(uint64_t)(i + 2), val.data(), 64, msgs[b][i].data(), msgs[b][i].size()});
+                who.push_back(i);
+            }
+            consumed = a;
+            st.assign(batch.size(), 0);
+            if (sbft_verifier_verify_consenter_sigs(v, batch.data(), batch.size(), &props[b], st.data())) wrong++;
+            ++launches;
+            for (size_t k = 0; k < batch.size(); ++k) {
+                const bool is_bad = bad_dec && who[k] == 7;
+                if (is_bad != (st[k] != 0)) wrong++;
+                if (!st[k] && valid < need) ++valid;
+            }
+        }
+        const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        if (valid != need) wrong++;
+        while (arrived.load(std::memory_order_acquire) < voters) __builtin_ia32_pause();
+        for (int k = 0; k < voters; ++k)
+            while (order[k].load(std::memory_order_acquire) == 0) __builtin_ia32_pause();
+        if (g >= 0) t.push_back(us);
+        else launches = 0;
+    }
+    stop.store(true);
+    gen.fetch_add(1);
+    futex(&gen, FUTEX_WAKE_PRIVATE, INT_MAX);
+    for (auto& x : th) x.join();
+    std::printf("{\"mode\": \"quorum-hook\", \"voters\": %d, \"need\": %d, \"decisions\": %d, \"p50_ms\": %.4f, "
+                "\"p99_ms\": %.4f, \"launches_per_decision\": %.2f, \"wrong_verdicts\": %d}\n",
+                voters, need, decisions, pct(t, 50) / 1e3, pct(t, 99) / 1e3, (double)launches / decisions, wrong);
+    for (auto* s : signers) sbft_signer_free(s);
+    sbft_verifier_free(v);
+    sbft_gv_destroy(ctx);
+    return wrong ? 2 : 0;
+}
+
 // SHA-256 through the low-level interface: OpenSSL 3's one-shot SHA256() fetches the digest
 // from the library context on every call, which serialises threads on its lock
 static void sha256_ll(const uint8_t* m, size_t n, uint8_t h[32]) {
@@ -405,13 +532,14 @@ static int proposal_cpu(int requests, int decisions, int threads) {
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|sign|quorum-cpu|proposal-cpu ...\n", argv[0]);
+        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-hook|sign|quorum-cpu|proposal-cpu ...\n", argv[0]);
         return 1;
     }
     const std::string mode = argv[1];
     auto arg = [&](int i, int def) { return argc > i ? std::atoi(argv[i]) : def; };
     if (mode == "quorum-gpu") return quorum_gpu(arg(2, 66), arg(3, 200), arg(4, 0), arg(5, 0));
     if (mode == "quorum-batch") return quorum_batch(arg(2, 67), arg(3, 200));
+    if (mode == "quorum-hook") return quorum_hook(arg(2, 67), arg(3, 66), arg(4, 200));
     if (mode == "sign") return sign_both(arg(2, 200));
     if (mode == "quorum-cpu") return quorum_cpu(arg(2, 66), arg(3, 200), arg(4, 66));
     if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
