@@ -878,12 +878,12 @@ SBFT_DEV fe f29_canon_plain(const f29& a) {
 SBFT_DEV bool verify_final(const jp29& acc, const fe& rv, bool& exc) {
     exc = f29_zero_mod_p(acc.z);
     const f29 r2 = f29_const(C29_R2);
-    f29 z2, lhs, rm;
+    f29 z2, lhs, rm, t;
     f29_sqr(z2, acc.z);
-    const fe xc = f29_canon_plain(acc.x);
     f29_mul(rm, f29_from_u256(rv), r2);
     f29_mul(lhs, rm, z2);
-    bool accept = fe_eq(f29_canon_plain(lhs), xc);
+    f29_sub(t, acc.x, lhs);  // X - r Z^2: |limb| < 2^30, |t| < 2^259
+    bool accept = f29_zero_mod_p_any(t);
     // R.x in [n, p): compare with r + n as well when r + n < p
     fe rn;
     u64 c = 0;
@@ -896,7 +896,8 @@ SBFT_DEV bool verify_final(const jp29& acc, const fe& rv, bool& exc) {
     if (c == 0 && fe_lt(rn, P256_P)) {
         f29_mul(rm, f29_from_u256(rn), r2);
         f29_mul(lhs, rm, z2);
-        accept = accept || fe_eq(f29_canon_plain(lhs), xc);
+        f29_sub(t, acc.x, lhs);
+        accept = accept || f29_zero_mod_p_any(t);
     }
     return accept;
 }

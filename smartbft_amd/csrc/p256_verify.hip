@@ -870,7 +870,11 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     auto dbl1 = [](jp29& p) { p29_dbl(p, p); };
     auto entry = [&](int i, f29& x2, f29& y2) __attribute__((always_inline)) {
         const int d2 = q_digit(k2, i);
+#ifdef SBFT_TABLE_PROBE  // measurement only (wrong verdicts): the ladder reads one fixed entry
+        const int m2 = 0;
+#else
         const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
+#endif
         x2 = tx[m2];
         y2 = ty[m2];
         if ((d2 < 0) != neg2) f29_neg(y2, y2);

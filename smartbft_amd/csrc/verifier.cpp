@@ -584,6 +584,10 @@ struct sbft_verifier {
     std::shared_ptr<CsBatch> cs_open;
     size_t cs_max = 0;  // 0 = off: every call is its own launch
     std::chrono::microseconds cs_wait{0};
+    // a batch that opens within 2 cs_wait of the previous one's close holds the stragglers of
+    // the same burst (callers the OS scheduled late): it waits only cs_follow for more
+    std::chrono::steady_clock::time_point cs_last_close{};
+    std::chrono::microseconds cs_follow{-1};  // < 0: cs_wait / 4 (SBFT_CS_FOLLOW_US overrides)
     std::atomic<uint64_t> cs_launches{0}, cs_calls{0};
 
     void digest_of(const sbft_proposal* p, char out[65]) {
@@ -1121,16 +1125,30 @@ static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const 
     bool leader = false;
     {
         std::unique_lock<std::mutex> g(v->cs_mu);
+        std::chrono::microseconds window = v->cs_wait;
         if (!v->cs_open) {
             v->cs_open = std::make_shared<Batch>();
-            v->cs_open->t_open = std::chrono::steady_clock::now();
+            const auto now = std::chrono::steady_clock::now();
+            v->cs_open->t_open = now;
             leader = true;
+            // stragglers of a burst whose first batch has just closed: the rest of the burst is
+            // already in that batch, so a full window would only delay these callers
+            if (now - v->cs_last_close < 2 * v->cs_wait) {
+                static const long follow_env = [] {
+                    const char* e = getenv("SBFT_CS_FOLLOW_US");
+                    return e ? std::atol(e) : -1L;
+                }();
+                window = follow_env >= 0 ? std::chrono::microseconds(follow_env)
+                         : v->cs_follow.count() >= 0 ? v->cs_follow
+                                                     : v->cs_wait / 4;
+            }
         }
         batch = v->cs_open;
         batch->entries.push_back(&me);
         if (batch->entries.size() >= v->cs_max) {
             batch->closed = true;
             v->cs_open.reset();
+            v->cs_last_close = std::chrono::steady_clock::now();
             batch->cv.notify_all();  // wakes the leader early
         }
         if (leader) {
@@ -1139,11 +1157,12 @@ static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const 
             // the thread's timer slack (50 us by default): 1 us for the wait, then restored.
             const int slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
             if (slack > 1000) (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
-            batch->cv.wait_until(g, batch->t_open + v->cs_wait, [&] { return batch->closed; });
+            batch->cv.wait_until(g, batch->t_open + window, [&] { return batch->closed; });
             if (slack > 1000) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)slack, 0, 0, 0);
             if (!batch->closed) {
                 batch->closed = true;
                 v->cs_open.reset();
+                v->cs_last_close = std::chrono::steady_clock::now();
             }
         }
     }
