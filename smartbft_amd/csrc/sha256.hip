@@ -169,10 +169,12 @@ __device__ __forceinline__ uint64_t sha_last_granule(uint64_t base, uint32_t ml,
 }
 
 // One step's DMA: slot s = m * 64 + lane fetches its P pieces from chunk[m] of its owner lane,
-// none past the slot's limit granule lim[m]. The owner packs its chunk address, moved two
-// granules down, with d' = 2 + (granules from the chunk to the limit, at least -1: a step
-// starts at most 8 bytes past its message's end) saturated to 15 into one 64-bit value; piece j
-// then reads granule min(j + 2, d') of that base: one and, one min and one add per piece.
+// none past the slot's limit granule lim[m]. A wave whose slots all have their step inside the
+// message (the common case: a lane's message ends in about one step in eight) takes the plain
+// path. Otherwise the owner packs its chunk address, moved two granules down, with
+// d' = 2 + (granules from the chunk to the limit, at least -1: a step starts at most 8 bytes
+// past its message's end) saturated to 15 into one 64-bit value, and piece j reads granule
+// min(j + 2, d') of that base: one and, one min and one add per piece.
 template <int C, int M>
 __device__ __forceinline__ void sha_lds_fetch(uint8_t* buf, const uint64_t (&chunk)[M], const uint64_t (&lim)[M],
                                               uint32_t lane) {
@@ -180,20 +182,19 @@ __device__ __forceinline__ void sha_lds_fetch(uint8_t* buf, const uint64_t (&chu
     typedef __attribute__((address_space(1))) void* gptr;
     constexpr int P = 4 * C + 1;
     static_assert(P + 1 <= 15, "the piece index + 2 must fit the 4-bit limit field");
-    uint32_t alo[M], ahi[M];
+    uint32_t dp[M];
+    bool clamp = false;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-        const uint64_t a = chunk[m] & ~(uint64_t)15;
-        const int64_t dg = ((int64_t)lim[m] - (int64_t)a) >> 4;
-        const uint32_t dp = dg >= 13 ? 15u : dg <= -2 ? 0u : (uint32_t)(dg + 2);
-        const uint64_t ab = (a - 32) | dp;
-        alo[m] = (uint32_t)ab;
-        ahi[m] = (uint32_t)(ab >> 32);
+        const int64_t dg = ((int64_t)lim[m] - (int64_t)(chunk[m] & ~(uint64_t)15)) >> 4;
+        dp[m] = dg >= 13 ? 15u : dg <= -2 ? 0u : (uint32_t)(dg + 2);
+        clamp = clamp || dp[m] < 15u;
     }
-#pragma unroll
-    for (int i = 0; i < M * P; ++i) {
+    // the slot's chunk address (packed form when clamping), from its owner lane
+    auto src_of = [&](int i, const uint32_t (&alo)[M], const uint32_t (&ahi)[M], uint32_t& piece) {
         const uint32_t g = (uint32_t)i * 64u + lane;
-        const uint32_t slot = g / (uint32_t)P, piece = g - slot * (uint32_t)P;
+        const uint32_t slot = g / (uint32_t)P;
+        piece = g - slot * (uint32_t)P;
         const uint32_t owner = slot & 63u, m = slot >> 6;
         uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -204,9 +205,40 @@ __device__ __forceinline__ void sha_lds_fetch(uint8_t* buf, const uint64_t (&chu
                 hi = h;
             }
         }
-        const uint32_t pe = min(piece + 2u, lo & 15u);
-        const uint64_t src = (((uint64_t)hi << 32) | (lo & ~15u)) + 16u * pe;
-        __builtin_amdgcn_global_load_lds((gptr)(uintptr_t)src, (lptr)(buf + i * 1024), 16, 0, 0);
+        return ((uint64_t)hi << 32) | lo;
+    };
+    uint32_t alo[M], ahi[M];
+#ifdef SBFT_SHA_NOCLAMP  // A/B measurement only: the unclamped DMA (needs the blob padding)
+    clamp = false;
+#endif
+    if (__any(clamp)) {  // wave-uniform
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const uint64_t ab = ((chunk[m] & ~(uint64_t)15) - 32) | dp[m];
+            alo[m] = (uint32_t)ab;
+            ahi[m] = (uint32_t)(ab >> 32);
+        }
+#pragma unroll
+        for (int i = 0; i < M * P; ++i) {
+            uint32_t piece;
+            const uint64_t a = src_of(i, alo, ahi, piece);
+            const uint32_t pe = min(piece + 2u, (uint32_t)a & 15u);
+            const uint64_t src = (a & ~(uint64_t)15) + 16u * pe;
+            __builtin_amdgcn_global_load_lds((gptr)(uintptr_t)src, (lptr)(buf + i * 1024), 16, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const uint64_t a = chunk[m] & ~(uint64_t)15;
+            alo[m] = (uint32_t)a;
+            ahi[m] = (uint32_t)(a >> 32);
+        }
+#pragma unroll
+        for (int i = 0; i < M * P; ++i) {
+            uint32_t piece;
+            const uint64_t src = src_of(i, alo, ahi, piece) + 16u * piece;
+            __builtin_amdgcn_global_load_lds((gptr)(uintptr_t)src, (lptr)(buf + i * 1024), 16, 0, 0);
+        }
     }
 }
 
