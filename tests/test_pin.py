@@ -2,7 +2,7 @@
 run, not only at fixture-generation time (tests/golden/gen_fixtures.py):
 
 - OpenSSL 3.0.2 libcrypto ECDSA_do_verify (oracle/openssl_xcheck, SEC1 key decoding) over
-  every record of tests/golden/p256_vectors.bin;
+  every record of tests/golden/p256_vectors.bin and tests/golden/p256_crafted.bin;
 - Node crypto.verify (oracle/node_xcheck.js, OpenSSL-backed, hashes the message itself) over
   every vector whose message is committed (tests/golden/p256_messages.bin).
 
@@ -42,6 +42,15 @@ def test_openssl_agrees_with_every_fixture_verdict(p256_vectors):
     assert len(bad) == 0, [(int(i), names[cat[i]]) for i in bad[:10]]
     # and the C oracle on the same records (the restatement the GPU tests compare against)
     assert np.array_equal(oracle.verify_batch(*split_fields(f)), got)
+
+
+def test_openssl_agrees_with_crafted_exceptional_fixture():
+    """tests/golden/p256_crafted.bin (keys crafted so the engine's lean additions meet
+    P + P or P + (-P) at a chosen step): OpenSSL's verdicts equal the fixture's."""
+    raw = np.fromfile(os.path.join(GOLDEN, "p256_crafted.bin"), dtype=np.uint8).reshape(-1, 162)
+    out = subprocess.run([_openssl_xcheck()], input=np.ascontiguousarray(raw[:, :160]).tobytes(),
+                         capture_output=True, check=True, timeout=300).stdout
+    assert np.array_equal(np.frombuffer(out, dtype=np.uint8), raw[:, 160])
 
 
 def test_openssl_agrees_with_oracle_on_random_corruptions():
