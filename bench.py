@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--latency-calls", type=int, default=200)
     ap.add_argument("--no-sha", action="store_true", help="skip the config-5 hashing measurement")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-buffer rate")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="skip the multi-stream sustained rate (its concurrent launches would mix into a profile)")
     ap.add_argument("--sha-messages", type=int, default=2_097_152,
                     help="config 5: 16M requests over 8 GPUs = 2M per GPU (~68 GB of payload in HBM)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -707,7 +709,7 @@ def main():
             rec["cpu_oracle"] = port
             rec["parity"]["oracle_sample_mismatches"] = int(
                 (ok[:len(ok_cpu)].cpu().numpy() != ok_cpu).sum())
-        if n_gpus == 1 and not rehearsal and S == 1:
+        if n_gpus == 1 and not rehearsal and S == 1 and not args.no_pipelined:
             rec["pipelined"] = pipelined(gv, wl, dev, args.steps)
         if world == 1 and not args.no_host_path:
             rec["host_buffer_path"] = host_path(gv, wls, dev)
