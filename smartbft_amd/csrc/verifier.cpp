@@ -416,6 +416,238 @@ bool parse_payload(const uint8_t* p, size_t len, std::vector<Req>& out) {
     return parse_payload(p, len, out, [](uint32_t) {});
 }
 
+// A process-wide pool of warm helper threads for the proposal parse. run(T, f) runs f(0) on the
+// caller and f(1..T-1) on helpers, and returns when all are done. A helper spins (yielding) for
+// ~2 ms after a job, so back-to-back proposals find it awake; then it sleeps. If another
+// caller holds the pool, run() returns false and the caller parses alone.
+struct ParsePool {
+    static constexpr int kMax = 4;  // threads per parse, the caller included
+    std::mutex busy;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<uint64_t> gen{0};
+    std::atomic<int> left{0};
+    std::function<void(int)> job;
+    std::thread th[kMax - 1];
+    bool started = false;
+
+    void worker(int t) {
+        uint64_t seen = 0;
+        for (;;) {
+            uint64_t g;
+            const auto t0 = std::chrono::steady_clock::now();
+            while ((g = gen.load(std::memory_order_acquire)) == seen &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2))
+                std::this_thread::yield();
+            if (g == seen) {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != seen; });
+                g = gen.load(std::memory_order_acquire);
+            }
+            seen = g;
+            if (t < (int)(g & 0xff)) {  // the job's thread count rides in the generation's low byte
+                job(t);
+                left.fetch_sub(1, std::memory_order_acq_rel);
+            }
+        }
+    }
+    bool run(int T, const std::function<void(int)>& f) {
+        if (T <= 1) {
+            f(0);
+            return true;
+        }
+        std::unique_lock<std::mutex> b(busy, std::try_to_lock);
+        if (!b.owns_lock()) return false;
+        T = std::min(T, kMax);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!started) {
+                for (int t = 1; t < kMax; ++t) {
+                    th[t - 1] = std::thread([this, t] { worker(t); });
+                    th[t - 1].detach();  // process-lifetime helpers
+                }
+                started = true;
+            }
+            job = f;
+            left.store(T - 1, std::memory_order_release);
+            gen.store(((gen.load() >> 8) + 1) << 8 | (uint64_t)T, std::memory_order_release);
+        }
+        cv.notify_all();
+        f(0);
+        while (left.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+        return true;
+    }
+};
+ParsePool& parse_pool() {
+    static ParsePool* pool = new ParsePool();  // never destroyed: its threads live with the process
+    return *pool;
+}
+
+// The first position q >= from (q < to) that can start a request of a payload p[0, len): a u32
+// length l at q with q + 4 + l <= len and a request that parses at q + 4. A candidate only: the
+// walk that reaches it decides whether it is a real boundary.
+// The search gives up after kCandidateWindow bytes: the split only pays for many small requests,
+// and a bounded scan keeps a payload crafted full of false "SBR1" headers cheap.
+constexpr size_t kCandidateWindow = 4096;
+size_t payload_candidate(const uint8_t* p, size_t len, size_t from, size_t to) {
+    to = std::min(to, from + kCandidateWindow);
+    for (size_t q = from; q + 8 <= len && q < to; ++q) {
+        if (p[q + 4] != 'S' || std::memcmp(p + q + 4, REQ_MAGIC, 4) != 0) continue;
+        const uint32_t l = (uint32_t)p[q] | (uint32_t)p[q + 1] << 8 | (uint32_t)p[q + 2] << 16 | (uint32_t)p[q + 3] << 24;
+        Req tmp;
+        if (l <= len - q - 4 && parse_request(p + q + 4, l, q + 4, tmp)) return q;
+    }
+    return SIZE_MAX;
+}
+
+// parse_payload over T threads, in two phases. sized(n) runs on the caller once the request count
+// is known (before any range call).
+//   walk : thread t follows the chain of length prefixes from its start (the payload's first
+//          request for t = 0; for t > 0 the first candidate boundary at or after t/T of the
+//          payload) up to the next thread's candidate, recording request positions. This chain of
+//          dependent loads is most of a sequential parse (a cache miss per request).
+//   join : thread t's walk is the payload's own chain iff thread t-1's ended exactly on its
+//          start. A false candidate (bytes that look like a request inside some payload) breaks
+//          the joint: the caller walks on from thread t-1's end alone. The walk must end at len
+//          with exactly `count` requests, as the sequential parse requires.
+//   parse: each thread parses its requests into their final slots, then calls range(b, e) on
+//          them (the caller's per-request work: offsets, key checks, registry lookups).
+// Returns false for a malformed payload (the same payloads parse_payload rejects). Falls back to
+// the sequential parse for small payloads or when the pool is busy.
+template <class Sized, class Range>
+bool parse_payload_par(const uint8_t* p, size_t len, std::vector<Req>& out, int T, Sized&& sized, Range&& range) {
+    if (len < 4) return false;
+    const uint32_t count = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+    if (count > len / 4) return false;
+    if (T > 1 && (count < 2048 || len < ((size_t)256 << 10) || len > 0xffffffffu)) T = 1;
+    T = std::min(T, ParsePool::kMax);
+    if (T <= 1) {
+        if (!parse_payload(p, len, out)) return false;
+        sized(out.size());
+        range((uint32_t)0, (uint32_t)out.size());
+        return true;
+    }
+    struct Part {
+        size_t start = SIZE_MAX, limit = 0, end = 0;
+        std::vector<uint32_t> pos;
+        bool bad = false;
+        uint32_t base = 0;
+        bool used = false;
+    };
+    thread_local std::vector<Part> parts_tl;
+    std::vector<Part>& parts = parts_tl;
+    parts.resize(T);
+    for (auto& x : parts) {
+        x.pos.clear();
+        x.start = SIZE_MAX;
+        x.end = 0;
+        x.bad = false;
+        x.used = false;
+    }
+    std::vector<size_t> cut(T + 1);
+    for (int t = 0; t <= T; ++t) cut[t] = t == 0 ? 4 : t == T ? len : 4 + (len - 4) * (size_t)t / (size_t)T;
+    std::atomic<bool> bad_parse{false};
+    auto walk = [&](int t) {
+        Part& x = parts[t];
+        x.start = t == 0 ? 4 : payload_candidate(p, len, cut[t], cut[t + 1]);
+        size_t nxt = len;  // the next thread's start (or the payload's end)
+        for (int u = t + 1; u < T; ++u) {
+            const size_t c = payload_candidate(p, len, cut[u], cut[u + 1]);
+            if (c != SIZE_MAX) {
+                nxt = c;
+                break;
+            }
+        }
+        x.limit = nxt;
+        if (x.start == SIZE_MAX) return;
+        x.pos.reserve(count / T + 64);
+        size_t pos = x.start;
+        while (pos < nxt) {
+            if (len - pos < 4) {
+                x.bad = true;
+                break;
+            }
+            __builtin_prefetch(p + pos + 2048);
+            const uint32_t l = (uint32_t)p[pos] | (uint32_t)p[pos + 1] << 8 | (uint32_t)p[pos + 2] << 16 |
+                               (uint32_t)p[pos + 3] << 24;
+            if (l > len - pos - 4) {
+                x.bad = true;
+                break;
+            }
+            x.pos.push_back((uint32_t)pos);
+            pos += 4 + (size_t)l;
+        }
+        x.end = pos;
+    };
+    auto parse = [&](int t) {
+        Part& x = parts[t];
+        if (!x.used) return;
+        for (size_t k = 0; k < x.pos.size(); ++k) {
+            const size_t q = x.pos[k];
+            const uint32_t l = (uint32_t)p[q] | (uint32_t)p[q + 1] << 8 | (uint32_t)p[q + 2] << 16 |
+                               (uint32_t)p[q + 3] << 24;
+            if (!parse_request(p + q + 4, l, q + 4, out[x.base + k])) {
+                bad_parse.store(true, std::memory_order_relaxed);
+                return;
+            }
+        }
+        range(x.base, x.base + (uint32_t)x.pos.size());
+    };
+    auto& pool = parse_pool();
+    if (!pool.run(T, walk)) {
+        if (!parse_payload(p, len, out)) return false;
+        sized(out.size());
+        range((uint32_t)0, (uint32_t)out.size());
+        return true;
+    }
+    // join: accept thread t's walk while the chain reaches its start exactly
+    size_t at = parts[0].end;
+    bool chain_bad = parts[0].bad;
+    parts[0].used = true;
+    int last = 0;
+    for (int t = 1; t < T && !chain_bad; ++t) {
+        if (parts[t].start == SIZE_MAX) continue;  // no candidate in this range: t-1 walked over it
+        if (parts[t].start != at) break;          // a false candidate: walk on alone from `at`
+        parts[t].used = true;
+        chain_bad = parts[t].bad;
+        at = parts[t].end;
+        last = t;
+    }
+    if (chain_bad) return false;
+    if (at != len) {  // the rest of the chain, on this thread
+        Part& x = parts[last];
+        size_t pos = at;
+        while (pos < len) {
+            if (len - pos < 4) return false;
+            const uint32_t l = (uint32_t)p[pos] | (uint32_t)p[pos + 1] << 8 | (uint32_t)p[pos + 2] << 16 |
+                               (uint32_t)p[pos + 3] << 24;
+            if (l > len - pos - 4) return false;
+            x.pos.push_back((uint32_t)pos);
+            pos += 4 + (size_t)l;
+        }
+        for (int t = last + 1; t < T; ++t) parts[t].used = false;
+    }
+    uint32_t total = 0;
+    for (auto& x : parts)
+        if (x.used) {
+            x.base = total;
+            total += (uint32_t)x.pos.size();
+        }
+    static const bool trace = getenv("SBFT_PARSE_TRACE") != nullptr;  // diagnostics
+    if (trace) {
+        fprintf(stderr, "parse T=%d", T);
+        for (auto& x : parts) fprintf(stderr, " [%s %zu]", x.used ? "used" : "dropped", x.pos.size());
+        fprintf(stderr, " total=%u count=%u\n", total, count);
+    }
+    if (total != count) return false;
+    out.resize(count);
+    sized((size_t)count);
+    if (!pool.run(T, parse)) {  // another caller took the pool meanwhile: parse alone
+        for (int t = 0; t < T; ++t) parse(t);
+    }
+    return !bad_parse.load();
+}
+
 struct Msg {
     const uint8_t* digest = nullptr;
     size_t digest_len = 0;
@@ -986,7 +1218,12 @@ int sbft_verifier_requests_from_proposal(sbft_verifier* v, const sbft_proposal* 
     if (!v || !p || !count) return SBFT_GV_EINVAL;
     std::vector<Req>& reqs = proposal_scratch().reqs;
     *count = 0;
-    if (!parse_payload(p->payload, p->payload_len, reqs)) return SBFT_V_EFORMAT;
+    static const int parse_threads = [] {
+        const char* e = getenv("SBFT_PARSE_THREADS");
+        return e ? std::max(1, std::atoi(e)) : 3;
+    }();
+    if (!parse_payload_par(p->payload, p->payload_len, reqs, parse_threads, [](size_t) {}, [](uint32_t, uint32_t) {}))
+        return SBFT_V_EFORMAT;
     char* w = infos;
     char* end = infos + infos_cap;
     for (auto& r : reqs)
@@ -1003,29 +1240,52 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     ProposalScratch& scr = proposal_scratch();  // this thread's, also when prepare runs elsewhere
     std::vector<Req>& reqs = scr.reqs;
     std::vector<uint8_t>& ok = scr.ok;
-    // parse + per-request format checks -> the body offsets / lengths of the framed requests
-    auto prepare_cb = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len, auto&& on_req) -> int {
-        if (!parse_payload(p->payload, p->payload_len, reqs, on_req)) {
+    // parse + per-request format checks -> the body offsets / lengths of the framed requests. The
+    // parse runs over several threads for a large proposal (parse_payload_par); per_req(b, e)
+    // is extra per-request work on the requests [b, e) (the registry lookups), run on the thread
+    // that parsed them.
+    static const int parse_threads = [] {
+        const char* e = getenv("SBFT_PARSE_THREADS");
+        return e ? std::max(1, std::atoi(e)) : 3;
+    }();
+    auto prepare_cb = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len, auto&& sized,
+                          auto&& per_req) -> int {
+        std::atomic<uint32_t> first_bad_key{UINT32_MAX};
+        const bool ok_parse = parse_payload_par(
+            p->payload, p->payload_len, reqs, parse_threads,
+            [&](size_t n) {
+                off.resize(n);
+                len.resize(n);
+                sized(n);
+            },
+            [&](uint32_t b, uint32_t e) {
+                for (uint32_t i = b; i < e; ++i) {
+                    if (reqs[i].pub[0] != 0x04) {  // the first one in order is reported below
+                        uint32_t cur = first_bad_key.load(std::memory_order_relaxed);
+                        while (i < cur && !first_bad_key.compare_exchange_weak(cur, i)) {
+                        }
+                        break;
+                    }
+                    off[i] = reqs[i].body_off;
+                    len[i] = (uint32_t)reqs[i].body_len;
+                }
+                per_req(b, e);
+            });
+        if (!ok_parse) {
             put_err(err, err_cap, "malformed proposal payload");
             return SBFT_V_EFORMAT;
         }
-        const size_t n = reqs.size();
-        off.resize(n);
-        len.resize(n);
-        for (size_t i = 0; i < n; ++i) {
-            if (reqs[i].pub[0] != 0x04) {
-                if (bad_index) *bad_index = (int64_t)i;
-                put_err(err, err_cap, "request %zu (%.*s:%.*s): public key is not SEC1 uncompressed", i,
-                        reqs[i].client_id.n, reqs[i].client_id.p, reqs[i].req_id.n, reqs[i].req_id.p);
-                return SBFT_V_EFORMAT;
-            }
-            off[i] = reqs[i].body_off;
-            len[i] = (uint32_t)reqs[i].body_len;
+        const uint32_t i = first_bad_key.load();
+        if (i != UINT32_MAX) {
+            if (bad_index) *bad_index = (int64_t)i;
+            put_err(err, err_cap, "request %u (%.*s:%.*s): public key is not SEC1 uncompressed", i,
+                    reqs[i].client_id.n, reqs[i].client_id.p, reqs[i].req_id.n, reqs[i].req_id.p);
+            return SBFT_V_EFORMAT;
         }
         return 0;
     };
     auto prepare = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
-        return prepare_cb(off, len, [](uint32_t) {});
+        return prepare_cb(off, len, [](size_t) {}, [](uint32_t, uint32_t) {});
     };
     bool registered;
     {
@@ -1047,23 +1307,25 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     std::vector<uint32_t>& kid = scr.kid;
     kid.clear();
     auto prepare_keyed = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
-        // the key lookups ride along the parse: request i's map slot is prefetched as soon as
-        // it is parsed, and looked up kAhead requests later
+        // each parse thread looks its own requests up, each map slot prefetched kAhead lookups
+        // before it is read
         constexpr uint32_t kAhead = 8;
-        bool all = true;
-        std::shared_lock<std::shared_mutex> g(v->clients_mu);
-        auto look = [&](uint32_t i) {
-            if (all && !(kid[i] = v->clients.find(reqs[i].pub + 1))) all = false;
-        };
-        const int prc = prepare_cb(off, len, [&](uint32_t i) {
-            if (i == 0) kid.resize(reqs.size());
-            v->clients.prefetch(reqs[i].pub + 1);
-            if (i >= kAhead) look(i - kAhead);
-        });
+        std::atomic<bool> all{true};
+        std::shared_lock<std::shared_mutex> g(v->clients_mu);  // covers the helpers' lookups too
+        const int prc = prepare_cb(
+            off, len, [&](size_t n) { kid.resize(n); },
+            [&](uint32_t b, uint32_t e) {
+                for (uint32_t i = b; i < e && i < b + kAhead; ++i) v->clients.prefetch(reqs[i].pub + 1);
+                for (uint32_t i = b; i < e; ++i) {
+                    if (i + kAhead < e) v->clients.prefetch(reqs[i + kAhead].pub + 1);
+                    if (!(kid[i] = v->clients.find(reqs[i].pub + 1))) {
+                        all.store(false, std::memory_order_relaxed);
+                        break;
+                    }
+                }
+            });
         if (prc) return prc;
-        const uint32_t n = (uint32_t)reqs.size();
-        for (uint32_t i = n > kAhead ? n - kAhead : 0; i < n; ++i) look(i);
-        if (!all) kid.clear();
+        if (!all.load()) kid.clear();
         return 0;
     };
     int info_rc = 0;

@@ -1,0 +1,118 @@
+"""The proposal parse over several threads (verifier.cpp parse_payload_par): large proposals are
+walked from several candidate request boundaries at once and joined where the chains meet. It
+must accept and reject exactly the payloads the sequential parse does, report the same first
+bad request, and survive payloads crafted to defeat the speculation (request-looking bytes
+inside payloads). CPU only: RequestsFromProposal and a parse-only VerifyProposal (no engine)."""
+import numpy as np
+import pytest
+
+from smartbft_amd import plugin
+
+
+def _req(i: int, rng, pl: bytes | None = None, key0: int = 0x04) -> bytes:
+    cid, rid = f"client{i}".encode(), f"tx{i}".encode()
+    if pl is None:
+        pl = rng.bytes(int(rng.integers(64, 257)))
+    key = bytes([key0]) + rng.bytes(64)
+    body = (b"SBR1" + len(cid).to_bytes(2, "little") + cid + len(rid).to_bytes(2, "little") + rid +
+            len(pl).to_bytes(4, "little") + pl + key)
+    return body + rng.bytes(64)
+
+
+def _want(n):
+    return [(f"client{i}", f"tx{i}") for i in range(n)]
+
+
+def _ids(infos):
+    return [(x.ClientID, x.ID) for x in infos]
+
+
+@pytest.fixture(scope="module")
+def reqs():
+    rng = np.random.default_rng(11)
+    return [_req(i, rng) for i in range(6000)]  # ~1.8 MB: the parallel path (>= 2048 requests, >= 256 KB)
+
+
+def test_large_proposal_parses_in_order(reqs):
+    v = plugin.Verifier(None)
+    p = plugin.Proposal(plugin.encode_payload(reqs), b"h", b"m", 0)
+    assert _ids(v.RequestsFromProposal(p)) == _want(len(reqs))
+    # no engine: the parse and the format checks run, then the call reports the missing GPU
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(p)
+    assert ei.value.code != plugin.EFORMAT
+    v.close()
+
+
+@pytest.mark.parametrize("where", [0.0, 0.33, 0.34, 0.5, 0.66, 0.67, 0.999])
+def test_false_boundaries_inside_payloads(where):
+    """Some requests carry, inside their payload, bytes that form a complete length-prefixed
+    request (a speculative walker starting there follows a false chain): the join must reject it
+    and the list must still be exact."""
+    rng = np.random.default_rng(int(where * 1000) + 5)
+    out = []
+    n = 5000
+    fake_at = int(where * n)
+    for i in range(n):
+        if fake_at - 40 <= i <= fake_at + 40:
+            inner = _req(10_000 + i, rng)
+            pl = rng.bytes(int(rng.integers(0, 40))) + len(inner).to_bytes(4, "little") + inner + rng.bytes(8)
+            out.append(_req(i, rng, pl=pl))
+        else:
+            out.append(_req(i, rng))
+    v = plugin.Verifier(None)
+    p = plugin.Proposal(plugin.encode_payload(out), b"h", b"m", 0)
+    assert _ids(v.RequestsFromProposal(p)) == _want(n)
+    v.close()
+
+
+def test_every_payload_full_of_fake_headers(reqs):
+    """Every request's payload is request-looking bytes: the candidate scan is bounded and the
+    list still exact."""
+    rng = np.random.default_rng(3)
+    fake = _req(99, rng)
+    out = [_req(i, rng, pl=(len(fake).to_bytes(4, "little") + fake)[: int(rng.integers(64, 257))]) for i in range(4000)]
+    v = plugin.Verifier(None)
+    assert _ids(v.RequestsFromProposal(plugin.Proposal(plugin.encode_payload(out), b"h", b"m", 0))) == _want(4000)
+    v.close()
+
+
+def _malformed(v, payload):
+    p = plugin.Proposal(payload, b"h", b"m", 0)
+    assert v.RequestsFromProposal(p) == []
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(p)
+    assert ei.value.code == plugin.EFORMAT and "malformed proposal payload" in str(ei.value)
+
+
+def test_malformed_large_payloads(reqs):
+    v = plugin.Verifier(None)
+    good = plugin.encode_payload(reqs)
+    n = len(reqs)
+    _malformed(v, (n + 1).to_bytes(4, "little") + good[4:])          # count says one more
+    _malformed(v, (n - 1).to_bytes(4, "little") + good[4:])          # count says one fewer
+    _malformed(v, good[:-1])                                          # truncated
+    _malformed(v, good + b"\0")                                       # trailing byte
+    for frac in (0.1, 0.5, 0.9):                                      # a bad length prefix late on
+        k = int(frac * n)
+        off = 4 + sum(4 + len(r) for r in reqs[:k])
+        bad = bytearray(good)
+        bad[off:off + 4] = (len(reqs[k]) + 3).to_bytes(4, "little")
+        _malformed(v, bytes(bad))
+        bad = bytearray(good)
+        bad[off + 4] = ord("X")                                       # a broken magic
+        _malformed(v, bytes(bad))
+    v.close()
+
+
+@pytest.mark.parametrize("bad", [[4999], [1200, 4700], [3001]])
+def test_first_bad_key_reported_in_order(bad):
+    rng = np.random.default_rng(17)
+    out = [_req(i, rng, key0=0x02 if i in bad else 0x04) for i in range(5000)]
+    v = plugin.Verifier(None)
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(plugin.Proposal(plugin.encode_payload(out), b"h", b"m", 0))
+    i = min(bad)
+    assert ei.value.code == plugin.EFORMAT and ei.value.index == i
+    assert f"request {i} (client{i}:tx{i}): public key is not SEC1 uncompressed" in str(ei.value)
+    v.close()
