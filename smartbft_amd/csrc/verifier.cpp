@@ -418,7 +418,7 @@ bool parse_payload(const uint8_t* p, size_t len, std::vector<Req>& out) {
 
 // A process-wide pool of warm helper threads for the proposal parse. run(T, f) runs f(0) on the
 // caller and f(1..T-1) on helpers, and returns when all are done. A helper spins (yielding) for
-// ~2 ms after a job, so back-to-back proposals find it awake; then it sleeps. If another
+// ~0.5 ms after a job, so back-to-back proposals find it awake; then it sleeps. If another
 // caller holds the pool, run() returns false and the caller parses alone.
 struct ParsePool {
     static constexpr int kMax = 4;  // threads per parse, the caller included
@@ -437,7 +437,7 @@ struct ParsePool {
             uint64_t g;
             const auto t0 = std::chrono::steady_clock::now();
             while ((g = gen.load(std::memory_order_acquire)) == seen &&
-                   std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2))
+                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(500))
                 std::this_thread::yield();
             if (g == seen) {
                 std::unique_lock<std::mutex> lk(mu);
@@ -1213,15 +1213,22 @@ void sbft_verifier_set_verification_sequence(sbft_verifier* v, uint64_t seq) {
     if (v) v->vseq = seq;
 }
 
+// Threads per proposal parse (parse_payload_par), SBFT_PARSE_THREADS overriding the default.
+// VerifyProposal parses on one: there the payload's DMA staging runs on another core at the same
+// time, and on the GPU box (16-core share of a 256-thread host) three parse threads took the
+// parse from ~92 to ~155 us and the call's p50 from 0.92 to 0.98 ms
+// (profiles/r03h_parse_threads_ab.txt).
+static int parse_threads_for(int dflt) {
+    const char* e = getenv("SBFT_PARSE_THREADS");
+    return e ? std::max(1, std::atoi(e)) : dflt;
+}
+
 int sbft_verifier_requests_from_proposal(sbft_verifier* v, const sbft_proposal* p, char* infos,
                                          size_t infos_cap, size_t* count) {
     if (!v || !p || !count) return SBFT_GV_EINVAL;
     std::vector<Req>& reqs = proposal_scratch().reqs;
     *count = 0;
-    static const int parse_threads = [] {
-        const char* e = getenv("SBFT_PARSE_THREADS");
-        return e ? std::max(1, std::atoi(e)) : 3;
-    }();
+    static const int parse_threads = parse_threads_for(3);
     if (!parse_payload_par(p->payload, p->payload_len, reqs, parse_threads, [](size_t) {}, [](uint32_t, uint32_t) {}))
         return SBFT_V_EFORMAT;
     char* w = infos;
@@ -1244,10 +1251,7 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     // parse runs over several threads for a large proposal (parse_payload_par); per_req(b, e)
     // is extra per-request work on the requests [b, e) (the registry lookups), run on the thread
     // that parsed them.
-    static const int parse_threads = [] {
-        const char* e = getenv("SBFT_PARSE_THREADS");
-        return e ? std::max(1, std::atoi(e)) : 3;
-    }();
+    static const int parse_threads = parse_threads_for(1);
     auto prepare_cb = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len, auto&& sized,
                           auto&& per_req) -> int {
         std::atomic<uint32_t> first_bad_key{UINT32_MAX};

@@ -2,7 +2,14 @@
 walked from several candidate request boundaries at once and joined where the chains meet. It
 must accept and reject exactly the payloads the sequential parse does, report the same first
 bad request, and survive payloads crafted to defeat the speculation (request-looking bytes
-inside payloads). CPU only: RequestsFromProposal and a parse-only VerifyProposal (no engine)."""
+inside payloads). CPU only: RequestsFromProposal and a parse-only VerifyProposal (no engine).
+RequestsFromProposal parses on 3 threads by default, VerifyProposal on 1 (verifier.cpp
+parse_threads_for); SBFT_PARSE_THREADS sets both, once per process, so the VerifyProposal cases
+run again in a child process with it set."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -116,3 +123,16 @@ def test_first_bad_key_reported_in_order(bad):
     assert ei.value.code == plugin.EFORMAT and ei.value.index == i
     assert f"request {i} (client{i}:tx{i}): public key is not SEC1 uncompressed" in str(ei.value)
     v.close()
+
+
+def test_verify_proposal_parallel_prepare_in_child():
+    """The VerifyProposal cases above with SBFT_PARSE_THREADS=3 (the parallel prepare: per-range
+    format checks, first bad key by atomic minimum)."""
+    env = dict(os.environ, SBFT_PARSE_THREADS="3")
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import pytest; "
+            "sys.exit(pytest.main(['-q', '-p', 'no:cacheprovider', %r, '-k', "
+            "'first_bad_key or malformed or in_order']))" % (here, os.path.join(here, "test_parse_parallel.py")))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600,
+                       cwd=os.path.dirname(here))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
