@@ -1438,8 +1438,10 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
                                                  (const uint32_t*)(vd + fo + fl), (const void* const*)sl->d_keytab,
                                                  nkeys, sl->dbuf, (uint32_t)n, sl->stream))
             return SBFT_GV_ELAUNCH;
-        HIPCHK(hipMemcpyAsync(ok.data(), sl->dbuf, n, hipMemcpyDeviceToHost, sl->stream));
+        // `during` before the verdict copy: a copy into pageable memory returns only once the
+        // kernel has finished, which would serialise the caller's host work behind it
         if (during) during();
+        HIPCHK(hipMemcpyAsync(ok.data(), sl->dbuf, n, hipMemcpyDeviceToHost, sl->stream));
         HIPCHK(hipStreamSynchronize(sl->stream));
         drain.armed = false;
         return SBFT_GV_OK;
@@ -1482,8 +1484,10 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
                                        (uint32_t*)d_work, gcomb, sl->stream, nullptr, nullptr, lanes, 1)) {
         return SBFT_GV_ELAUNCH;
     }
+    // the caller's host work that does not need the verdicts, under the launch: before the
+    // verdict copy, which (into pageable memory) returns only once the kernel has finished
+    if (during) during();
     HIPCHK(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, sl->stream));
-    if (during) during();  // the caller's host work that does not need the verdicts, under the launch
     HIPCHK(hipStreamSynchronize(sl->stream));
     drain.armed = false;
     return SBFT_GV_OK;

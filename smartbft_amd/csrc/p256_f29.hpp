@@ -218,6 +218,46 @@ SBFT_DEV void f29_sqr2(f29& r0, const f29& a0, f29& r1, const f29& a1) {
     f29_mulv<2, 3u>(r, a, a);
 }
 
+// (a b - c d) 2^-261 mod p with ONE Montgomery reduction: each column sums both products (a's
+// terms and c's against -d, in two accumulators so no two dependent mads issue back to back)
+// before its reduction step. It replaces two products and a subtraction (the additions' Y3 =
+// r (V - X3) - Y1 H^3): 36 reduction mads and 17 (mask, shift) pairs fewer.
+// Contract (f29_mul's, with both products in the column): 9 (A B + C D) + 2^60 < 2^63 for the
+// limb bounds (A B + C D <= 2^59.6; the uses have 2^29.2 x 2^29.2 + 2^29.2 x 2^29 = 2^59.3), and
+// |a b - c d| < 2^518 so that the output is normal (N).
+SBFT_DEV void f29_mul_sub(f29& r, const f29& a, const f29& b, const f29& c, const f29& d) {
+    const f29_red K = f29_red_consts();
+    u32 nd[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) nd[i] = 0u - d.v[i];
+    u32 m[9];
+    i64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+        i64 acc1 = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const int j = k - i;
+            if (j < 0 || j > 8) continue;
+            acc = smad(a.v[i], b.v[j], acc);
+            acc1 = smad(c.v[i], nd[j], acc1);
+        }
+        acc += acc1;
+        if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], K.c9, acc);
+        if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], K.c18, acc);
+        if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], K.c7, acc);
+        if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], K.c8, acc);
+        if (k < 9) m[k] = lo29(acc);
+        else r.v[k - 9] = lo29(acc);
+        acc = sar29(acc);
+    }
+    r.v[8] = (u32)acc;
+}
+
+#ifndef SBFT_MULSUB
+#define SBFT_MULSUB 1  // the additions' Y3 through f29_mul_sub (0: two products + subtraction)
+#endif
+
 SBFT_DEV void f29_add(f29& r, const f29& a, const f29& b) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + b.v[i];
@@ -396,9 +436,13 @@ SBFT_DEV void p29_add_jac_lean_s(jp29& acc, const jp29& b) {
     for (int i = 0; i < 9; ++i) t.v[i] = t.v[i] - hhh.v[i] - (u1.v[i] << 1);  // (-3 2^29, 2^29)
     f29_normalize(acc.x, t);
     f29_sub(t, u1, acc.x);           // (-2^29.2, 2^29 + 2^26)
-    f29_mul(t, rr, t);
-    f29_mul(s1, s1, hhh);
-    f29_sub(acc.y, t, s1);           // N+-
+    if (SBFT_MULSUB) {
+        f29_mul_sub(acc.y, rr, t, s1, hhh);  // rr t - S1 H^3 (2^29 x 2^29.2 + 2^29 x 2^29): N
+    } else {
+        f29_mul(t, rr, t);
+        f29_mul(s1, s1, hhh);
+        f29_sub(acc.y, t, s1);       // N+-
+    }
 }
 
 // acc += (x2, y2) affine (N; y2 may be N+-), same structure: 8M + 3S.
@@ -418,10 +462,14 @@ SBFT_DEV void p29_add_aff_lean_s(jp29& acc, const f29& x2, const f29& y2) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) t.v[i] = t.v[i] - hhh.v[i] - (u2.v[i] << 1);
     f29_normalize(acc.x, t);
-    f29_sub(t, u2, acc.x);
-    f29_mul(t, rr, t);
-    f29_mul(s2, acc.y, hhh);
-    f29_sub(acc.y, t, s2);           // N+-
+    f29_sub(t, u2, acc.x);           // (-2^29.2, 2^29 + 2^26)
+    if (SBFT_MULSUB) {
+        f29_mul_sub(acc.y, rr, t, acc.y, hhh);  // rr t - Y1 H^3 (2^29.2 x 2^29.2 + 2^29.2 x 2^29): N
+    } else {
+        f29_mul(t, rr, t);
+        f29_mul(s2, acc.y, hhh);
+        f29_sub(acc.y, t, s2);       // N+-
+    }
 }
 
 SBFT_DEV void p29_dbl_i(jp29& r, const jp29& p) {
@@ -465,8 +513,12 @@ SBFT_DEV void p29_add_jac_lean_i(jp29& acc, const jp29& b) {
     for (int i = 0; i < 9; ++i) t1.v[i] = r2.v[i] - hhh.v[i] - (u1.v[i] << 1);  // (-3 2^29, 2^29)
     f29_normalize(acc.x, t1);
     f29_sub(t1, u1, acc.x);          // (-2^29.2, 2^29 + 2^26)
-    f29_mul2(t1, rr, t1, s1, s1, hhh);
-    f29_sub(acc.y, t1, s1);          // N+-
+    if (SBFT_MULSUB) {
+        f29_mul_sub(acc.y, rr, t1, s1, hhh);  // rr t - S1 H^3: N
+    } else {
+        f29_mul2(t1, rr, t1, s1, s1, hhh);
+        f29_sub(acc.y, t1, s1);      // N+-
+    }
 }
 
 // acc += (x2, y2) affine (N; y2 may be N+-), same structure: 8M + 3S.
@@ -482,9 +534,13 @@ SBFT_DEV void p29_add_aff_lean_i(jp29& acc, const f29& x2, const f29& y2) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) t.v[i] = r2.v[i] - hhh.v[i] - (u2.v[i] << 1);
     f29_normalize(acc.x, t);
-    f29_sub(t, u2, acc.x);
-    f29_mul2(t, rr, t, s2, acc.y, hhh);
-    f29_sub(acc.y, t, s2);           // N+-
+    f29_sub(t, u2, acc.x);           // (-2^29.2, 2^29 + 2^26)
+    if (SBFT_MULSUB) {
+        f29_mul_sub(acc.y, rr, t, acc.y, hhh);  // rr t - Y1 H^3: N
+    } else {
+        f29_mul2(t, rr, t, s2, acc.y, hhh);
+        f29_sub(acc.y, t, s2);       // N+-
+    }
 }
 
 // dbl-2001-b shape (3M + 5S in the literature) under the signed-limb bounds: 4M + 4S and two

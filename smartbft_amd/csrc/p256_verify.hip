@@ -236,6 +236,7 @@ struct sinv_ws {
     uint4* suf;  // n x 32 B
     uint4* tot;  // nb x 32 B
     uint4* kb;   // nb x 32 B
+    uint4* qtab; // n x 640 B: per-lane Q tables (SBFT_QTAB_GLOBAL)
 };
 #ifdef SBFT_DEBUG_BOUNDS
 #define SBFT_CHECK(cond, what, a, b)                                                              \
@@ -481,7 +482,23 @@ __global__ __launch_bounds__(256) void p256_gcomb_build_kernel(uint4* __restrict
     e[4] = make_uint4(my.v[6], my.v[7], my.v[8], 0u);
 }
 
+// an affine point as a 20-word entry (the comb's layout): x limbs 0..8, pad, y limbs 0..8, pad
+SBFT_DEV void pack_entry(const f29& x, const f29& y, uint4 (&e)[5]) {
+    e[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+    e[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+    e[2] = make_uint4(x.v[8], 0u, y.v[0], y.v[1]);
+    e[3] = make_uint4(y.v[2], y.v[3], y.v[4], y.v[5]);
+    e[4] = make_uint4(y.v[6], y.v[7], y.v[8], 0u);
+}
+
 // ------------------------------------------------------------ the kernels
+// The throughput kernel's Q table: 1 = each lane's 8 entries contiguous in the workspace (640 B
+// per tuple, 5 x 16-B loads per digit); 0 = a private array (lane-interleaved scratch, A/B only).
+// Same-box A/B (profiles/r03i_qtab_mulsub_ab.txt): 14.75 -> 14.04 ms per 1M, HBM traffic 21.7 ->
+// 7.9 KB per verify.
+#ifndef SBFT_QTAB_GLOBAL
+#define SBFT_QTAB_GLOBAL 1
+#endif
 #ifndef SBFT_DBL_UNROLL
 #define SBFT_DBL_UNROLL 1
 #endif
@@ -853,6 +870,21 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
         inv::inv_mod_p(zi.v, zp.v, dtab);
         return zi;
     });
+#if SBFT_QTAB_GLOBAL
+    // the ladder reads the table from this lane's own contiguous 640 B (5 x 16 B per entry) in
+    // the workspace: a digit's entry is 72 contiguous bytes (two 64-B segments), where the
+    // lane-interleaved scratch layout spreads it over 18 rows shared by the wave's 8 entries
+    uint4* const qg = ws.qtab + (size_t)idx * (kQTab * 5);
+    if (active) {
+#pragma unroll
+        for (int m = 0; m < kQTab; ++m) {
+            uint4 e[5];
+            pack_entry(tx[m], ty[m], e);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) qg[m * 5 + k] = e[k];
+        }
+    }
+#endif
     fe u1, u2;
     bool neg1, neg2;
     verify_scalars(sinv_from_ws(ws, gid, n, active), valid, e_raw, r, u1, u2, neg1, neg2);
@@ -875,8 +907,20 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
 #else
         const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
 #endif
+#if SBFT_QTAB_GLOBAL
+        uint4 e[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) e[k] = qg[m2 * 5 + k];
+        const u32* w = reinterpret_cast<const u32*>(e);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            x2.v[k] = w[k];
+            y2.v[k] = w[10 + k];
+        }
+#else
         x2 = tx[m2];
         y2 = ty[m2];
+#endif
         if ((d2 < 0) != neg2) f29_neg(y2, y2);
     };
     auto digit_step = [&](int i) __attribute__((always_inline)) {
@@ -1403,7 +1447,8 @@ __global__ __launch_bounds__(FRAMED ? 320 : 256) void p256_verify_keyed_lanes_ke
 }  // namespace sbft
 
 // Workspace layout (sbft_verify_work_bytes): [0, 4(n+1)) fixup counter + list, then the
-// batched-inversion arrays pre | suf (32 B per tuple) and tot | kb (32 B per workgroup).
+// batched-inversion arrays pre | suf (32 B per tuple) and tot | kb (32 B per workgroup), then
+// (256-aligned) the throughput kernel's per-lane Q tables (640 B per tuple).
 // The counter is zeroed on the stream before the lean kernel; the fixup grid reads it on the
 // device, so the whole sequence stays asynchronous.
 extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
@@ -1420,6 +1465,7 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
     ws.suf = reinterpret_cast<uint4*>(base + o_pre + 32ull * n);
     ws.tot = reinterpret_cast<uint4*>(base + o_pre + 64ull * n);
     ws.kb = reinterpret_cast<uint4*>(base + o_pre + 64ull * n + 32ull * blocks);
+    ws.qtab = reinterpret_cast<uint4*>(base + ((o_pre + 64ull * n + 64ull * blocks + 255) & ~255ull));
 #ifdef SBFT_DEBUG_BOUNDS
 #define SBFT_STEP(name)                                                                      \
     do {                                                                                     \

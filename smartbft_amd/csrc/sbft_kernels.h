@@ -9,10 +9,12 @@
 // fixup counter + list (4(n+1) B, rounded to 256), then the batched-inversion arrays
 // pre | suf (32 B per tuple) and tot | kb (32 B per 1,024-tuple s^-1 group). tot | kb are
 // sized per 256 tuples (an over-allocation of 48 B per 1,024 tuples, kept so the workspace
-// formula, and so sbft_gv_verify_workspace_bytes, did not change with the group size).
+// formula, and so sbft_gv_verify_workspace_bytes, did not change with the group size). Then,
+// 256-aligned, the throughput kernel's per-lane Q tables: 8 affine entries x 80 B = 640 B per
+// tuple (SBFT_QTAB_GLOBAL, p256_verify.hip).
 static inline size_t sbft_verify_work_bytes(size_t n) {
     const size_t blocks = (n + 255) / 256;
-    return ((4 * (n + 1) + 255) & ~(size_t)255) + 64 * n + 64 * blocks;
+    return ((((4 * (n + 1) + 255) & ~(size_t)255) + 64 * n + 64 * blocks + 255) & ~(size_t)255) + 640 * n;
 }
 
 extern "C" {

@@ -416,6 +416,32 @@ bool parse_payload(const uint8_t* p, size_t len, std::vector<Req>& out) {
     return parse_payload(p, len, out, [](uint32_t) {});
 }
 
+// The chain of length prefixes alone, VerifyProposal's part of the parse before its launch:
+// each request's body offset and length (the request without its 64-byte signature). Every
+// request must be at least as long as the smallest well-formed one (magic, two empty ids, an
+// empty payload, key, signature), so the kernel's reads of the body's last 64 bytes (Q) and of
+// the signature stay inside it. A payload this rejects, parse_payload rejects too; one it
+// accepts can still be malformed inside a request (the full parse decides, during the verify).
+constexpr uint32_t kMinRequest = 4 + 2 + 2 + 4 + 65 + 64;
+bool walk_payload(const uint8_t* p, size_t len, std::vector<uint64_t>& off, std::vector<uint32_t>& blen) {
+    Reader r{p, len};
+    uint32_t count;
+    if (!r.u32(count) || count > len / 4) return false;
+    off.resize(count);
+    blen.resize(count);
+    for (uint32_t i = 0; i < count; ++i) {
+        uint32_t l;
+        const uint8_t* q;
+        __builtin_prefetch(p + r.pos + 2048);
+        if (!r.u32(l) || l < kMinRequest) return false;
+        const size_t at = r.pos;
+        if (!r.take(l, q)) return false;
+        off[i] = at;
+        blen[i] = l - 64;
+    }
+    return r.pos == len;
+}
+
 // A process-wide pool of warm helper threads for the proposal parse. run(T, f) runs f(0) on the
 // caller and f(1..T-1) on helpers, and returns when all are done. A helper spins (yielding) for
 // ~0.5 ms after a job, so back-to-back proposals find it awake; then it sleeps. If another
@@ -1247,35 +1273,28 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
     ProposalScratch& scr = proposal_scratch();  // this thread's, also when prepare runs elsewhere
     std::vector<Req>& reqs = scr.reqs;
     std::vector<uint8_t>& ok = scr.ok;
-    // parse + per-request format checks -> the body offsets / lengths of the framed requests. The
-    // parse runs over several threads for a large proposal (parse_payload_par); per_req(b, e)
-    // is extra per-request work on the requests [b, e) (the registry lookups), run on the thread
-    // that parsed them.
+    // The format verdict: the full parse (magic, ids, lengths) and the key prefix of every
+    // request, the first bad one in order reported. It runs while the GPU verifies (`during`):
+    // the launch needs only the chain of length prefixes (walk_payload), and the call returns
+    // its verdict, not the GPU's, whenever it finds a malformed request.
     static const int parse_threads = parse_threads_for(1);
-    auto prepare_cb = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len, auto&& sized,
-                          auto&& per_req) -> int {
+    bool checked = false;
+    int fmt_rc = 0;
+    auto check = [&]() -> int {
+        checked = true;
         std::atomic<uint32_t> first_bad_key{UINT32_MAX};
         const bool ok_parse = parse_payload_par(
-            p->payload, p->payload_len, reqs, parse_threads,
-            [&](size_t n) {
-                off.resize(n);
-                len.resize(n);
-                sized(n);
-            },
-            [&](uint32_t b, uint32_t e) {
-                for (uint32_t i = b; i < e; ++i) {
+            p->payload, p->payload_len, reqs, parse_threads, [](size_t) {}, [&](uint32_t b, uint32_t e) {
+                for (uint32_t i = b; i < e; ++i)
                     if (reqs[i].pub[0] != 0x04) {  // the first one in order is reported below
                         uint32_t cur = first_bad_key.load(std::memory_order_relaxed);
                         while (i < cur && !first_bad_key.compare_exchange_weak(cur, i)) {
                         }
                         break;
                     }
-                    off[i] = reqs[i].body_off;
-                    len[i] = (uint32_t)reqs[i].body_len;
-                }
-                per_req(b, e);
             });
         if (!ok_parse) {
+            reqs.clear();
             put_err(err, err_cap, "malformed proposal payload");
             return SBFT_V_EFORMAT;
         }
@@ -1288,52 +1307,56 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
         }
         return 0;
     };
-    auto prepare = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
-        return prepare_cb(off, len, [](size_t) {}, [](uint32_t, uint32_t) {});
-    };
-    bool registered;
-    {
-        std::shared_lock<std::shared_mutex> g(v->clients_mu);
-        registered = v->clients.count != 0;
-    }
     if (!v->ctx) {
-        if (int prc = prepare(scr.off, scr.len)) return prc;
+        if (int prc = check()) return prc;
         ok.clear();
         if (reqs.empty()) return finish_proposal(reqs, ok, infos, infos_cap, count, bad_index, err, err_cap);
         put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(SBFT_GV_ENODEV));
         return SBFT_GV_ENODEV;
     }
-    // One framed launch, the parse overlapped with the payload copy, and the RequestInfo
-    // records written while the GPU verifies (they are returned only if every request passes).
-    // With client keys registered, the parse also looks every request's key up: if all are
-    // registered, the batch takes the keyed launch over their comb tables (no doublings);
-    // otherwise the generic launch verifies every request (the same verdicts).
+    bool registered;
+    {
+        std::shared_lock<std::shared_mutex> g(v->clients_mu);
+        registered = v->clients.count != 0;
+    }
+    // One framed launch, the walk overlapped with the payload copy; the format check and the
+    // RequestInfo records run while the GPU verifies (they are returned only if every request
+    // passes). With client keys registered, every request's key (the 64 bytes before its
+    // signature) is looked up after the walk: if all are registered, the batch takes the keyed
+    // launch over their comb tables (no doublings); otherwise the generic launch verifies every
+    // request (the same verdicts).
     std::vector<uint32_t>& kid = scr.kid;
     kid.clear();
+    auto prepare = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
+        if (!walk_payload(p->payload, p->payload_len, off, len)) {
+            checked = true;  // the full parse would reject it too: no launch
+            reqs.clear();
+            put_err(err, err_cap, "malformed proposal payload");
+            return fmt_rc = SBFT_V_EFORMAT;
+        }
+        return 0;
+    };
     auto prepare_keyed = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
-        // each parse thread looks its own requests up, each map slot prefetched kAhead lookups
-        // before it is read
-        constexpr uint32_t kAhead = 8;
-        std::atomic<bool> all{true};
-        std::shared_lock<std::shared_mutex> g(v->clients_mu);  // covers the helpers' lookups too
-        const int prc = prepare_cb(
-            off, len, [&](size_t n) { kid.resize(n); },
-            [&](uint32_t b, uint32_t e) {
-                for (uint32_t i = b; i < e && i < b + kAhead; ++i) v->clients.prefetch(reqs[i].pub + 1);
-                for (uint32_t i = b; i < e; ++i) {
-                    if (i + kAhead < e) v->clients.prefetch(reqs[i + kAhead].pub + 1);
-                    if (!(kid[i] = v->clients.find(reqs[i].pub + 1))) {
-                        all.store(false, std::memory_order_relaxed);
-                        break;
-                    }
-                }
-            });
-        if (prc) return prc;
-        if (!all.load()) kid.clear();
+        if (int prc = prepare(off, len)) return prc;
+        // each key's map slot prefetched kAhead lookups before it is read
+        constexpr size_t kAhead = 8;
+        const size_t n = off.size();
+        auto key = [&](size_t i) { return p->payload + off[i] + len[i] - 64; };
+        std::shared_lock<std::shared_mutex> g(v->clients_mu);
+        kid.resize(n);
+        for (size_t i = 0; i < n && i < kAhead; ++i) v->clients.prefetch(key(i));
+        for (size_t i = 0; i < n; ++i) {
+            if (i + kAhead < n) v->clients.prefetch(key(i + kAhead));
+            if (!(kid[i] = v->clients.find(key(i)))) {
+                kid.clear();
+                break;
+            }
+        }
         return 0;
     };
     int info_rc = 0;
     auto during = [&] {
+        if ((fmt_rc = check())) return;
         char* w = infos;
         char* end = infos + infos_cap;
         for (auto& q : reqs)
@@ -1346,10 +1369,13 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
                                                           ok, during, &kid)
                               : sbft_gv_framed_overlapped(v->ctx, p->payload, p->payload_len, 0, -64, prepare, ok,
                                                           during);
+    if (!checked) fmt_rc = check();  // the engine returned before `during` (or failed)
+    if (fmt_rc) return fmt_rc;       // the format verdict first, as before any launch
     if (rc) {
-        if (rc != SBFT_V_EFORMAT) put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
+        put_err(err, err_cap, "gpu engine: %s", sbft_gv_strerror(rc));
         return rc;
     }
+    if (reqs.size() != ok.size()) return SBFT_GV_EINVAL;
     return finish_proposal(reqs, ok, nullptr, 0, count, bad_index, err, err_cap, info_rc);
 }
 

@@ -62,13 +62,14 @@ def test_strerror_and_no_gpu_failure_is_loud():
 
 def test_verify_workspace_layout():
     """The verify pipeline's device workspace: fixup counter + list (4(n+1) B, 256-aligned),
-    then pre | suf (32 B per tuple) and tot | kb (32 B per 256-tuple workgroup). An undersized
-    workspace is a device fault, so pin the formula on the CPU."""
+    then pre | suf (32 B per tuple) and tot | kb (32 B per 256-tuple workgroup), then (256-aligned)
+    the per-lane Q tables (640 B per tuple). An undersized workspace is a device fault, so pin
+    the formula on the CPU."""
     from smartbft_amd import gpuverify
     lib = gpuverify.load_library()
     for n in [1, 255, 256, 257, 65280, 65536, 1_000_000]:
         blocks = (n + 255) // 256
-        want = ((4 * (n + 1) + 255) // 256) * 256 + 64 * n + 64 * blocks
+        want = ((((4 * (n + 1) + 255) // 256) * 256 + 64 * n + 64 * blocks + 255) // 256) * 256 + 640 * n
         assert lib.sbft_gv_verify_workspace_bytes(n) == want, n
 
 

@@ -342,6 +342,53 @@ def test_verify_proposal_registered_clients(gpu, net):
     v.close()
 
 
+@pytest.mark.parametrize("registered", [False, True])
+def test_verify_proposal_format_checked_during_verify(gpu, net, registered):
+    """VerifyProposal launches after the chain of length prefixes alone and runs the full format
+    check while the GPU verifies (verifier.cpp walk_payload / check): a request malformed inside
+    (magic, a NUL in an id, a compressed key) under an intact length chain gets the format
+    verdict, ahead of any signature verdict, on the generic and the registered-key launch; a good
+    proposal after them verifies."""
+    _, nodes, clients = net
+    v = plugin.Verifier(gpu, 3)
+    good, reqs = _proposal(clients, 1100)
+    if registered:
+        v.add_clients([q[-129:-64] for q in reqs[:len(clients)]])
+
+    def enc(rs):
+        return plugin.Proposal(plugin.encode_payload(rs), b"header", b"metadata", 3)
+
+    def expect(rs, text, index=None):
+        with pytest.raises(plugin.VerifyError) as ei:
+            v.VerifyProposal(enc(rs))
+        assert ei.value.code == plugin.EFORMAT and text in str(ei.value), str(ei.value)
+        if index is not None:
+            assert ei.value.index == index
+        if index is None:
+            assert v.RequestsFromProposal(enc(rs)) == []
+
+    _, bad_sig = _proposal(clients, 1100, tamper=100)
+    for at in (0, 700, 1099):
+        rs = list(bad_sig)
+        rs[at] = b"X" + rs[at][1:]                     # broken magic, same length
+        expect(rs, "malformed proposal payload")
+        rs = list(bad_sig)
+        rs[at] = rs[at][:6] + b"\0" + rs[at][7:]      # NUL inside the client id
+        expect(rs, "malformed proposal payload")
+        rs = list(bad_sig)
+        rs[at] = rs[at][:-129] + b"\x02" + rs[at][-128:]  # compressed-key prefix
+        expect(rs, "public key is not SEC1 uncompressed", index=at)
+    # a request shorter than the smallest well-formed one fails the walk (no launch)
+    rs = list(reqs)
+    rs[5] = rs[5][:100]
+    expect(rs, "malformed proposal payload")
+    assert len(v.VerifyProposal(good)) == 1100
+    with pytest.raises(plugin.VerifyError) as ei:
+        v.VerifyProposal(enc(bad_sig))
+    assert ei.value.code == plugin.EVERIFY and ei.value.index == 100
+    v.close()
+
+
 def test_verify_proposal_format_errors_and_concurrent_callers(net):
     """The overlapped path (parse on the engine's helper thread): format errors found there come
     back with their own code and text, and concurrent callers (helper busy -> inline parse)
