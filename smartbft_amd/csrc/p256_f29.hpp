@@ -109,11 +109,11 @@ SBFT_DEV void f29_mul(f29& r, const f29& a, const f29& b) {
 }
 
 // a^2: off-diagonal products against the doubled operand (one mad each), then the squares.
-SBFT_DEV void f29_sqr(f29& r, const f29& a) {
+// f29_sqr_d takes the doubled operand from the caller when it has it already (2Y, 2g in the
+// doubling): d must be exactly 2a limb by limb.
+SBFT_DEV void f29_sqr_d(f29& r, const f29& a, const f29& d2) {
     const f29_red K = f29_red_consts();
-    u32 d[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
+    const u32* d = d2.v;
     u32 m[9];
     i64 acc = 0;
 #pragma unroll
@@ -134,6 +134,12 @@ SBFT_DEV void f29_sqr(f29& r, const f29& a) {
         acc = sar29(acc);
     }
     r.v[8] = (u32)acc;
+}
+SBFT_DEV void f29_sqr(f29& r, const f29& a) {
+    f29 d;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d.v[i] = a.v[i] << 1;
+    f29_sqr_d(r, a, d);
 }
 
 // N independent products (job x squares a[x] when bit x of SQ is set) with their mads
@@ -257,6 +263,121 @@ SBFT_DEV void f29_mul_sub(f29& r, const f29& a, const f29& b, const f29& c, cons
 #ifndef SBFT_MULSUB
 #define SBFT_MULSUB 1  // the additions' Y3 through f29_mul_sub (0: two products + subtraction)
 #endif
+
+// ---------------------------------------------------------------- products with addends
+// Mont(a b) + sum_t c_t v_t (mod p) in one pass, c_t small signed constants (|c_t v_t limb| <
+// 2^34). Montgomery's output comes out of columns 9..17, so adding v 2^261 to the column sums
+// adds v to the result exactly: v's limb i goes into column 9 + i, one mad each, after the
+// reduction multipliers m[] are taken from columns 0..8. The formulas' "X3 = u^2 - 4 b2",
+// "Y3 = al t - 8 g^2" then need no subtraction loop and no separate normalisation:
+// f29_fold_top takes the bits at 2^256 and up off the signed top limb (as f29_normalize does)
+// and the output is N' (limbs 0..7 in (-2^25, 2^29 + 2^25), limb 8 in [0, 2^24), |x| < 2^257).
+// Column contract: f29_mul's (the addend terms are < 2^34 against 2^63 of headroom); value:
+// |Mont(a b)| < |a b| 2^-261 + p, plus |sum c_t v_t|, must stay below 2^260 (|h| <= 2^4).
+// hmask = 0 skips the fold (the output then stays a plain product's N, for c_t = 0 lanes).
+SBFT_DEV void f29_fold_top(f29& r, u32 top, u32 hmask) {
+    const i32 h = ((i32)top >> 24) & (i32)hmask;
+    r.v[8] = top - ((u32)h << 24);
+    r.v[7] += (u32)h << 21;
+    r.v[6] = (u32)((i32)r.v[6] + h * -(1 << 18));
+    r.v[3] = (u32)((i32)r.v[3] + h * -(1 << 9));
+    r.v[0] += (u32)h;
+#ifndef SBFT_NO_OPAQUE_LIMBS
+#pragma unroll
+    for (int i = 0; i < 9; ++i) asm("" : "+v"(r.v[i]));
+#endif
+}
+// Opaque small constants for the addends (SGPRs; a visible -4 becomes shifts and 64-bit adds).
+SBFT_DEV u32 f29_kconst(i32 c) {
+    u32 k = (u32)c;
+    asm("" : "+s"(k));
+    return k;
+}
+// Chain form (the throughput kernel: 4 waves per SIMD hide the dependent mads' wait states).
+template <bool SQ, int NA>
+SBFT_DEV void f29_mulsq_add(f29& r, const f29& a, const f29& b, const f29* const (&v)[NA], const u32 (&c)[NA]) {
+    const f29_red K = f29_red_consts();
+    u32 d[9];
+    if (SQ)
+#pragma unroll
+        for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
+    u32 m[9];
+    i64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const int j = k - i;
+            if (SQ) {
+                if (j > i && j <= 8) acc = smad(a.v[i], d[j], acc);
+            } else {
+                if (j >= 0 && j <= 8) acc = smad(a.v[i], b.v[j], acc);
+            }
+        }
+        if (SQ && (k & 1) == 0) acc = smad(a.v[k >> 1], a.v[k >> 1], acc);
+        if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], K.c9, acc);
+        if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], K.c18, acc);
+        if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], K.c7, acc);
+        if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], K.c8, acc);
+        if (k >= 9)
+#pragma unroll
+            for (int t = 0; t < NA; ++t) acc = smad(v[t]->v[k - 9], c[t], acc);
+        if (k < 9) m[k] = lo29(acc);
+        else r.v[k - 9] = lo29(acc);
+        acc = sar29(acc);
+    }
+#pragma unroll
+    for (int t = 0; t < NA; ++t) acc = smad(v[t]->v[8], c[t], acc);
+    f29_fold_top(r, (u32)acc, ~0u);
+}
+// ILP form (lane pairs: one product per lane per step; see f29_mulsq_ilp below), per-lane
+// constants c (VGPRs) and fold mask.
+template <bool SQ, int NA>
+SBFT_DEV void f29_mulsq_add_ilp(f29& r, const f29& a, const f29& b, const f29* const (&v)[NA], const u32 (&c)[NA],
+                                u32 hmask) {
+    const f29_red K = f29_red_consts();
+    u32 d[9];
+    if (SQ)
+#pragma unroll
+        for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
+    i64 col[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) col[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int k = 0; k < 17; ++k) {
+            const int j = k - i;
+            if (SQ) {
+                if (j > i && j <= 8) col[k] = smad(a.v[i], d[j], col[k]);
+                if (j == i) col[k] = smad(a.v[i], a.v[i], col[k]);
+            } else {
+                if (j >= 0 && j <= 8) col[k] = smad(a.v[i], b.v[j], col[k]);
+            }
+        }
+#pragma unroll
+    for (int k = 9; k < 17; ++k)
+#pragma unroll
+        for (int t = 0; t < NA; ++t) col[k] = smad(v[t]->v[k - 9], c[t], col[k]);
+    u32 m[9];
+    i64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+        i64 x = col[k];
+        if (k >= 3 && k - 3 <= 8) x = smad(m[k - 3], K.c9, x);
+        if (k >= 6 && k - 6 <= 8) x = smad(m[k - 6], K.c18, x);
+        if (k >= 7 && k - 7 <= 8) x = smad(m[k - 7], K.c7, x);
+        if (k >= 8 && k - 8 <= 8) x = smad(m[k - 8], K.c8, x);
+        acc = k == 0 ? x : x + acc;
+        if (k < 9) m[k] = lo29(acc);
+        else r.v[k - 9] = lo29(acc);
+        acc = sar29(acc);
+    }
+    u32 top = (u32)acc;
+#pragma unroll
+    for (int t = 0; t < NA; ++t) top += v[t]->v[8] * c[t];
+    f29_fold_top(r, top, hmask);
+}
 
 SBFT_DEV void f29_add(f29& r, const f29& a, const f29& b) {
 #pragma unroll
@@ -578,15 +699,51 @@ SBFT_DEV void p29_dbl_b(jp29& r, const jp29& p) {
     f29_normalize(r.y, t1);          // Y3 (N')
 }
 
+// p29_dbl_b with X3 and Y3 as products with addends (f29_mulsq_add): the same 4M + 4S, but
+// X3 = al^2 - 4 b2 and Y3 = al (2 b2 - X3) - 8 g^2 leave their products already folded to N',
+// so the two subtraction loops, the 4L scaling and three normalisations are gone.
+// Value bounds: b2, l = g^2 < 2^256.6 (products of N' values), so |X3| < 2^259, |Y3| < 2^259.3
+// before the fold. In/out as p29_dbl_b (X3, Y3 in N', Z3 a product output in N).
+SBFT_DEV void p29_dbl_f(jp29& r, const jp29& p) {
+    f29 d, g, t0, t1, a1, al, b2, l, x3;
+    f29 y2;
+    f29_add(y2, p.y, p.y);           // 2Y < 2^30.2
+    f29_sqr(d, p.z);                 // 2^29.2^2
+    f29_sqr_d(g, p.y, y2);
+    f29_add(t0, g, g);               // 2g < 2^30
+    f29_mul(b2, p.x, t0);            // 2^29.2 x 2^30
+    f29_sub(t1, p.x, d);             // |.| < 2^29.2
+    f29_add(a1, p.x, d);             // < 2^30.1
+    f29_mul(a1, t1, a1);             // a' (2^29.2 x 2^30.1)
+    f29_muls(al, a1, 3);             // 3a' < 2^30.6, |3a'| < 2^259.6
+    f29_normalize(al, al);           // alpha (N')
+    f29_mul(r.z, y2, p.z);           // Z3 = 2YZ (2^30.2 x 2^29.2)
+    {
+        const f29* const v[1] = {&b2};
+        const u32 c[1] = {f29_kconst(-4)};
+        f29_mulsq_add<true, 1>(x3, al, al, v, c);  // X3 = alpha^2 - 4 b2 (2^29.2^2; -4 b2 < 2^31): N'
+    }
+    f29_sqr_d(l, g, t0);             // gamma^2 (N)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t0.v[i] = (b2.v[i] << 1) - x3.v[i];  // (-2^29.2, 2^30 + 2^25)
+    {
+        const f29* const v[1] = {&l};
+        const u32 c[1] = {f29_kconst(-8)};
+        f29_mulsq_add<false, 1>(r.y, al, t0, v, c);  // Y3 = alpha t0 - 8 L (2^29.2 x 2^30.1): N'
+    }
+    r.x = x3;
+}
+
 #ifndef SBFT_F29_IL
 #define SBFT_F29_IL 6
 #endif
 // SBFT_F29_IL bit 0/1/2: interleaved form of the doubling / Jacobian addition / mixed addition
 #ifndef SBFT_DBL_FORM
-#define SBFT_DBL_FORM 1  // 0: 6M + 2S (p29_dbl_s / _i), 1: 4M + 4S (p29_dbl_b)
+#define SBFT_DBL_FORM 2  // 0: 6M + 2S (p29_dbl_s / _i), 1: 4M + 4S (p29_dbl_b), 2: p29_dbl_b fused (p29_dbl_f)
 #endif
 SBFT_DEV void p29_dbl(jp29& r, const jp29& p) {
-    if (SBFT_DBL_FORM == 1) p29_dbl_b(r, p);
+    if (SBFT_DBL_FORM == 2) p29_dbl_f(r, p);
+    else if (SBFT_DBL_FORM == 1) p29_dbl_b(r, p);
     else if (SBFT_F29_IL & 1) p29_dbl_i(r, p);
     else p29_dbl_s(r, p);
 }
@@ -594,8 +751,38 @@ SBFT_DEV void p29_add_jac_lean(jp29& acc, const jp29& b) {
     if (SBFT_F29_IL & 2) p29_add_jac_lean_i(acc, b);
     else p29_add_jac_lean_s(acc, b);
 }
+#ifndef SBFT_ADD_FUSED
+#define SBFT_ADD_FUSED 1  // the mixed additions' X3 as a product with addends (p29_add_aff_lean_f)
+#endif
+// p29_add_aff_lean_i with X3 = r^2 - HHH - 2V as one product with two addends (f29_mulsq_add):
+// no subtraction loop, no normalisation. HH rides with S2 (one interleaved pair) so r^2 can
+// wait for HHH and V. |X3| < 2^256.1 + 2^256.6 + 2^257.6 < 2^258.5 before the fold: N'.
+SBFT_DEV void p29_add_aff_lean_f(jp29& acc, const f29& x2, const f29& y2) {
+    f29 z1z1, u2, s2, h, rr, hh, hhh, t, x3;
+    f29_sqr(z1z1, acc.z);
+    f29_mul2(u2, x2, z1z1, t, acc.z, z1z1);
+    f29_sub(h, u2, acc.x);           // (-2^29.2, 2^29 + 2^25)
+    {
+        f29* const r[2] = {&s2, &hh};
+        const f29* const a[2] = {&y2, &h};
+        const f29* const b[2] = {&t, &h};
+        f29_mulv<2, 2u>(r, a, b);    // S2 = y2 Z1^3 (2^29.2 x 2^29) | HH = H^2 (2^29.2^2)
+    }
+    f29_sub(rr, s2, acc.y);          // (-2^29.2, 2^29.2)
+    f29_mul3(hhh, hh, h, u2, acc.x, hh, acc.z, acc.z, h);  // H^3, V = X1 H^2, Z3 = Z1 H
+    {
+        const f29* const v[2] = {&hhh, &u2};
+        const u32 c[2] = {f29_kconst(-1), f29_kconst(-2)};
+        f29_mulsq_add<true, 2>(x3, rr, rr, v, c);  // X3 = r^2 - HHH - 2V: N'
+    }
+    f29_sub(t, u2, x3);              // (-2^29.2, 2^29 + 2^25)
+    f29_mul_sub(acc.y, rr, t, acc.y, hhh);  // rr t - Y1 H^3: N
+    acc.x = x3;
+}
+
 SBFT_DEV void p29_add_aff_lean(jp29& acc, const f29& x2, const f29& y2) {
-    if (SBFT_F29_IL & 4) p29_add_aff_lean_i(acc, x2, y2);
+    if (SBFT_ADD_FUSED) p29_add_aff_lean_f(acc, x2, y2);
+    else if (SBFT_F29_IL & 4) p29_add_aff_lean_i(acc, x2, y2);
     else p29_add_aff_lean_s(acc, x2, y2);
 }
 
@@ -710,7 +897,7 @@ SBFT_DEV void f29_unpair(const f29& o, f29& e, f29& d) {
 // p29_dbl_b on a lane pair (same products, same bounds):
 //   1: d = Z^2 | g = Y^2     2: b2 = X (2g) | a' = (X - d)(X + d)
 //   3: alpha^2 | gamma^2     4: alpha (2 b2 - X3) | Z3 = 2 Y Z
-SBFT_DEV void p29_dbl_pair(jp29& r, const jp29& p, bool odd) {
+SBFT_DEV void p29_dbl_pair_b(jp29& r, const jp29& p, bool odd) {
     f29 o, d, g, t0, t1, a1, al, b2, m, l, x3, z3;
     f29_sqr_ilp(o, f29_pick(odd, p.z, p.y));                        // 2^29.2^2
     f29_unpair(o, d, g);
@@ -744,7 +931,7 @@ SBFT_DEV void p29_dbl_pair(jp29& r, const jp29& p, bool odd) {
 // p29_add_aff_lean on a lane pair (same products, same bounds, no case analysis):
 //   1: Z1^2 (both)          2: U2 = x2 Z1^2 | Z1^3     3: HH = H^2 | S2 = y2 Z1^3
 //   4: V = X1 HH | HHH      5: r^2 | Z3 = Z1 H          6: r (V - X3) | Y1 HHH
-SBFT_DEV void p29_add_aff_pair(jp29& acc, const f29& x2, const f29& y2, bool odd) {
+SBFT_DEV void p29_add_aff_pair_b(jp29& acc, const f29& x2, const f29& y2, bool odd) {
     f29 o, z1z1, u2, s2, h, rr, hh, hhh, v, r2, z3, t, s;
     f29_sqr_ilp(z1z1, acc.z);
     f29_mul_ilp(o, f29_pick(odd, x2, acc.z), z1z1);
@@ -765,6 +952,83 @@ SBFT_DEV void p29_add_aff_pair(jp29& acc, const f29& x2, const f29& y2, bool odd
     f29_unpair(o, t, s);
     f29_sub(acc.y, t, s);                                       // N+-
     acc.z = z3;
+}
+
+// The pair forms with products with addends (f29_mulsq_add_ilp): the even lane's X3 and Y3
+// come out of their products folded (N'), the odd lane's product takes c = 0. This takes the
+// normalisations and subtraction loops off the pair's critical path.
+#ifndef SBFT_PAIR_FUSED
+#define SBFT_PAIR_FUSED 1
+#endif
+//   1: d = Z^2 | g = Y^2     2: b2 = X (2g) | a' = (X - d)(X + d)
+//   3: X3 = alpha^2 - 4 b2 | L = gamma^2     4: Y3 = alpha (2 b2 - X3) - 8 L | Z3 = 2 Y Z
+SBFT_DEV void p29_dbl_pair_f(jp29& r, const jp29& p, bool odd) {
+    f29 o, d, g, t0, t1, a1, al, b2, l, x3, z3;
+    f29_sqr_ilp(o, f29_pick(odd, p.z, p.y));                        // 2^29.2^2
+    f29_unpair(o, d, g);
+    f29_add(t0, g, g);                                          // 2g < 2^30
+    f29_sub(t1, p.x, d);                                        // |.| < 2^29.2
+    f29_add(a1, p.x, d);                                        // < 2^30.1
+    f29_mul_ilp(o, f29_pick(odd, p.x, t1), f29_pick(odd, t0, a1));  // 2^29.2 x 2^30 | 2^29.2 x 2^30.1
+    f29_unpair(o, b2, a1);
+    f29_muls(al, a1, 3);                                        // 3a' < 2^30.6
+    f29_normalize(al, al);                                      // alpha (N')
+    {
+        const f29* const v[1] = {&b2};
+        const u32 c[1] = {odd ? 0u : (u32)-4};
+        const f29 sq = f29_pick(odd, al, g);
+        f29_mulsq_add_ilp<true, 1>(o, sq, sq, v, c, ~0u);       // alpha^2 - 4 b2 | gamma^2: N'
+    }
+    f29_unpair(o, x3, l);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t0.v[i] = (b2.v[i] << 1) - x3.v[i];  // (-2^29.2, 2^30 + 2^25)
+    f29_add(t1, p.y, p.y);                                      // 2Y < 2^30.2
+    {
+        const f29* const v[1] = {&l};
+        const u32 c[1] = {odd ? 0u : (u32)-8};
+        f29_mulsq_add_ilp<false, 1>(o, f29_pick(odd, al, t1), f29_pick(odd, t0, p.z), v, c,
+                                    odd ? 0u : ~0u);            // alpha t0 - 8 L: N' | 2YZ: N
+    }
+    f29_unpair(o, r.y, z3);
+    r.x = x3;
+    r.z = z3;
+}
+
+//   1: Z1^2 (both)          2: U2 = x2 Z1^2 | Z1^3     3: HH = H^2 | S2 = y2 Z1^3
+//   4: V = X1 HH | HHH      5: X3 = r^2 - HHH - 2V | Z3 = Z1 H      6: r (V - X3) | Y1 HHH
+SBFT_DEV void p29_add_aff_pair_f(jp29& acc, const f29& x2, const f29& y2, bool odd) {
+    f29 o, z1z1, u2, s2, h, rr, hh, hhh, v, x3, z3, t, s;
+    f29_sqr_ilp(z1z1, acc.z);
+    f29_mul_ilp(o, f29_pick(odd, x2, acc.z), z1z1);
+    f29_unpair(o, u2, s2);
+    f29_sub(h, u2, acc.x);                                      // (-2^29.2, 2^29 + 2^26)
+    f29_mul_ilp(o, f29_pick(odd, h, y2), f29_pick(odd, h, s2));
+    f29_unpair(o, hh, s2);
+    f29_sub(rr, s2, acc.y);                                     // (-2^29.2, 2^29.2)
+    f29_mul_ilp(o, f29_pick(odd, acc.x, hh), f29_pick(odd, hh, h));
+    f29_unpair(o, v, hhh);
+    {
+        const f29* const w[2] = {&hhh, &v};
+        const u32 c[2] = {odd ? 0u : (u32)-1, odd ? 0u : (u32)-2};
+        f29_mulsq_add_ilp<false, 2>(o, f29_pick(odd, rr, acc.z), f29_pick(odd, rr, h), w, c,
+                                    odd ? 0u : ~0u);            // r^2 - HHH - 2V: N' | Z1 H: N
+    }
+    f29_unpair(o, x3, z3);
+    f29_sub(t, v, x3);                                          // (-2^29.2, 2^29 + 2^25)
+    f29_mul_ilp(o, f29_pick(odd, rr, acc.y), f29_pick(odd, t, hhh));
+    f29_unpair(o, t, s);
+    f29_sub(acc.y, t, s);                                       // N+-
+    acc.x = x3;
+    acc.z = z3;
+}
+
+SBFT_DEV void p29_dbl_pair(jp29& r, const jp29& p, bool odd) {
+    if (SBFT_PAIR_FUSED) p29_dbl_pair_f(r, p, odd);
+    else p29_dbl_pair_b(r, p, odd);
+}
+SBFT_DEV void p29_add_aff_pair(jp29& acc, const f29& x2, const f29& y2, bool odd) {
+    if (SBFT_PAIR_FUSED) p29_add_aff_pair_f(acc, x2, y2, odd);
+    else p29_add_aff_pair_b(acc, x2, y2, odd);
 }
 
 // ---------------------------------------------------------------- co-Z table building
