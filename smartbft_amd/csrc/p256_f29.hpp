@@ -334,50 +334,7 @@ SBFT_DEV void f29_mulsq_add(f29& r, const f29& a, const f29& b, const f29* const
 // constants c (VGPRs) and fold mask.
 template <bool SQ, int NA>
 SBFT_DEV void f29_mulsq_add_ilp(f29& r, const f29& a, const f29& b, const f29* const (&v)[NA], const u32 (&c)[NA],
-                                u32 hmask) {
-    const f29_red K = f29_red_consts();
-    u32 d[9];
-    if (SQ)
-#pragma unroll
-        for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
-    i64 col[17];
-#pragma unroll
-    for (int k = 0; k < 17; ++k) col[k] = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i)
-#pragma unroll
-        for (int k = 0; k < 17; ++k) {
-            const int j = k - i;
-            if (SQ) {
-                if (j > i && j <= 8) col[k] = smad(a.v[i], d[j], col[k]);
-                if (j == i) col[k] = smad(a.v[i], a.v[i], col[k]);
-            } else {
-                if (j >= 0 && j <= 8) col[k] = smad(a.v[i], b.v[j], col[k]);
-            }
-        }
-#pragma unroll
-    for (int k = 9; k < 17; ++k)
-#pragma unroll
-        for (int t = 0; t < NA; ++t) col[k] = smad(v[t]->v[k - 9], c[t], col[k]);
-    u32 m[9];
-    i64 acc = 0;
-#pragma unroll
-    for (int k = 0; k < 17; ++k) {
-        i64 x = col[k];
-        if (k >= 3 && k - 3 <= 8) x = smad(m[k - 3], K.c9, x);
-        if (k >= 6 && k - 6 <= 8) x = smad(m[k - 6], K.c18, x);
-        if (k >= 7 && k - 7 <= 8) x = smad(m[k - 7], K.c7, x);
-        if (k >= 8 && k - 8 <= 8) x = smad(m[k - 8], K.c8, x);
-        acc = k == 0 ? x : x + acc;
-        if (k < 9) m[k] = lo29(acc);
-        else r.v[k - 9] = lo29(acc);
-        acc = sar29(acc);
-    }
-    u32 top = (u32)acc;
-#pragma unroll
-    for (int t = 0; t < NA; ++t) top += v[t]->v[8] * c[t];
-    f29_fold_top(r, top, hmask);
-}
+                                u32 hmask);
 
 SBFT_DEV void f29_add(f29& r, const f29& a, const f29& b) {
 #pragma unroll
@@ -426,6 +383,29 @@ SBFT_DEV void f29_normalize(f29& r, const f29& a) {
 #endif
     r = t;
 }
+
+// alpha = 3 a' for a product output a' (limbs 0..7 in [0, 2^29), |a'| < 2^256.6): one carry
+// pass, no fold. Out: limbs 0..7 in [0, 2^29 + 2), limb 8 = 3 a'_8 + carry (|.| < 2^26.2),
+// |alpha| < 2^258.2 -- limb bounds within N', and alpha^2, alpha t (|t| < 2^258.2) stay below
+// 2^516.4, so their Montgomery outputs are < 2^256.6 like any product of N' values.
+SBFT_DEV void f29_triple(f29& r, const f29& a) {
+    u32 t[9], c[8];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t[i] = a.v[i] * 3u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = t[i] >> 29;  // 3 a_i < 2^30.6: carry 0..2
+    r.v[0] = t[0] & F29_MASK;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) r.v[i] = (t[i] & F29_MASK) + c[i - 1];
+    r.v[8] = t[8] + c[7];
+#if !defined(SBFT_NO_OPAQUE_LIMBS) && !defined(SBFT_NO_OPAQUE_NORM)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) asm("" : "+v"(r.v[i]));
+#endif
+}
+#ifndef SBFT_TRIPLE_CARRY
+#define SBFT_TRIPLE_CARRY 1  // alpha by f29_triple (0: f29_muls + f29_normalize)
+#endif
 
 // ---------------------------------------------------------------- exact zero tests mod p
 // Common tail: limbs 0..7 in [0, 2^29), limb 8 signed, |x| < 2^258. The bits at 2^256 and up,
@@ -715,8 +695,12 @@ SBFT_DEV void p29_dbl_f(jp29& r, const jp29& p) {
     f29_sub(t1, p.x, d);             // |.| < 2^29.2
     f29_add(a1, p.x, d);             // < 2^30.1
     f29_mul(a1, t1, a1);             // a' (2^29.2 x 2^30.1)
-    f29_muls(al, a1, 3);             // 3a' < 2^30.6, |3a'| < 2^259.6
-    f29_normalize(al, al);           // alpha (N')
+    if (SBFT_TRIPLE_CARRY) {
+        f29_triple(al, a1);          // alpha (limbs < 2^29 + 2, |alpha| < 2^258.2)
+    } else {
+        f29_muls(al, a1, 3);         // 3a' < 2^30.6, |3a'| < 2^259.6
+        f29_normalize(al, al);       // alpha (N')
+    }
     f29_mul(r.z, y2, p.z);           // Z3 = 2YZ (2^30.2 x 2^29.2)
     {
         const f29* const v[1] = {&b2};
@@ -835,45 +819,80 @@ SBFT_DEV void add_aff_fix(jp29& acc, bool& inf, Dbl dbl, Reload reload) {
 // pair forms use f29_mul_ilp / f29_sqr_ilp: the 17 product columns are summed first as
 // independent chains, then the Montgomery pass adds carry and reduction terms column by column
 // (one extra 64-bit add per column, no wait states in the product part).
+// SBFT_ILP_LA > 0: software-pipelined form. At one wave per SIMD (the latency kernels) nothing
+// hides the Montgomery pass's serial chain (per column a 64-bit add and a 64-bit shift, each
+// waiting on the last), and with every column summed first (SBFT_ILP_LA = 0) the chain runs
+// after all 81 product mads with idle issue slots. Summing column k + LA while the chain is at
+// column k gives the scheduler product mads to fill those slots with; the instructions are the
+// same.
+#ifndef SBFT_ILP_LA
+#define SBFT_ILP_LA 4
+#endif
 template <bool SQ>
-SBFT_DEV void f29_mulsq_ilp(f29& r, const f29& a, const f29& b) {
+SBFT_DEV i64 f29_column(int k, const f29& a, const f29& b, const u32 (&d)[9]) {
+    i64 c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const int j = k - i;
+        if (SQ) {
+            if (j > i && j <= 8) c = smad(a.v[i], d[j], c);
+            if (j == i) c = smad(a.v[i], a.v[i], c);
+        } else {
+            if (j >= 0 && j <= 8) c = smad(a.v[i], b.v[j], c);
+        }
+    }
+    return c;
+}
+// Mont(a b) + sum_t c_t v_t with NA addends (see f29_mulsq_add; NA = 0: a plain product, v and
+// c unused), the fold masked by hmask.
+template <bool SQ, int NA>
+SBFT_DEV void f29_mulsq_core(f29& r, const f29& a, const f29& b, const f29* const* v, const u32* c, u32 hmask) {
     const f29_red K = f29_red_consts();
     u32 d[9];
     if (SQ)
 #pragma unroll
         for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
     i64 col[17];
+    constexpr int LA = SBFT_ILP_LA > 0 ? SBFT_ILP_LA : 17;
 #pragma unroll
-    for (int k = 0; k < 17; ++k) col[k] = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i)
-#pragma unroll
-        for (int k = 0; k < 17; ++k) {
-            const int j = k - i;
-            if (SQ) {
-                if (j > i && j <= 8) col[k] = smad(a.v[i], d[j], col[k]);
-                if (j == i) col[k] = smad(a.v[i], a.v[i], col[k]);
-            } else {
-                if (j >= 0 && j <= 8) col[k] = smad(a.v[i], b.v[j], col[k]);
-            }
-        }
+    for (int k = 0; k < LA && k < 17; ++k) col[k] = f29_column<SQ>(k, a, b, d);
     // Reduction terms first (m[k-3..] are ready columns ahead), the carry last: the serial
     // chain is one 64-bit add and one shift per column.
     u32 m[9];
     i64 acc = 0;
 #pragma unroll
     for (int k = 0; k < 17; ++k) {
+        if (k + LA < 17) col[k + LA] = f29_column<SQ>(k + LA, a, b, d);
         i64 x = col[k];
         if (k >= 3 && k - 3 <= 8) x = smad(m[k - 3], K.c9, x);
         if (k >= 6 && k - 6 <= 8) x = smad(m[k - 6], K.c18, x);
         if (k >= 7 && k - 7 <= 8) x = smad(m[k - 7], K.c7, x);
         if (k >= 8 && k - 8 <= 8) x = smad(m[k - 8], K.c8, x);
+        if (k >= 9)
+#pragma unroll
+            for (int t = 0; t < NA; ++t) x = smad(v[t]->v[k - 9], c[t], x);
         acc = k == 0 ? x : x + acc;
         if (k < 9) m[k] = lo29(acc);
         else r.v[k - 9] = lo29(acc);
         acc = sar29(acc);
     }
-    r.v[8] = (u32)acc;
+    u32 top = (u32)acc;
+    if (NA > 0) {
+#pragma unroll
+        for (int t = 0; t < NA; ++t) top += v[t]->v[8] * c[t];
+        f29_fold_top(r, top, hmask);
+    } else {
+        r.v[8] = top;
+    }
+}
+template <bool SQ>
+SBFT_DEV void f29_mulsq_ilp(f29& r, const f29& a, const f29& b) {
+    f29_mulsq_core<SQ, 0>(r, a, b, nullptr, nullptr, 0u);
+}
+template <bool SQ, int NA>
+SBFT_DEV void f29_mulsq_add_ilp(f29& r, const f29& a, const f29& b, const f29* const (&v)[NA], const u32 (&c)[NA],
+                                u32 hmask) {
+    f29_mulsq_core<SQ, NA>(r, a, b, v, c, hmask);
 }
 SBFT_DEV void f29_mul_ilp(f29& r, const f29& a, const f29& b) { f29_mulsq_ilp<false>(r, a, b); }
 SBFT_DEV void f29_sqr_ilp(f29& r, const f29& a) { f29_mulsq_ilp<true>(r, a, a); }
@@ -971,8 +990,12 @@ SBFT_DEV void p29_dbl_pair_f(jp29& r, const jp29& p, bool odd) {
     f29_add(a1, p.x, d);                                        // < 2^30.1
     f29_mul_ilp(o, f29_pick(odd, p.x, t1), f29_pick(odd, t0, a1));  // 2^29.2 x 2^30 | 2^29.2 x 2^30.1
     f29_unpair(o, b2, a1);
-    f29_muls(al, a1, 3);                                        // 3a' < 2^30.6
-    f29_normalize(al, al);                                      // alpha (N')
+    if (SBFT_TRIPLE_CARRY) {
+        f29_triple(al, a1);                                     // alpha (limbs < 2^29 + 2)
+    } else {
+        f29_muls(al, a1, 3);                                    // 3a' < 2^30.6
+        f29_normalize(al, al);                                  // alpha (N')
+    }
     {
         const f29* const v[1] = {&b2};
         const u32 c[1] = {odd ? 0u : (u32)-4};
@@ -1030,6 +1053,141 @@ SBFT_DEV void p29_add_aff_pair(jp29& acc, const f29& x2, const f29& y2, bool odd
     if (SBFT_PAIR_FUSED) p29_add_aff_pair_f(acc, x2, y2, odd);
     else p29_add_aff_pair_b(acc, x2, y2, odd);
 }
+
+// ---------------------------------------------------------------- lane-local pair doubling
+// A lane of the pair issues one instruction every ~4 cycles whatever it is (one wave per SIMD),
+// so the pair's glue counts as much as its products. p29_dbl_pair keeps every value in both
+// lanes: each step picks the two lanes' operands (18 v_cndmask) and hands both products to both
+// lanes (18 DPP moves). The lane-local form keeps the point as
+//   xb = X (both lanes), zy = Z (even lane) | Y (odd lane), zo = Z (odd lane),
+// feeds each step from the lanes' own results, and moves across the pair (one quad_perm swap,
+// 9 DPP) only the value the other lane needs: 159 glue instructions per doubling against 213.
+// Same products, same bounds as p29_dbl_pair_f:
+//   1: d = Z^2 | g = Y^2                     2: b2 = X (2g) | a' = (X - d)(X + d)
+//   3: X3 = alpha^2 - 4 b2 | L = gamma^2     4: Y3 = alpha (2 b2 - X3) - 8 L | Z3 = 2 Y Z
+struct pl29 {
+    f29 xb, zy, zo;
+};
+// even lane's e, odd lane's o: one v_cndmask on the constant odd-lane mask. Written as asm so
+// the compiler cannot turn a run of selects into a branch on the lane parity (it did: both
+// sides then run one after the other, with exec-mask flips between them).
+SBFT_DEV u32 sel_pair(u32 e, u32 o) {
+    u32 r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(e), "v"(o), "s"(0xAAAAAAAAAAAAAAAAull));
+    return r;
+}
+SBFT_DEV f29 f29_sel_pair(const f29& e, const f29& o) {
+    f29 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = sel_pair(e.v[i], o.v[i]);
+    return r;
+}
+SBFT_DEV f29 f29_swap_pair(const f29& a) {  // each lane gets its partner's value (quad_perm [1,0,3,2])
+    f29 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)a.v[i], 0xB1, 0xF, 0xF, false);
+    return r;
+}
+SBFT_DEV f29 f29_bcast_pair(const f29& a, bool from_odd) {  // the even (odd) lane's value in both lanes
+    f29 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+        r.v[i] = from_odd ? (u32)__builtin_amdgcn_mov_dpp((int)a.v[i], 0xF5, 0xF, 0xF, false)
+                          : (u32)__builtin_amdgcn_mov_dpp((int)a.v[i], 0xA0, 0xF, 0xF, false);
+    return r;
+}
+SBFT_DEV pl29 pl29_from(const jp29& p, bool odd) {
+    pl29 q;
+    q.xb = p.x;
+    q.zy = f29_sel_pair(p.z, p.y);
+    q.zo = p.z;
+    (void)odd;
+    return q;
+}
+SBFT_DEV void pl29_to(jp29& p, const pl29& q) {
+    p.x = q.xb;
+    p.y = f29_bcast_pair(q.zy, true);
+    p.z = f29_bcast_pair(q.zy, false);
+}
+SBFT_DEV void p29_dbl_pl(pl29& P, bool odd) {
+    const u32 om = sel_pair(0u, ~0u);
+    f29 o1, s1, a, b, o2, s2, al, o3, s3, o4;
+    f29_sqr_ilp(o1, P.zy);                                      // d | g (2^29.2^2)
+    s1 = f29_swap_pair(o1);                                     // g | d
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        a.v[i] = P.xb.v[i] - (s1.v[i] & om);                    // X | X - d: |.| < 2^29.2
+        b.v[i] = s1.v[i] + sel_pair(s1.v[i], P.xb.v[i]);        // 2g < 2^30 | X + d < 2^30.1
+    }
+    f29_mul_ilp(o2, a, b);                                      // b2 | a'
+    s2 = f29_swap_pair(o2);                                     // a' | b2
+    f29_triple(al, s2);                                         // alpha (even lane)
+    {
+        const f29 sq = f29_sel_pair(al, o1);
+        const f29* const v[1] = {&o2};
+        const u32 c[1] = {sel_pair((u32)-4, 0u)};
+        f29_mulsq_add_ilp<true, 1>(o3, sq, sq, v, c, ~0u);     // X3 = alpha^2 - 4 b2 | L = gamma^2: N'
+    }
+    s3 = f29_swap_pair(o3);                                     // L | X3
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const u32 t0 = (o2.v[i] << 1) - o3.v[i];                // 2 b2 - X3: (-2^29.2, 2^30 + 2^25)
+        const u32 y2 = P.zy.v[i] << 1;                          // 2Y < 2^30.2 (odd lane)
+        a.v[i] = sel_pair(al.v[i], y2);
+        b.v[i] = sel_pair(t0, P.zo.v[i]);
+    }
+    {
+        const f29* const v[1] = {&s3};
+        const u32 c[1] = {sel_pair((u32)-8, 0u)};
+        f29_mulsq_add_ilp<false, 1>(o4, a, b, v, c, ~om);      // Y3 = alpha t0 - 8 L: N' | Z3 = 2YZ: N
+    }
+    P.xb = f29_sel_pair(o3, s3);                                // X3 in both lanes
+    P.zy = f29_swap_pair(o4);                                   // Z3 | Y3
+    P.zo = o4;                                                  // Z3 (odd lane)
+    (void)odd;
+}
+// The mixed addition in the lane-local form (p29_add_aff_pair_f's products, same bounds):
+//   1: Z1^2 (both)   2: U2 = x2 Z1^2 | Z1^3   3: HH = H^2 | S2 = y2 Z1^3   4: V = X1 HH | HHH
+//   5: Z3 = Z1 H | X3 = r^2 - HHH - 2V        6: Y1 HHH | r (V - X3)
+// (x2, y2) affine in both lanes. Out: X3 in N', Y3 in N+-, Z3 in N, as p29_add_aff_pair_f.
+SBFT_DEV void p29_add_aff_pl(pl29& P, const f29& x2, const f29& y2) {
+    f29 z1, o1, o2, s2, h, o3, s3, hh, o4, s4, r, o5, s5, szy, a, b, o6, s6;
+    z1 = f29_sel_pair(P.zy, P.zo);                              // Z1 in both lanes
+    f29_sqr_ilp(o1, z1);                                        // Z1^2
+    f29_mul_ilp(o2, f29_sel_pair(x2, z1), o1);                  // U2 | Z1^3
+    s2 = f29_swap_pair(o2);                                     // Z1^3 | U2
+#pragma unroll
+    for (int i = 0; i < 9; ++i) h.v[i] = sel_pair(o2.v[i], s2.v[i]) - P.xb.v[i];  // H: (-2^29.2, 2^29 + 2^25)
+    f29_mul_ilp(o3, f29_sel_pair(h, y2), f29_sel_pair(h, o2));  // HH | S2
+    s3 = f29_swap_pair(o3);                                     // S2 | HH
+    hh = f29_sel_pair(o3, s3);                                  // HH in both lanes
+    f29_mul_ilp(o4, f29_sel_pair(P.xb, h), hh);                 // V | HHH
+    s4 = f29_swap_pair(o4);                                     // HHH | V
+    f29_sub(r, o3, P.zy);                                       // r = S2 - Y1 (odd lane): |.| < 2^29.2
+    {
+        const f29* const v[2] = {&o4, &s4};
+        const u32 c[2] = {sel_pair(0u, (u32)-1), sel_pair(0u, (u32)-2)};
+        f29_mulsq_add_ilp<false, 2>(o5, f29_sel_pair(P.zy, r), f29_sel_pair(h, r), v, c,
+                                    sel_pair(0u, ~0u));         // Z3 = Z1 H: N | X3 = r^2 - HHH - 2V: N'
+    }
+    szy = f29_swap_pair(P.zy);                                  // Y1 (even lane)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        a.v[i] = sel_pair(szy.v[i], r.v[i]);
+        b.v[i] = sel_pair(s4.v[i], s4.v[i] - o5.v[i]);          // HHH | V - X3: (-2^29.2, 2^29 + 2^25)
+    }
+    f29_mul_ilp(o6, a, b);                                      // Y1 HHH | r (V - X3)
+    s6 = f29_swap_pair(o6);
+    s5 = f29_swap_pair(o5);                                     // X3 | Z3
+    P.xb = f29_bcast_pair(o5, true);                            // X3 in both lanes
+#pragma unroll
+    for (int i = 0; i < 9; ++i) P.zy.v[i] = sel_pair(o5.v[i], o6.v[i] - s6.v[i]);  // Z3 | Y3 (N+-)
+    P.zo = s5;                                                  // Z3 (odd lane)
+}
+
+#ifndef SBFT_PAIR_LANE_LOCAL
+#define SBFT_PAIR_LANE_LOCAL 1
+#endif
 
 // ---------------------------------------------------------------- co-Z table building
 // Odd multiples [1, 3, ..., 2^w - 1]Q with Meloni's co-Z additions (2007): every point of the

@@ -741,8 +741,8 @@ SBFT_DEV int q_digit(const fe& k2, int i) {
 // fix(reload) runs after every addition (add_aff_fix: the comb's points are added on top of
 // u2 Q, so with a crafted Q any of them can meet acc == +-entry); reload(x, y) reloads the entry
 // just added.
-template <bool PINGPONG = false, class AddAff, class Fix>
-SBFT_DEV void comb_add_u1g(jp29& acc, const fe& u1, bool neg1, const uint4* __restrict__ gcomb, AddAff add,
+template <bool PINGPONG = false, class Acc, class AddAff, class Fix>
+SBFT_DEV void comb_add_u1g(Acc& acc, const fe& u1, bool neg1, const uint4* __restrict__ gcomb, AddAff add,
                            Fix fix) {
     constexpr int T = kGK + 1;  // entries summed
     fe k1 = u1;
@@ -1181,32 +1181,59 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
 #ifndef SBFT_PAIR_LADDER_DIGITS  // development: time the phases (tools/pair_probe.py --no-check)
 #define SBFT_PAIR_LADDER_DIGITS kQDigits
 #endif
-#pragma unroll 1
-    for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 0; --i) {
-        const int j = SBFT_PAIR_LADDER_DIGITS - 1 - i;  // additions done so far
+    auto qentry = [&](int i, f29& x, f29& y) {
+        const int d2 = q_digit(k2, i);
+        const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
 #pragma unroll
-        for (int d = 0; d < kQWin; ++d) {
-            if constexpr (kQuad) {
+        for (int k = 0; k < 9; ++k) {
+            x.v[k] = qtab[(m2 * 18 + k) * kTuples + pr];
+            y.v[k] = qtab[(m2 * 18 + 9 + k) * kTuples + pr];
+        }
+        if ((d2 < 0) != neg2) f29_neg(y, y);
+    };
+    if constexpr (!kQuad) {
+        if (SBFT_PAIR_LANE_LOCAL && SBFT_PAIR_LADDER_DIGITS > 0) {
+            // the ladder in the lane-local form; the last digit's addition (the only one that can
+            // be exceptional) in the both-lanes form, for add_aff_fix
+            pl29 q = pl29_from(acc, odd);
+#pragma unroll 1
+            for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 1; --i) {
+#pragma unroll
+                for (int d = 0; d < kQWin; ++d) p29_dbl_pl(q, odd);
+                f29 x2, y2;
+                qentry(i, x2, y2);
+                p29_add_aff_pl(q, x2, y2);
+            }
+#pragma unroll
+            for (int d = 0; d < kQWin; ++d) p29_dbl_pl(q, odd);
+            pl29_to(acc, q);
+            f29 x2, y2;
+            qentry(0, x2, y2);
+            p29_add_aff_pair(acc, x2, y2, odd);
+            add_aff_fix(acc, inf, dblp, [&](f29& x, f29& y) { qentry(0, x, y); });
+        } else {
+#pragma unroll 1
+            for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 0; --i) {
+#pragma unroll
+                for (int d = 0; d < kQWin; ++d) p29_dbl_pair(acc, acc, odd);
+                f29 x2, y2;
+                qentry(i, x2, y2);
+                p29_add_aff_pair(acc, x2, y2, odd);
+                if (i == 0) add_aff_fix(acc, inf, dblp, [&](f29& x, f29& y) { qentry(0, x, y); });
+            }
+        }
+    } else {
+#pragma unroll 1
+        for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 0; --i) {
+            const int j = SBFT_PAIR_LADDER_DIGITS - 1 - i;  // additions done so far
+#pragma unroll
+            for (int d = 0; d < kQWin; ++d) {
                 jp29 tt;
                 p29_dbl_pair(tt, acc, odd);
                 if (!comb_role) acc = tt;
-            } else {
-                p29_dbl_pair(acc, acc, odd);
             }
-        }
-        const int d2 = q_digit(k2, i);
-        const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
-        auto entry = [&](f29& x, f29& y) {
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                x.v[k] = qtab[(m2 * 18 + k) * kTuples + pr];
-                y.v[k] = qtab[(m2 * 18 + 9 + k) * kTuples + pr];
-            }
-            if ((d2 < 0) != neg2) f29_neg(y, y);
-        };
-        f29 x2, y2;
-        entry(x2, y2);
-        if constexpr (kQuad) {
+            f29 x2, y2;
+            qentry(i, x2, y2);
             // comb lanes: entry j + 1 while j + 1 <= K, then their accumulator is final
             const int ce = j + 1 <= kGK ? j + 1 : kGK;
             if (comb_role)
@@ -1218,9 +1245,6 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
             jp29 tt = acc;
             p29_add_aff_pair(tt, x2, y2, odd);
             if (!comb_role || j + 1 <= kGK) acc = tt;
-        } else {
-            p29_add_aff_pair(acc, x2, y2, odd);
-            if (i == 0) add_aff_fix(acc, inf, dblp, entry);  // the ladder's only exceptional spot
         }
     }
     if constexpr (kQuad) {
@@ -1235,9 +1259,25 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
         p29_add_jac_lean(acc, g);
     } else {
 #ifndef SBFT_PAIR_NO_COMB
-        comb_add_u1g<true>(acc, u1, neg1, gcomb,
-                           [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); },
-                           [&](auto reload) { add_aff_fix(acc, inf, dblp, reload); });
+        if (SBFT_PAIR_LANE_LOCAL) {
+            // lane-local comb additions; the exceptional-case repair (a wave-uniform branch that
+            // only runs when a lane of the wave needs it) converts to the both-lanes form
+            pl29 q = pl29_from(acc, odd);
+            comb_add_u1g<true>(q, u1, neg1, gcomb, [](pl29& a, const f29& x, const f29& y) { p29_add_aff_pl(a, x, y); },
+                               [&](auto reload) {
+                                   const bool hz = !inf && f29_zero_mod_p(f29_sel_pair(q.zy, q.zo));
+                                   if (__builtin_expect(__any(hz || inf), 0)) {
+                                       pl29_to(acc, q);
+                                       add_aff_fix(acc, inf, dblp, reload);
+                                       q = pl29_from(acc, odd);
+                                   }
+                               });
+            pl29_to(acc, q);
+        } else {
+            comb_add_u1g<true>(acc, u1, neg1, gcomb,
+                               [odd](jp29& a, const f29& x, const f29& y) { p29_add_aff_pair(a, x, y, odd); },
+                               [&](auto reload) { add_aff_fix(acc, inf, dblp, reload); });
+        }
 #endif
     }
 
