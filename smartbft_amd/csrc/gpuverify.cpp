@@ -1428,22 +1428,21 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256);
         rc = ensure_tables(sl, nkeys);
         if (!rc) rc = sl->reserve(align_up(n, 256));
-        if (!rc) rc = sl->reserve_vmap(fo + 2 * fl);
+        if (!rc) rc = sl->reserve_vmap(fo + 2 * fl + align_up(n, 256));
         if (rc) return rc;
         std::memcpy(sl->vmap, off.data(), 8 * n);
         std::memcpy(sl->vmap + fo, len.data(), 4 * n);
         std::memcpy(sl->vmap + fo + fl, kid->data(), 4 * n);
         const uint8_t* vd = sl->vmap_dev;
+        // verdicts straight to mapped host memory (no device-to-host copy after the launch)
         if (sbft_launch_p256_verify_keyed_framed(sl->bbuf, (const uint64_t*)vd, (const uint32_t*)(vd + fo), sig_rel,
                                                  (const uint32_t*)(vd + fo + fl), (const void* const*)sl->d_keytab,
-                                                 nkeys, sl->dbuf, (uint32_t)n, sl->stream))
+                                                 nkeys, sl->vmap_dev + fo + 2 * fl, (uint32_t)n, sl->stream))
             return SBFT_GV_ELAUNCH;
-        // `during` before the verdict copy: a copy into pageable memory returns only once the
-        // kernel has finished, which would serialise the caller's host work behind it
-        if (during) during();
-        HIPCHK(hipMemcpyAsync(ok.data(), sl->dbuf, n, hipMemcpyDeviceToHost, sl->stream));
+        if (during) during();  // the caller's host work that does not need the verdicts
         HIPCHK(hipStreamSynchronize(sl->stream));
         drain.armed = false;
+        std::memcpy(ok.data(), sl->vmap + fo + 2 * fl, n);
         return SBFT_GV_OK;
     }
     // Device: hash counter (256) | verify workspace | digests | r | s | qx | qy | ok. The
@@ -1454,7 +1453,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256), fd = align_up(32 * n, 256);
     const size_t fw = align_up(sbft_verify_work_bytes(n), 256);
     rc = sl->reserve(256 + fw + 5 * fd + align_up(n, 256));
-    if (!rc) rc = sl->reserve_vmap(fo + fl);
+    if (!rc) rc = sl->reserve_vmap(fo + fl + align_up(n, 256));
     if (rc) return rc;
     uint8_t* b = sl->dbuf;
     uint8_t *d_ctr = b, *d_work = d_ctr + 256, *d_dig = d_work + fw;
@@ -1471,11 +1470,20 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     // front (~37 us of a 10k-tuple call).
     const int lanes = ctx->lanes_for(n);
     if (framed_fused_on() && lanes >= 2) {
+        // the verdicts go straight to mapped host memory (n bytes over PCIe from the kernels'
+        // stores): no device-to-host copy and no copy-engine hand-off after the verify
+        uint8_t* const h_ok = sl->vmap + fo + fl;
         if (((!pre_dbuf || sl->dgen != pre_gen) &&
              hipMemsetAsync(d_work, 0, sizeof(uint32_t), sl->stream) != hipSuccess) ||
             sbft_launch_p256_verify_framed(sl->bbuf, d_off, d_len, (uint32_t)n, sig_rel, pub_rel, d_dig, v, v + fd,
-                                           v + 2 * fd, v + 3 * fd, d_ok, (uint32_t*)d_work, gcomb, sl->stream, lanes))
+                                           v + 2 * fd, v + 3 * fd, sl->vmap_dev + fo + fl, (uint32_t*)d_work, gcomb,
+                                           sl->stream, lanes))
             return SBFT_GV_ELAUNCH;
+        if (during) during();
+        HIPCHK(hipStreamSynchronize(sl->stream));
+        drain.armed = false;
+        std::memcpy(ok.data(), h_ok, n);
+        return SBFT_GV_OK;
     } else if (sbft_launch_gather_framed(sl->bbuf, d_off, d_len, (uint32_t)n, sig_rel, pub_rel, v, v + fd,
                                          v + 2 * fd, v + 3 * fd, sl->stream, (uint32_t*)d_ctr, (uint32_t*)d_work) ||
                sbft_launch_sha256(sl->bbuf, d_off, d_len, nullptr, d_dig, (uint32_t)n, (uint32_t*)d_ctr, sl->stream,
