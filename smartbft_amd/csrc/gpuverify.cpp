@@ -1453,7 +1453,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256), fd = align_up(32 * n, 256);
     const size_t fw = align_up(sbft_verify_work_bytes(n), 256);
     rc = sl->reserve(256 + fw + 5 * fd + align_up(n, 256));
-    if (!rc) rc = sl->reserve_vmap(fo + fl + align_up(n, 256));
+    if (!rc) rc = sl->reserve_vmap(fo + fl + align_up(n, 256) + 256);
     if (rc) return rc;
     uint8_t* b = sl->dbuf;
     uint8_t *d_ctr = b, *d_work = d_ctr + 256, *d_dig = d_work + fw;
@@ -1473,14 +1473,25 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         // the verdicts go straight to mapped host memory (n bytes over PCIe from the kernels'
         // stores): no device-to-host copy and no copy-engine hand-off after the verify
         uint8_t* const h_ok = sl->vmap + fo + fl;
+        uint8_t* const d_hok = sl->vmap_dev + fo + fl;
+        // the fixup kernel (the exact net for flagged tuples, which the in-place repair leaves
+        // none of in practice) runs only if the verify kernel raised this mapped flag
+        volatile uint32_t* const flag = (volatile uint32_t*)(h_ok + align_up(n, 256));
+        *flag = 0;
         if (((!pre_dbuf || sl->dgen != pre_gen) &&
              hipMemsetAsync(d_work, 0, sizeof(uint32_t), sl->stream) != hipSuccess) ||
             sbft_launch_p256_verify_framed(sl->bbuf, d_off, d_len, (uint32_t)n, sig_rel, pub_rel, d_dig, v, v + fd,
-                                           v + 2 * fd, v + 3 * fd, sl->vmap_dev + fo + fl, (uint32_t*)d_work, gcomb,
-                                           sl->stream, lanes))
+                                           v + 2 * fd, v + 3 * fd, d_hok, (uint32_t*)d_work, gcomb, sl->stream, lanes,
+                                           (uint32_t*)(d_hok + align_up(n, 256))))
             return SBFT_GV_ELAUNCH;
         if (during) during();
         HIPCHK(hipStreamSynchronize(sl->stream));
+        if (*flag) {
+            if (sbft_launch_p256_verify_fixup(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_hok, (const uint32_t*)d_work,
+                                              (uint32_t)n, sl->stream))
+                return SBFT_GV_ELAUNCH;
+            HIPCHK(hipStreamSynchronize(sl->stream));
+        }
         drain.armed = false;
         std::memcpy(ok.data(), h_ok, n);
         return SBFT_GV_OK;

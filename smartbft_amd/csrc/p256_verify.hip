@@ -979,6 +979,8 @@ struct FramedIn {
     const uint32_t* len;
     int32_t sig_rel, pub_rel;
     uint8_t *dig, *r, *s, *qx, *qy;  // SoA rows for the fixup kernel (flagged tuples only)
+    uint32_t* flagged;  // non-null: set to 1 (mapped host memory) when a tuple is flagged, and the
+                        // caller launches the fixup only then (sbft_launch_p256_verify_framed)
 };
 
 // 32 big-endian bytes at any byte address -> 8 little-endian limbs (reads up to 3 bytes past)
@@ -1298,6 +1300,9 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
             }
             const uint32_t slot = atomicAdd(work, 1u);
             work[1 + slot] = t;
+            if constexpr (FRAMED) {
+                if (fr.flagged) *(volatile uint32_t*)fr.flagged = 1u;
+            }
         } else {
             ok[t] = (valid && accept) ? 1 : 0;
         }
@@ -1610,11 +1615,28 @@ extern "C" int sbft_launch_gcomb_build(void* d_table, hipStream_t stream) {
 // Framed tuples on the small-batch kernels (lanes 2 or 4): hash, field reads and verify in one
 // launch (p256_verify_small_kernel<LPT, true>), then the fixup. The SoA rows (32 B per tuple
 // each) are written only for the rare tuples the fixup takes; d_work's counter must be zero.
+extern "C" int sbft_launch_p256_verify_fixup(const uint8_t* d_dig, const uint8_t* d_r, const uint8_t* d_s,
+                                             const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
+                                             const uint32_t* d_work, uint32_t n, hipStream_t stream) {
+    if (n == 0) return 0;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    const unsigned blocks = (n + 255) / 256, fix_cap = 8u * (unsigned)cus;
+    hipLaunchKernelGGL(sbft::p256_verify_fixup_kernel, dim3(blocks < fix_cap ? blocks : fix_cap), dim3(256), 0,
+                       stream, d_dig, d_r, d_s, d_qx, d_qy, d_ok, d_work);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
                                               uint32_t n, int32_t sig_rel, int32_t pub_rel, uint8_t* d_dig,
                                               uint8_t* d_r, uint8_t* d_s, uint8_t* d_qx, uint8_t* d_qy,
                                               uint8_t* d_ok, uint32_t* d_work, const void* d_gcomb,
-                                              hipStream_t stream, int lanes) {
+                                              hipStream_t stream, int lanes, uint32_t* h_flagged) {
     if (n == 0) return 0;
     if (lanes != 2 && lanes != 4) return -1;
     static int cus = 0;
@@ -1624,7 +1646,7 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
     }
-    const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, pub_rel, d_dig, d_r, d_s, d_qx, d_qy};
+    const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, pub_rel, d_dig, d_r, d_s, d_qx, d_qy, h_flagged};
     const unsigned tpw = 64 / (unsigned)lanes, sblocks = (n + tpw - 1) / tpw;
     if (lanes == 2)
         hipLaunchKernelGGL((sbft::p256_verify_small_kernel<2, true>), dim3(sblocks), dim3(128), 0, stream, d_dig,
@@ -1632,8 +1654,7 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
     else
         hipLaunchKernelGGL((sbft::p256_verify_small_kernel<4, true>), dim3(sblocks), dim3(128), 0, stream, d_dig,
                            d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
-    const unsigned blocks = (n + 255) / 256, fix_cap = 8u * (unsigned)cus;
-    hipLaunchKernelGGL(sbft::p256_verify_fixup_kernel, dim3(blocks < fix_cap ? blocks : fix_cap), dim3(256), 0,
-                       stream, d_dig, d_r, d_s, d_qx, d_qy, d_ok, (const uint32_t*)d_work);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (h_flagged) return 0;  // the caller launches the fixup if a tuple was flagged
+    return sbft_launch_p256_verify_fixup(d_dig, d_r, d_s, d_qx, d_qy, d_ok, d_work, n, stream);
 }

@@ -39,7 +39,14 @@ int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const u
 int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len, uint32_t n,
                                    int32_t sig_rel, int32_t pub_rel, uint8_t* d_dig, uint8_t* d_r, uint8_t* d_s,
                                    uint8_t* d_qx, uint8_t* d_qy, uint8_t* d_ok, uint32_t* d_work,
-                                   const void* d_gcomb, hipStream_t stream, int lanes);
+                                   const void* d_gcomb, hipStream_t stream, int lanes,
+                                   uint32_t* h_flagged = nullptr);
+// h_flagged (mapped host memory, zeroed by the caller): when given, the fixup kernel is not
+// launched; the verify kernel sets *h_flagged = 1 if it flagged a tuple, and the caller then
+// runs sbft_launch_p256_verify_fixup (same arguments) after its synchronisation.
+int sbft_launch_p256_verify_fixup(const uint8_t* d_dig, const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_qx,
+                                  const uint8_t* d_qy, uint8_t* d_ok, const uint32_t* d_work, uint32_t n,
+                                  hipStream_t stream);
 size_t sbft_gcomb_table_bytes(void);
 int sbft_launch_gcomb_build(void* d_table, hipStream_t stream);
 // SHA-256 of n messages blob[off[k] .. off[k]+len[k]); the blob must be readable

@@ -97,3 +97,66 @@ def test_crafted_exceptional_framed(crafted):
         assert np.array_equal(got, np.array(exp, dtype=np.uint8))
     finally:
         gv.close()
+
+
+def _sbr1(i: int, pl: bytes, qx: bytes, qy: bytes) -> bytes:
+    cid, rid = f"c{i}".encode(), f"r{i}".encode()
+    return (b"SBR1" + len(cid).to_bytes(2, "little") + cid + len(rid).to_bytes(2, "little") + rid +
+            len(pl).to_bytes(4, "little") + pl + b"\x04" + qx + qy)
+
+
+@pytest.mark.parametrize("mode", ["pair", "quad"])
+def test_crafted_exceptional_proposal(crafted, mode):
+    """The crafted tuples as signed requests inside a VerifyProposal of honest ones
+    (sbft_gv_framed_overlapped: fused hash + verify launch, verdicts in mapped host memory).
+    SBR1 signs the client's key, so a crafted request keeps u1 = e/s and u2 = r/s (the scalars
+    that make the ladder or the comb meet an exceptional addition) but not a valid r: each is a
+    rejection. The four-lane kernel joins u2 Q and u1 G with one lean Jacobian addition and has
+    no in-place repair, so these tuples are flagged and the fix-up kernel must run -- launched
+    only because the verify kernel raised the mapped flag; the two-lane kernel repairs them in
+    place. Each crafted request replaces an honest one of an all-valid proposal of the same size
+    verified just before (whose verdict bytes, all 1, are still in the mapped buffer), so a
+    skipped fix-up would show as an accepted proposal; the error must name that request."""
+    from smartbft_amd import GpuVerifier, plugin
+    cols, tags, want = crafted
+    opts = dict(pair_max=1 << 30, quad_max=-1) if mode == "pair" else dict(quad_max=1 << 30)
+    gv = GpuVerifier(**opts)
+    v = plugin.Verifier(gv)
+    try:
+        rng = np.random.default_rng(5)
+        honest = []
+        for i in range(96):
+            d = int.from_bytes(rng.bytes(32), "big") % N or 1
+            k = int.from_bytes(rng.bytes(32), "big") % N or 1
+            qx, qy = oracle.pubkey(d)
+            body = _sbr1(i, rng.bytes(int(rng.integers(16, 200))), qx, qy)
+            r, s = oracle.sign(d, k, hashlib.sha256(body).digest())
+            honest.append(body + r + s)
+        assert len(v.VerifyProposal(plugin.Proposal(plugin.encode_payload(honest)))) == len(honest)
+        tried = 0
+        for j in range(0, len(tags), max(1, len(tags) // 12)):
+            e0, r0, s0 = (int.from_bytes(bytes(cols[k][j]), "big") for k in range(3))
+            u1, u2 = e0 * pow(s0, -1, N) % N, r0 * pow(s0, -1, N) % N
+            qx, qy = bytes(cols[3][j]), bytes(cols[4][j])
+            body = _sbr1(1000 + j, rng.bytes(int(rng.integers(16, 200))), qx, qy)
+            e = int.from_bytes(hashlib.sha256(body).digest(), "big") % N
+            if e == 0 or u1 == 0:
+                continue
+            s = e * pow(u1, -1, N) % N
+            r = u2 * s % N
+            if r == 0:
+                continue
+            assert not oracle.verify_batch(*[np.frombuffer(x, dtype=np.uint8).reshape(1, 32) for x in
+                                             (hashlib.sha256(body).digest(), _b(r), _b(s), qx, qy)])[0]
+            at = (7 * j) % len(honest)
+            reqs = honest[:at] + [body + _b(r) + _b(s)] + honest[at + 1:]
+            with pytest.raises(plugin.VerifyError) as ei:
+                v.VerifyProposal(plugin.Proposal(plugin.encode_payload(reqs)))
+            assert ei.value.index == at, (tags[j], at, ei.value.index)
+            # the all-valid proposal again (its verdict bytes back to 1 for the next round)
+            assert len(v.VerifyProposal(plugin.Proposal(plugin.encode_payload(honest)))) == len(honest)
+            tried += 1
+        assert tried >= 8
+    finally:
+        v.close()
+        gv.close()
