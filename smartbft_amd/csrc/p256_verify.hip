@@ -236,7 +236,7 @@ struct sinv_ws {
     uint4* suf;  // n x 32 B
     uint4* tot;  // nb x 32 B
     uint4* kb;   // nb x 32 B
-    uint4* qtab; // n x 640 B: per-lane Q tables (SBFT_QTAB_GLOBAL)
+    uint4* qtab; // n x SBFT_VERIFY_QTAB_BYTES: per-lane Q tables (SBFT_QTAB_GLOBAL)
 };
 #ifdef SBFT_DEBUG_BOUNDS
 #define SBFT_CHECK(cond, what, a, b)                                                              \
@@ -506,9 +506,15 @@ constexpr int kDblUnroll = SBFT_DBL_UNROLL;  // doublings per iteration of the w
 #ifndef SBFT_QWIN
 #define SBFT_QWIN 4
 #endif
-constexpr int kQWin = SBFT_QWIN;                    // u2 in radix 2^w
+constexpr int kQWin = SBFT_QWIN;                    // u2 in radix 2^w (latency kernels)
 constexpr int kQTab = 1 << (kQWin - 1);             // [1, 3, ..., 2^w - 1]Q
 constexpr int kQDigits = (255 + kQWin - 1) / kQWin; // windows over u2 >> 1 (< 2^255)
+// the throughput kernel's window (SBFT_TQWIN): its Q table lives in the workspace
+// (SBFT_VERIFY_QTAB_BYTES per tuple), the latency kernels' in LDS
+constexpr int kTWin = SBFT_TQWIN;
+constexpr int kTTab = 1 << (kTWin - 1);
+constexpr int kTDigits = (255 + kTWin - 1) / kTWin;
+static_assert(kTTab * 80 == SBFT_VERIFY_QTAB_BYTES, "workspace Q-table stride (sbft_kernels.h)");
 #ifndef SBFT_VERIFY_WAVES
 #define SBFT_VERIFY_WAVES 4
 #endif
@@ -539,8 +545,8 @@ SBFT_DEV bool verify_inputs_valid(const fe& r, const fe& s, const fe& qx, const 
 // 4M + 2S each), then made affine with ONE inversion per lane (safegcd mod p of the final Z;
 // the earlier Z's follow from the recorded ratios h_k).
 // inv_p(z) returns z^-1 mod p (plain 8 x 32 limbs) for the plain canonical z.
-template <class InvP>
-SBFT_DEV void build_q_table(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, const fe& qy, bool valid,
+template <int TAB, class InvP>
+SBFT_DEV void build_q_table(f29 (&tx)[TAB], f29 (&ty)[TAB], const fe& qx, const fe& qy, bool valid,
                             InvP inv_p) {
     const f29 r2 = f29_const(C29_R2);
     f29 qxm, qym;
@@ -554,9 +560,9 @@ SBFT_DEV void build_q_table(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, co
     ty[0] = qym;
     f29 dx, dy, cx, cy, z;  // D = 2Q and the current odd multiple, co-Z (Z = z)
     p29_dblu(qxm, qym, dx, dy, cx, cy, z);
-    f29 hs[kQTab - 1];      // Z ratios: Z(T_k) = Z(T_{k-1}) h_k
+    f29 hs[TAB - 1];      // Z ratios: Z(T_k) = Z(T_{k-1}) h_k
 #pragma unroll 1
-    for (int k = 1; k < kQTab; ++k) {
+    for (int k = 1; k < TAB; ++k) {
         f29 h;
         p29_zaddu(cx, cy, dx, dy, h);  // T_k = T_{k-1} + 2Q
         tx[k] = cx;
@@ -570,7 +576,7 @@ SBFT_DEV void build_q_table(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, co
         f29_mul(inv, f29_from_u256(zi), r2);
     }
 #pragma unroll 1
-    for (int k = kQTab - 1; k >= 1; --k) {
+    for (int k = TAB - 1; k >= 1; --k) {
         f29 zi2, zi3;
         f29_sqr(zi2, inv);
         f29_mul(zi3, zi2, inv);
@@ -724,10 +730,12 @@ SBFT_DEV void verify_scalars(const fe& w, bool valid, const fe& e_raw, const fe&
 
 // Radix-2^w signed-odd digit i of u2 (u2 = sum_{i<K} d_i 2^(w i) + 2^(w K),
 // d_i = 2*((u2 >> (w i + 1)) & (2^w - 1)) - (2^w - 1), odd and nonzero).
+template <int W = kQWin>
 SBFT_DEV int q_digit(const fe& k2, int i) {
-    const int b = kQWin * i + 1, lw = b >> 5;
+    constexpr int tab = 1 << (W - 1);
+    const int b = W * i + 1, lw = b >> 5;
     const u32 lo = k2.v[lw], hi = lw < 7 ? k2.v[lw + 1] : 0u;
-    return 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & (2 * kQTab - 1)) - (2 * kQTab - 1);
+    return 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & (2 * tab - 1)) - (2 * tab - 1);
 }
 
 // u1*G by the fixed-base comb in HBM (no doublings): u1 = sum_{i<K} d_i 2^(W i) + 2^(W K) with
@@ -864,20 +872,20 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     const fe qy = load_be32(qyy + 32ull * idx);
     const bool valid = verify_inputs_valid(r, s, qx, qy);
 
-    f29 tx[kQTab], ty[kQTab];  // affine odd multiples (scratch)
+    f29 tx[kTTab], ty[kTTab];  // affine odd multiples (scratch)
     build_q_table(tx, ty, qx, qy, valid, [&](const fe& zp) {
         fe zi;
         inv::inv_mod_p(zi.v, zp.v, dtab);
         return zi;
     });
 #if SBFT_QTAB_GLOBAL
-    // the ladder reads the table from this lane's own contiguous 640 B (5 x 16 B per entry) in
+    // the ladder reads the table from this lane's own contiguous 80 B x 2^(w-1) (5 x 16 B per entry) in
     // the workspace: a digit's entry is 72 contiguous bytes (two 64-B segments), where the
     // lane-interleaved scratch layout spreads it over 18 rows shared by the wave's 8 entries
-    uint4* const qg = ws.qtab + (size_t)idx * (kQTab * 5);
+    uint4* const qg = ws.qtab + (size_t)idx * (kTTab * 5);
     if (active) {
 #pragma unroll
-        for (int m = 0; m < kQTab; ++m) {
+        for (int m = 0; m < kTTab; ++m) {
             uint4 e[5];
             pack_entry(tx[m], ty[m], e);
 #pragma unroll
@@ -901,7 +909,7 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     bool inf = false;  // acc is the point at infinity (add_aff_fix)
     auto dbl1 = [](jp29& p) { p29_dbl(p, p); };
     auto entry = [&](int i, f29& x2, f29& y2) __attribute__((always_inline)) {
-        const int d2 = q_digit(k2, i);
+        const int d2 = q_digit<kTWin>(k2, i);
 #ifdef SBFT_TABLE_PROBE  // measurement only (wrong verdicts): the ladder reads one fixed entry
         const int m2 = 0;
 #else
@@ -925,13 +933,13 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     };
     auto digit_step = [&](int i) __attribute__((always_inline)) {
 #pragma unroll kDblUnroll
-        for (int d = 0; d < kQWin; ++d) p29_dbl(acc, acc);
+        for (int d = 0; d < kTWin; ++d) p29_dbl(acc, acc);
         f29 x2, y2;
         entry(i, x2, y2);
         p29_add_aff_lean(acc, x2, y2);
     };
 #pragma unroll 1
-    for (int i = kQDigits - 1; i >= 1; --i) digit_step(i);
+    for (int i = kTDigits - 1; i >= 1; --i) digit_step(i);
     digit_step(0);  // the last digit, peeled: the fix's state stays out of the loop
     add_aff_fix(acc, inf, dbl1, [&](f29& x2, f29& y2) { entry(0, x2, y2); });
     comb_add_u1g(acc, u1, neg1, gcomb, [](jp29& a, const f29& x, const f29& y) { p29_add_aff_lean(a, x, y); },
@@ -1493,9 +1501,15 @@ __global__ __launch_bounds__(FRAMED ? 320 : 256) void p256_verify_keyed_lanes_ke
 
 // Workspace layout (sbft_verify_work_bytes): [0, 4(n+1)) fixup counter + list, then the
 // batched-inversion arrays pre | suf (32 B per tuple) and tot | kb (32 B per workgroup), then
-// (256-aligned) the throughput kernel's per-lane Q tables (640 B per tuple).
+// (256-aligned) the throughput kernel's per-lane Q tables (SBFT_VERIFY_QTAB_BYTES per tuple).
 // The counter is zeroed on the stream before the lean kernel; the fixup grid reads it on the
 // device, so the whole sequence stays asynchronous.
+extern "C" size_t sbft_verify_work_bytes(size_t n) {
+    const size_t blocks = (n + 255) / 256;
+    return ((((4 * (n + 1) + 255) & ~(size_t)255) + 64 * n + 64 * blocks + 255) & ~(size_t)255) +
+           (size_t)SBFT_VERIFY_QTAB_BYTES * n;
+}
+
 extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                        const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
                                        uint32_t n, uint32_t* d_work, const void* d_gcomb, hipStream_t stream,

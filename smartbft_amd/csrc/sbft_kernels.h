@@ -10,14 +10,18 @@
 // pre | suf (32 B per tuple) and tot | kb (32 B per 1,024-tuple s^-1 group). tot | kb are
 // sized per 256 tuples (an over-allocation of 48 B per 1,024 tuples, kept so the workspace
 // formula, and so sbft_gv_verify_workspace_bytes, did not change with the group size). Then,
-// 256-aligned, the throughput kernel's per-lane Q tables: 8 affine entries x 80 B = 640 B per
-// tuple (SBFT_QTAB_GLOBAL, p256_verify.hip).
-static inline size_t sbft_verify_work_bytes(size_t n) {
-    const size_t blocks = (n + 255) / 256;
-    return ((((4 * (n + 1) + 255) & ~(size_t)255) + 64 * n + 64 * blocks + 255) & ~(size_t)255) + 640 * n;
-}
+// 256-aligned, the throughput kernel's per-lane Q tables: 2^(w-1) affine entries x 80 B per
+// tuple (SBFT_VERIFY_QTAB_BYTES; w = SBFT_TQWIN, p256_verify.hip kTWin: 640 B at w = 4). The size is computed by the object that
+// holds the kernel (sbft_verify_work_bytes below), so a -DSBFT_TQWIN build of p256_verify.hip
+// alone sizes its own workspace.
+#ifndef SBFT_TQWIN
+#define SBFT_TQWIN 4
+#endif
+#define SBFT_VERIFY_QTAB_BYTES (80 << (SBFT_TQWIN - 1))
 
 extern "C" {
+// bytes of device workspace one sbft_launch_p256_verify call of n tuples needs
+size_t sbft_verify_work_bytes(size_t n);
 // P-256 verify of n SoA tuples (32-byte big-endian fields) -> n verdict bytes.
 // d_work: device workspace of sbft_verify_work_bytes(n) bytes, private to the stream.
 // d_gcomb: the device's fixed-base comb table for u1*G (sbft_gcomb_table_bytes() bytes, built
