@@ -1,0 +1,270 @@
+"""Overflow and limb-range model of the radix-2^29 field arithmetic (smartbft_amd/csrc/p256_f29.hpp),
+run on the CPU: every product column, every 64-bit accumulator and every 32-bit limb of the
+throughput kernel's doubling (p29_dbl_f) and mixed addition (p29_add_aff_lean_f), including the
+products with addends (f29_mulsq_add) and the carry-only tripling (f29_triple), is restated here
+in Python integers and checked against the int64 / int32 widths the GPU computes in, while the
+values are checked against the curve (oracle/pyref.py, the group law in Python big integers).
+
+The inputs are not just canonical: before every operation each value is re-limbed at random
+inside its stated contract (N: limbs 0..7 in [0, 2^29); N': limbs 0..7 in (-2^26, 2^29 + 2^26),
+limb 8 in [0, 2^24); N+-: |limb| < 2^29), value unchanged, so the column bounds are exercised
+near the edges the comments at each use site claim. The lane-pair forms (p29_dbl_pl,
+p29_add_aff_pl) compute the same products on the same operands, in a different summation order
+whose partial sums the per-column sum of |terms| bounds as well (checked here)."""
+import random
+
+import pytest
+
+from oracle import pyref
+
+P = pyref.P
+R = 1 << 261
+RINV = pow(R, -1, P)
+MASK = (1 << 29) - 1
+I64 = 1 << 63
+I32 = 1 << 31
+
+
+def i32(u):
+    u &= 0xFFFFFFFF
+    return u - (1 << 32) if u & 0x80000000 else u
+
+
+def val(limbs):
+    return sum(i32(w) << (29 * i) for i, w in enumerate(limbs))
+
+
+def to_limbs(x):  # canonical limbs of 0 <= x < 2^261 (limb 8 holds the top 29 bits)
+    return [(x >> (29 * i)) & MASK for i in range(8)] + [x >> 232]
+
+
+def fits64(v):
+    assert -I64 <= v < I64, "64-bit accumulator overflow"
+    return v
+
+
+def fits32(v):
+    assert -I32 <= v < I32, "32-bit limb overflow"
+    return v & 0xFFFFFFFF
+
+
+# ---- the device primitives (p256_f29.hpp) -------------------------------------------------
+RED = ((3, 1 << 9), (6, 1 << 18), (7, 0x1FE00000), (8, 0x00FFFFFF))  # (column offset, multiplier)
+
+
+def mont(a, b, sq=False, addends=(), fold=False):
+    """f29_mul / f29_sqr / f29_mulsq_add (chain form): Mont(a b) + sum c v, columns checked."""
+    d = [fits32(2 * i32(x)) for x in a] if sq else None
+    m = [0] * 9
+    out = [0] * 9
+    acc = 0
+    for k in range(17):
+        terms = []
+        for i in range(9):
+            j = k - i
+            if sq:
+                if i < j <= 8:
+                    terms.append(i32(a[i]) * i32(d[j]))
+                if j == i:
+                    terms.append(i32(a[i]) * i32(a[i]))
+            elif 0 <= j <= 8:
+                terms.append(i32(a[i]) * i32(b[j]))
+        for off, c in RED:
+            if k >= off and k - off <= 8:
+                terms.append(i32(m[k - off]) * c)
+        if k >= 9:
+            for v, c in addends:
+                terms.append(i32(v[k - 9]) * c)
+        # any summation order (chain, ILP columns first, pipelined) stays below this
+        fits64(abs(acc) + sum(abs(t) for t in terms))
+        acc = fits64(acc + sum(terms))
+        if k < 9:
+            m[k] = acc & MASK
+        else:
+            out[k - 9] = acc & MASK
+        acc >>= 29
+    for v, c in addends:
+        acc += i32(v[8]) * c
+    top = fits32(acc)
+    if fold:
+        h = i32(top) >> 24
+        out[8] = (top - (h << 24)) & 0xFFFFFFFF
+        out[7] = fits32(out[7] + (h << 21))
+        out[6] = fits32(out[6] - (h << 18))
+        out[3] = fits32(out[3] - (h << 9))
+        out[0] = fits32(out[0] + h)
+    else:
+        out[8] = top
+    return out
+
+
+def mul_sub(a, b, c, d):  # f29_mul_sub: a b - c d, one reduction
+    nd = [fits32(-i32(x)) for x in d]
+    m = [0] * 9
+    out = [0] * 9
+    acc = 0
+    for k in range(17):
+        terms = []
+        for i in range(9):
+            j = k - i
+            if 0 <= j <= 8:
+                terms += [i32(a[i]) * i32(b[j]), i32(c[i]) * i32(nd[j])]
+        for off, cc in RED:
+            if k >= off and k - off <= 8:
+                terms.append(i32(m[k - off]) * cc)
+        fits64(abs(acc) + sum(abs(t) for t in terms))
+        acc = fits64(acc + sum(terms))
+        if k < 9:
+            m[k] = acc & MASK
+        else:
+            out[k - 9] = acc & MASK
+        acc >>= 29
+    out[8] = fits32(acc)
+    return out
+
+
+def add(a, b):
+    return [fits32(i32(x) + i32(y)) for x, y in zip(a, b)]
+
+
+def sub(a, b):
+    return [fits32(i32(x) - i32(y)) for x, y in zip(a, b)]
+
+
+def normalize(a):  # f29_normalize
+    c = [i32(a[i]) >> 29 for i in range(8)]
+    t = [a[0] & MASK] + [fits32((a[i] & MASK) + c[i - 1]) for i in range(1, 8)] + [0]
+    top = fits32(i32(a[8]) + c[7])
+    h = i32(top) >> 24
+    t[8] = top & 0x00FFFFFF
+    t[7] = fits32(i32(t[7]) + (h << 21))
+    t[6] = fits32(i32(t[6]) - (h << 18))
+    t[3] = fits32(i32(t[3]) - (h << 9))
+    t[0] = fits32(i32(t[0]) + h)
+    return t
+
+
+def triple(a):  # f29_triple (a product output)
+    t = [fits32(3 * i32(x)) for x in a]
+    c = [(t[i] & 0xFFFFFFFF) >> 29 for i in range(8)]
+    return [t[0] & MASK] + [fits32((t[i] & MASK) + c[i - 1]) for i in range(1, 8)] + [fits32(i32(t[8]) + c[7])]
+
+
+# ---- contracts ------------------------------------------------------------------------------
+def check_N(a):  # product output
+    assert all(0 <= a[i] <= MASK for i in range(8)) and abs(val(a)) < 1 << 258
+
+
+def check_Np(a):  # f29_normalize / fold output
+    assert all(-(1 << 26) < i32(a[i]) < (1 << 29) + (1 << 26) for i in range(8))
+    assert 0 <= i32(a[8]) < 1 << 24 and abs(val(a)) < 1 << 257
+
+
+def relimb(a, rng, lo, hi, top_lo=None, top_hi=None):
+    """The same value with limbs 0..7 moved at random inside [lo, hi) (limb 8 absorbs)."""
+    v = [i32(x) for x in a]
+    for i in range(8):
+        k = rng.choice((-2, -1, 0, 1, 2))
+        nv = v[i] + k * (1 << 29)
+        if lo <= nv < hi:
+            v[i] = nv
+            v[i + 1] -= k
+    if top_lo is not None and not top_lo <= v[8] < top_hi:
+        return a
+    return [x & 0xFFFFFFFF for x in v]
+
+
+def mont_of(x):
+    return to_limbs(x * R % P)
+
+
+def plain(a):
+    return val(a) * RINV % P
+
+
+# ---- the formulas (p256_f29.hpp p29_dbl_f, p29_add_aff_lean_f) ------------------------------
+def dbl_f(X, Y, Z):
+    y2 = add(Y, Y)
+    d = mont(Z, Z, sq=True)
+    g = mont(Y, Y, sq=True)
+    t0 = add(g, g)
+    b2 = mont(X, t0)
+    t1 = sub(X, d)
+    a1 = add(X, d)
+    a1 = mont(t1, a1)
+    al = triple(a1)
+    Z3 = mont(y2, Z)
+    X3 = mont(al, al, sq=True, addends=[(b2, -4)], fold=True)
+    l = mont(g, g, sq=True)
+    t0 = [fits32((i32(b) << 1) - i32(x)) for b, x in zip(b2, X3)]
+    Y3 = mont(al, t0, addends=[(l, -8)], fold=True)
+    for v in (d, g, b2, a1, Z3, l):
+        check_N(v)
+    check_Np(X3)
+    check_Np(Y3)
+    return X3, Y3, Z3
+
+
+def add_aff_f(X, Y, Z, x2, y2):
+    z1z1 = mont(Z, Z, sq=True)
+    u2 = mont(x2, z1z1)
+    t = mont(Z, z1z1)
+    h = sub(u2, X)
+    s2 = mont(y2, t)
+    hh = mont(h, h, sq=True)
+    rr = sub(s2, Y)
+    hhh = mont(hh, h)
+    V = mont(X, hh)
+    Z3 = mont(Z, h)
+    X3 = mont(rr, rr, sq=True, addends=[(hhh, -1), (V, -2)], fold=True)
+    t = sub(V, X3)
+    Y3 = mul_sub(rr, t, Y, hhh)
+    for v in (z1z1, u2, hh, hhh, V, Z3, Y3):
+        check_N(v)
+    check_Np(X3)
+    return X3, Y3, Z3
+
+
+def jac_to_affine(X, Y, Z):
+    x, y, z = plain(X), plain(Y), plain(Z)
+    zi = pow(z, -1, P)
+    return x * zi * zi % P, y * zi * zi * zi % P
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_ladder_bounds_and_values(seed):
+    """200 doublings and 50 mixed additions per seed, every operand re-limbed at the edges of
+    its contract before use: no int64 column or int32 limb overflows, every output meets its
+    stated contract, and the point matches the Python group law."""
+    rng = random.Random(seed)
+    G = pyref.G
+    k = rng.randrange(1, pyref.N)
+    pt = pyref.mul(k, G)
+    X, Y, Z = mont_of(pt[0]), mont_of(pt[1]), mont_of(1)
+    ref = pt
+    for step in range(250):
+        X = relimb(X, rng, -(1 << 26) + 1, (1 << 29) + (1 << 26), 0, 1 << 24)   # N'
+        Y = relimb(Y, rng, -(1 << 26) + 1, (1 << 29) + (1 << 26), 0, 1 << 24)   # N'
+        if step % 5 == 4:
+            q = pyref.mul(rng.randrange(1, pyref.N), G)
+            x2, y2 = mont_of(q[0]), mont_of(q[1])
+            if rng.random() < 0.5:  # a negated table entry: N+- limbs
+                y2 = [(-i32(w)) & 0xFFFFFFFF for w in y2]
+                q = (q[0], (-q[1]) % P)
+            X, Y, Z = add_aff_f(X, Y, Z, x2, y2)
+            ref = pyref.add(ref, q)
+            Y = relimb(Y, rng, -(1 << 29) + 1, 1 << 29)  # N+- (a difference of products)
+        else:
+            X, Y, Z = dbl_f(X, Y, Z)
+            ref = pyref.add(ref, ref)
+        assert jac_to_affine(X, Y, Z) == ref, step
+
+
+def test_extreme_operands():
+    """The doubling and the addition on operands whose every limb sits at the top of its
+    contract (the worst case of each column), values then reduced: no overflow anywhere."""
+    top = (1 << 29) + (1 << 26) - 1
+    Np_max = [top] * 8 + [(1 << 24) - 1]
+    N_max = [MASK] * 8 + [(1 << 24) - 1]
+    X3, Y3, Z3 = dbl_f(Np_max, Np_max, N_max)
+    add_aff_f(X3, Y3, Z3, N_max, [(-MASK) & 0xFFFFFFFF] * 8 + [0])

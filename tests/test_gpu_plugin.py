@@ -382,6 +382,14 @@ def test_verify_proposal_format_checked_during_verify(gpu, net, registered):
     rs = list(reqs)
     rs[5] = rs[5][:100]
     expect(rs, "malformed proposal payload")
+    # the walk's own length checks (with clients registered the key lookups trail the walk on a
+    # second thread and must stop at its last whole request): payload cut inside the last
+    # request, one trailing byte, a count one higher than the requests present
+    pl = plugin.encode_payload(reqs)
+    for raw in (pl[:-1], pl + b"\0", (len(reqs) + 1).to_bytes(4, "little") + pl[4:]):
+        with pytest.raises(plugin.VerifyError) as ei:
+            v.VerifyProposal(plugin.Proposal(raw, b"header", b"metadata", 3))
+        assert ei.value.code == plugin.EFORMAT and "malformed proposal payload" in str(ei.value)
     assert len(v.VerifyProposal(good)) == 1100
     with pytest.raises(plugin.VerifyError) as ei:
         v.VerifyProposal(enc(bad_sig))
