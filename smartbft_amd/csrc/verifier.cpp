@@ -1336,87 +1336,22 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
         }
         return 0;
     };
-    // With clients registered, the key lookups (a map probe per request, ~6 ns each) trail the
-    // walk on a warm parse-pool thread instead of following it: the walk publishes how far it
-    // has got, the second thread looks up every key the walk has passed. The walk is a chain of
-    // dependent loads, the lookups independent probes, so the lookups finish just after the walk
-    // (10k requests: walk + lookups 133 -> ~75 us). Without a free pool thread: one after the other.
     auto prepare_keyed = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& len) -> int {
-        const uint8_t* const P = p->payload;
-        const size_t L = p->payload_len;
-        uint32_t count = 0;
-        if (L >= 4) count = (uint32_t)P[0] | (uint32_t)P[1] << 8 | (uint32_t)P[2] << 16 | (uint32_t)P[3] << 24;
-        if (L < 4 || count > L / 4) return prepare(off, len);  // malformed: prepare's error path
-        off.resize(count);
-        len.resize(count);
-        kid.resize(count);
-        static const size_t kAhead = [] {  // SBFT_KEY_AHEAD: A/B only
-            const char* e = getenv("SBFT_KEY_AHEAD");
-            return e ? (size_t)std::max(1L, std::atol(e)) : (size_t)8;
-        }();
-        std::atomic<uint32_t> walked{0};
-        std::atomic<int> walk_state{0};  // 0 walking, 1 done, 2 malformed
-        std::atomic<bool> miss{false};
-        auto walker = [&] {
-            Reader r{P, L};
-            uint32_t c = 0;
-            bool good = r.u32(c);
-            for (uint32_t i = 0; good && i < count; ++i) {
-                uint32_t l;
-                const uint8_t* q;
-                __builtin_prefetch(P + r.pos + 2048);
-                if (!r.u32(l) || l < kMinRequest) {
-                    good = false;
-                    break;
-                }
-                const size_t at = r.pos;
-                if (!r.take(l, q)) {
-                    good = false;
-                    break;
-                }
-                off[i] = at;
-                len[i] = l - 64;
-                if ((i & 15) == 15) walked.store(i + 1, std::memory_order_release);
+        if (int prc = prepare(off, len)) return prc;
+        // each key's map slot prefetched kAhead lookups before it is read
+        constexpr size_t kAhead = 8;
+        const size_t n = off.size();
+        auto key = [&](size_t i) { return p->payload + off[i] + len[i] - 64; };
+        std::shared_lock<std::shared_mutex> g(v->clients_mu);
+        kid.resize(n);
+        for (size_t i = 0; i < n && i < kAhead; ++i) v->clients.prefetch(key(i));
+        for (size_t i = 0; i < n; ++i) {
+            if (i + kAhead < n) v->clients.prefetch(key(i + kAhead));
+            if (!(kid[i] = v->clients.find(key(i)))) {
+                kid.clear();
+                break;
             }
-            good = good && r.pos == L;
-            // a malformed payload publishes nothing past its last whole request
-            if (good) walked.store(count, std::memory_order_release);
-            walk_state.store(good ? 1 : 2, std::memory_order_release);
-        };
-        auto key = [&](size_t i) { return P + off[i] + len[i] - 64; };
-        auto looker = [&] {
-            size_t i = 0;
-            for (;;) {
-                const int st = walk_state.load(std::memory_order_acquire);
-                const size_t w = walked.load(std::memory_order_acquire);
-                if (st == 2) return;
-                for (; i < w; ++i) {
-                    if (i + kAhead < w) v->clients.prefetch(key(i + kAhead));
-                    if (!(kid[i] = v->clients.find(key(i)))) {
-                        miss.store(true, std::memory_order_relaxed);
-                        return;
-                    }
-                }
-                if (st == 1) return;  // w == count was read after st: every key is looked up
-                __builtin_ia32_pause();
-            }
-        };
-        std::shared_lock<std::shared_mutex> g(v->clients_mu);  // held for both threads' probes
-        if (!parse_pool().run(2, [&](int t) {
-                if (t == 0) walker();
-                else looker();
-            })) {
-            walker();
-            looker();
         }
-        if (walk_state.load() != 1) {
-            checked = true;  // the full parse would reject it too: no launch
-            reqs.clear();
-            kid.clear();
-            put_err(err, err_cap, "malformed proposal payload");
-            return fmt_rc = SBFT_V_EFORMAT;
-        }
-        if (miss.load()) kid.clear();
         return 0;
     };
     int info_rc = 0;
