@@ -390,9 +390,12 @@ __global__ __launch_bounds__(256) void p256_sinv_totals_kernel(uint32_t nb, sinv
 // doublings): W-bit windows, K = ceil(256 / W) of them, 2^(W-1) odd multiples each. The 33
 // radix-256 additions of an LDS table inside the ladder it replaced were 1.6 M instructions per
 // 1,000 verifies more. Wider windows trade HBM for additions (entries are gathered, never
-// scanned): W = 16: 17 additions, 42 MB; W = 20: 14, 0.55 GB; W = 24: 12, 7.4 GB.
+// scanned): W = 16: 17 additions, 42 MB; W = 20: 14, 0.55 GB; W = 22: 13, 2.0 GB (the default
+// since round 3, built at init in ~0.44 s: once the products with addends had made the
+// doublings cheaper, the 4 additions saved were worth 0.9% of the throughput kernel,
+// profiles/r03u_gcomb22_ab.txt); W = 24: 12, 7.4 GB.
 #ifndef SBFT_GCOMB_W
-#define SBFT_GCOMB_W 16
+#define SBFT_GCOMB_W 22
 #endif
 #define SBFT_GCOMB_WINDOWS ((256 + SBFT_GCOMB_W - 1) / SBFT_GCOMB_W)
 #define SBFT_GCOMB_ENTRIES (1u << (SBFT_GCOMB_W - 1))  // odd digits 1, 3, ..., 2^W - 1
@@ -970,7 +973,7 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
 //     run the same instruction stream on the comb: their accumulator starts at the first comb
 //     entry and takes one comb entry at each of the first 16 digits' mixed additions (their
 //     doublings and later additions are discarded by a select). One lean Jacobian addition of
-//     the two halves ends it: the 17 comb additions leave the critical path.
+//     the two halves ends it: the K + 1 comb additions leave the critical path.
 // Setup (checks, Q table, scalars) and the final comparison run redundantly on all lanes of a
 // tuple. The Q table lives in LDS (one copy per tuple). One wavefront per workgroup spreads a
 // small batch over as many CUs as possible.
@@ -1158,7 +1161,7 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
     }
     acc.z = f29_const(C29_ONE);
     if (neg2) f29_neg(acc.y, acc.y);
-    // quad: the tuple's 17 comb points (signs applied) staged in LDS over the divstep table,
+    // quad: the tuple's K + 1 comb points (signs applied) staged in LDS over the divstep table,
     // which the inversions are done with: [entry][x limbs, y limbs][tuple]
     u32* const ctab = dtab;
     static_assert(!kQuad || (kGK + 1) * 18 * kTuples <= SBFT_DIVSTEP5_WORDS, "comb points fit the divstep table");

@@ -6,8 +6,9 @@ Run from the repo root in the build container:  python tests/golden/gen_crafted.
 Each tuple is a signature whose scalars u1 = e/s, u2 = r/s make a lean point addition of the
 engine's verify ladders meet acc == +-addend (p256_f29.hpp add_aff_fix, p256_verify.hip):
   ladder_last : the last addition of the u2 Q ladder (u2 = n - 2|d| or 2|d|: P + P);
-  comb_dbl_j  : comb step j (0..16) of u1 G on top of u2 Q meets acc == entry (P + P);
-  comb_inf_j  : ... meets acc == -entry (P + (-P)); at j = 16 that is R = infinity.
+  comb_dbl_j  : comb step j (0..K) of u1 G on top of u2 Q meets acc == entry (P + P);
+  comb_inf_j  : ... meets acc == -entry (P + (-P)); at j = K that is R = infinity.
+(K = ceil(256 / W) windows of W = SBFT_GCOMB_W bits: the engine's comb, 22-bit windows.)
 The key is Q = q G with q chosen so that u2 q + (the comb's partial sum) = +-(the entry), which
 any client can do for its own request. Verdicts are the oracle's (oracle/p256_oracle.c, Go
 crypto/ecdsa.Verify restated), cross-checked with the pure-Python restatement (oracle/pyref.py).
@@ -31,8 +32,9 @@ import oracle  # noqa: E402
 from oracle import pyref  # noqa: E402
 
 N = oracle.N
-GW = 16  # the comb's window bits (SBFT_GCOMB_W)
-KG = 256 // GW
+GW = 22  # the comb's window bits (SBFT_GCOMB_W, p256_verify.hip)
+KG = (256 + GW - 1) // GW
+TOP = 1 << (GW * KG)  # the comb's constant term 2^(W K) (table[K][0] = 2^(W K) G)
 
 
 def _b(x: int) -> bytes:
@@ -53,20 +55,20 @@ def craft(u1: int, u2: int, q: int, rng):
 
 def comb_digits(u1: int):
     """The comb's recoding of u1 (comb_add_u1g): sign s1 and the odd digits of u1' with
-    u1' = sum d_i 2^(16 i) + 2^256, u1' = u1 (odd) or n - u1 (even u1, negated base)."""
+    u1' = sum d_i 2^(W i) + 2^(W K), u1' = u1 (odd) or n - u1 (even u1, negated base)."""
     neg = u1 % 2 == 0
     u = N - u1 if neg else u1
     m = (1 << GW) - 1
     d = [2 * ((u >> (GW * i + 1)) & m) - m for i in range(KG)]
-    assert sum(di << (GW * i) for i, di in enumerate(d)) + (1 << 256) == u
+    assert sum(di << (GW * i) for i, di in enumerate(d)) + TOP == u
     return (-1 if neg else 1), d
 
 
 def comb_collision(u1: int, u2: int, j: int, kind: str):
-    """q such that acc == +-entry at comb step j (0..16) for these scalars (None if q = 0)."""
+    """q such that acc == +-entry at comb step j (0..K) for these scalars (None if q = 0)."""
     s1, d = comb_digits(u1)
     partial = sum(d[i] << (GW * i) for i in range(min(j, KG)))
-    entry = s1 * (d[j] << (GW * j) if j < KG else 1 << 256)
+    entry = s1 * (d[j] << (GW * j) if j < KG else TOP)
     target = (entry if kind == "dbl" else -entry) - s1 * partial
     q = target * pow(u2, -1, N) % N
     return q or None

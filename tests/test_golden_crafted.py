@@ -25,9 +25,13 @@ def test_crafted_fixture_verdicts():
     cols = [np.ascontiguousarray(raw[:, 32 * k:32 * k + 32]) for k in range(5)]
     assert np.array_equal(oracle.verify_batch(*cols), raw[:, 160])
     tags = [names[i] for i in raw[:, 161]]
-    assert len(tags) > 100 and {t.rsplit("_", 1)[0] for t in tags} == {"ladder_last", "comb_dbl", "comb_inf"}
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import gen_crafted
+    # 16 ladder tuples + 3 x 2 x (K + 1) comb tuples (K = 12 windows of 22 bits), minus q = 0 / r = 0
+    assert len(tags) > 80 and {t.rsplit("_", 1)[0] for t in tags} == {"ladder_last", "comb_dbl", "comb_inf"}
     for t, w in zip(tags, raw[:, 160]):
         if t.startswith(("comb_dbl", "ladder_last")):
             assert w == 1, t
-        if t == "comb_inf_16":
+        if t == f"comb_inf_{gen_crafted.KG}":  # the last step: R = infinity
             assert w == 0, t

@@ -2,7 +2,7 @@
 signatures whose scalars make a lean addition of the verify ladders meet acc == +-addend, at
 every place one can (p256_f29.hpp add_aff_fix, p256_verify.hip):
   - the last addition of the u2 Q ladder (u2 = n - 2|d|: P + P);
-  - each of the 17 comb additions of u1 G, which land on top of u2 Q: with a key Q = q G of
+  - each of the 13 comb additions of u1 G (12 windows of 22 bits + 2^264 G), which land on top of u2 Q: with a key Q = q G of
     known q the attacker picks q so that u2 q + (the comb's partial sum) = +-(the next entry),
     giving a doubling (P + P) or the point at infinity (P + (-P)) at that step; at the last
     entry the infinity case is R = infinity itself.
@@ -24,7 +24,6 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 N = oracle.N
-KG = 16
 
 
 def _b(x: int) -> bytes:
