@@ -310,10 +310,13 @@ struct Slot {
     std::mutex gcomb_mu;
     void* gcomb = nullptr;
     bool gcomb_ready = false;
+    Slot* gcomb_owner = nullptr;  // the device's first slot, whose table every slot of it reads
 
-    // The comb table, building it (synchronously, on this slot's stream) the first time.
-    // Returns nullptr on failure.
+    // The comb table, building it (synchronously, on the owner slot's stream) the first time.
+    // The table is read-only once built, so the slots of one device (slots_per_device > 1)
+    // share one copy (2.0 GB at 22-bit windows). Returns nullptr on failure.
     const void* gcomb_table() {
+        if (gcomb_owner && gcomb_owner != this) return gcomb_owner->gcomb_table();
         std::lock_guard<std::mutex> g(gcomb_mu);
         if (gcomb_ready) return gcomb;
         const size_t bytes = sbft_gcomb_table_bytes();
@@ -597,15 +600,18 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     }
     for (int d = 0; d < ndev && d < 32; ++d) {
         if (!(mask & (1u << d))) continue;
+        Slot* first = nullptr;
         for (uint32_t k = 0; k < spd; ++k) {
             auto* s = new Slot();
             s->device = d;
+            s->gcomb_owner = first ? first : s;
             if (hipSetDevice(d) != hipSuccess ||
                 hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
                 delete s;
                 break;
             }
             ctx->slots.push_back(s);
+            if (!first) first = s;
         }
     }
     if (ctx->slots.empty()) {
@@ -634,6 +640,15 @@ void sbft_gv_destroy(sbft_gv_ctx* ctx) {
     uint64_t nl;
     double ms;
     (void)sbft_gv_kernel_time(ctx, &nl, &ms);  // releases pending timing events
+    // drain every device first: a slot's launches (on its streams or a caller's) may read
+    // tables another slot of the device owns (the shared G comb)
+    uint32_t drained = 0;
+    for (Slot* s : ctx->slots)
+        if (!(drained & (1u << s->device))) {
+            drained |= 1u << s->device;
+            (void)hipSetDevice(s->device);
+            (void)hipDeviceSynchronize();
+        }
     for (Slot* s : ctx->slots) {
         (void)hipSetDevice(s->device);
         if (s->stream) (void)hipStreamSynchronize(s->stream);
