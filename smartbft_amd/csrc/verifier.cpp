@@ -1458,9 +1458,14 @@ static int consenter_coalesced(sbft_verifier* v, const sbft_signature* s, const 
             }
         }
     }
+    // Pre-wake (followers yield-spin through the launch) is off by default: it doubles the
+    // fan-out's CPU time (7.2-7.5 against 3.0-3.7 ms per 66-caller decision) and a job under a
+    // CPU quota (the GPU box: cpu.max 16 CPUs, 256 in the affinity mask) is then throttled for
+    // the rest of a quota period, a 2.7-48 ms outlier every few hundred decisions; without it
+    // p99 0.30 ms, max 0.35-0.78 ms, p50 the same (profiles/r03w_cs_tail.txt).
     static const bool prewake = [] {
         const char* e = getenv("SBFT_CS_PREWAKE");
-        return !e || std::strcmp(e, "0") != 0;
+        return e && std::strcmp(e, "1") == 0;
     }();
     if (!leader) {
         if (prewake) {

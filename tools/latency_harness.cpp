@@ -117,6 +117,27 @@ static std::vector<double> fan_out(size_t n, int rounds, const std::function<voi
     return out;
 }
 
+// The job's cgroup CPU accounting (cgroup v2 cpu.stat; zeros where absent): a quota-limited
+// job whose threads spin can be throttled for the rest of the quota period, which shows up as
+// multi-millisecond outliers in the fan-out latencies.
+struct CgroupCpu {
+    long long usage_us = 0, nr_throttled = 0, throttled_us = 0;
+};
+static CgroupCpu cgroup_cpu() {
+    CgroupCpu c;
+    FILE* f = std::fopen("/sys/fs/cgroup/cpu.stat", "r");
+    if (!f) return c;
+    char key[64];
+    long long val;
+    while (std::fscanf(f, "%63s %lld", key, &val) == 2) {
+        if (!std::strcmp(key, "usage_usec")) c.usage_us = val;
+        else if (!std::strcmp(key, "nr_throttled")) c.nr_throttled = val;
+        else if (!std::strcmp(key, "throttled_usec")) c.throttled_us = val;
+    }
+    std::fclose(f);
+    return c;
+}
+
 static void priv_of(uint64_t tag, uint8_t out[32]) {
     // deterministic private keys in [1, n-1]: SHA-256(tag) with the top bit cleared
     uint8_t in[16] = "sbft-harness";
@@ -238,13 +259,19 @@ static int quorum_gpu(int callers, int decisions, int cmax, int cwait) {
     fan_out(callers, 5, run);  // warm-up: tables, staging, memo
     uint64_t l0, c0, l1, c1;
     sbft_verifier_consenter_stats(v, &l0, &c0);
+    const CgroupCpu cg0 = cgroup_cpu();
     auto t = fan_out(callers, decisions, run);
+    const CgroupCpu cg1 = cgroup_cpu();
     sbft_verifier_consenter_stats(v, &l1, &c1);
+    int over1ms = 0;
+    for (double us : t) over1ms += us > 1000.0;
     std::printf("{\"mode\": \"quorum-gpu\", \"callers\": %d, \"decisions\": %d, \"coalesce_max\": %d, "
-                "\"coalesce_wait_us\": %d, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"launches_per_decision\": %.2f, "
-                "\"wrong_verdicts\": %d}\n",
-                callers, decisions, cmax, cwait, pct(t, 50) / 1e3, pct(t, 99) / 1e3,
-                (double)(l1 - l0) / decisions, wrong.load());
+                "\"coalesce_wait_us\": %d, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f, "
+                "\"decisions_over_1ms\": %d, \"launches_per_decision\": %.2f, \"cpu_ms_per_decision\": %.3f, "
+                "\"cgroup_throttled\": %lld, \"cgroup_throttled_ms\": %.3f, \"wrong_verdicts\": %d}\n",
+                callers, decisions, cmax, cwait, pct(t, 50) / 1e3, pct(t, 99) / 1e3, pct(t, 100) / 1e3, over1ms,
+                (double)(l1 - l0) / decisions, (cg1.usage_us - cg0.usage_us) / 1e3 / decisions,
+                cg1.nr_throttled - cg0.nr_throttled, (cg1.throttled_us - cg0.throttled_us) / 1e3, wrong.load());
     for (auto* s : signers) sbft_signer_free(s);
     sbft_verifier_free(v);
     sbft_gv_destroy(ctx);
