@@ -330,6 +330,69 @@ SBFT_DEV void f29_mulsq_add(f29& r, const f29& a, const f29& b, const f29* const
     for (int t = 0; t < NA; ++t) acc = smad(v[t]->v[8], c[t], acc);
     f29_fold_top(r, (u32)acc, ~0u);
 }
+// Mont(a b - c^2) in one pass (chain form): the square's terms go into the same column sums
+// with their signs flipped, c's cross terms as c_i (-2 c_j) and its diagonal as c_i (-c_i), so
+// c^2 costs 45 mads and no reduction of its own. nc = -c, nc2 = -2c (limbs), supplied by the
+// caller. Column contract: |a_i b_j| < 2^58.2 (9 of them), |c_i 2 c_j| < 2^59 (4 cross + 1
+// diagonal per column), reduction terms < 2^58.1: < 2^62.4 with the carry, under 2^63
+// (tests/test_f29_bounds.py checks the sums). Output N (limbs 0..7 in [0, 2^29), signed top,
+// |r| < 2^258 for |a b - c^2| < 2^518).
+SBFT_DEV void f29_mul_sqsub(f29& r, const f29& a, const f29& b, const f29& c, const f29& nc, const f29& nc2) {
+    const f29_red K = f29_red_consts();
+    u32 m[9];
+    i64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const int j = k - i;
+            if (j >= 0 && j <= 8) acc = smad(a.v[i], b.v[j], acc);
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const int j = k - i;
+            if (j > i && j <= 8) acc = smad(c.v[i], nc2.v[j], acc);
+        }
+        if ((k & 1) == 0 && (k >> 1) <= 8) acc = smad(c.v[k >> 1], nc.v[k >> 1], acc);
+        if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], K.c9, acc);
+        if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], K.c18, acc);
+        if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], K.c7, acc);
+        if (k >= 8 && k - 8 <= 8) acc = smad(m[k - 8], K.c8, acc);
+        if (k < 9) m[k] = lo29(acc);
+        else r.v[k - 9] = lo29(acc);
+        acc = sar29(acc);
+    }
+    r.v[8] = (u32)acc;
+}
+
+// alpha/2 = 3 a' / 2 (mod p) for a product output a' (limbs 0..7 in [0, 2^29), |a'| < 2^256.6):
+// s = a' + (a' odd ? p : 0) is even (the value's parity is limb 0's), u = 3 s limb by limb
+// (< 2^31.6, unsigned), one carry pass (limbs [0, 2^29 + 5)), then the halving: limb i takes
+// u_i >> 1 plus limb i+1's low bit at bit 28 (u_0 is even). Out: limbs 0..7 in [0, 2^29 + 3),
+// |out| < 1.5 (2^256.6 + p) < 2^258.1 -- f29_triple's contract.
+SBFT_DEV void f29_triple_half(f29& r, const f29& a) {
+    const u32 odd = 0u - (a.v[0] & 1u);
+    constexpr u32 P29[9] = {0x1fffffffu, 0x1fffffffu, 0x1fffffffu, 0x000001ffu, 0u, 0u, 0x00040000u, 0x1fe00000u,
+                            0x00ffffffu};
+    u32 t[9], c[8];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t[i] = (a.v[i] + (P29[i] & odd)) * 3u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = t[i] >> 29;  // 3 s_i < 2^31.6: carry 0..5
+    u32 w[9];
+    w[0] = t[0] & F29_MASK;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) w[i] = (t[i] & F29_MASK) + c[i - 1];
+    w[8] = t[8] + c[7];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = (w[i] >> 1) + ((w[i + 1] & 1u) << 28);
+    r.v[8] = (u32)((i32)w[8] >> 1);
+#if !defined(SBFT_NO_OPAQUE_LIMBS) && !defined(SBFT_NO_OPAQUE_NORM)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) asm("" : "+v"(r.v[i]));
+#endif
+}
+
 // ILP form (lane pairs: one product per lane per step; see f29_mulsq_ilp below), per-lane
 // constants c (VGPRs) and fold mask.
 template <bool SQ, int NA>
@@ -718,15 +781,50 @@ SBFT_DEV void p29_dbl_f(jp29& r, const jp29& p) {
     r.x = x3;
 }
 
+// p29_dbl_f on the representative scaled by 1/2 ((X, Y, Z) ~ (X/4, Y/8, Z/2), the same point):
+//   d = Z^2, g = Y^2, b = X g, a' = (X - d)(X + d), h = 3 a' / 2 (f29_triple_half),
+//   X3 = h^2 - 2 b, Y3 = h (b - X3) - g^2, Z3 = Y Z
+// The 8 of dbl-2001-b's 8 gamma^2 is gone, so g^2 joins Y3's product as negated column terms
+// (f29_mul_sqsub: 45 mads, no reduction of its own); the halving costs ~40 32-bit ops. 765
+// mads per doubling against 810. In: X in N or N', Y in N' or N+-, Z in N. Out: X3 in N', Y3
+// and Z3 in N (Y3 signed top, |Y3| < 2^258). Z = 0 maps to Z3 = 0.
+SBFT_DEV void p29_dbl_h(jp29& r, const jp29& p) {
+    f29 d, g, t0, t1, a1, al, b, x3, ng;
+    f29_add(t0, p.y, p.y);           // 2Y < 2^30.2
+    f29_sqr(d, p.z);                 // 2^29.2^2
+    f29_sqr_d(g, p.y, t0);           // gamma (N)
+    f29_mul(b, p.x, g);              // beta = X gamma (2^29.2 x 2^29)
+    f29_sub(t1, p.x, d);             // |.| < 2^29.2
+    f29_add(a1, p.x, d);             // < 2^30.1
+    f29_mul(a1, t1, a1);             // a' (2^29.2 x 2^30.1)
+    f29_triple_half(al, a1);         // alpha / 2 (limbs < 2^29 + 3, |.| < 2^258.1)
+    f29_mul(r.z, p.y, p.z);          // Z3 = Y Z
+    {
+        const f29* const v[1] = {&b};
+        const u32 c[1] = {f29_kconst(-2)};
+        f29_mulsq_add<true, 1>(x3, al, al, v, c);  // X3 = (alpha/2)^2 - 2 beta: N'
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        t1.v[i] = b.v[i] - x3.v[i];  // (-2^29.2, 2^29 + 2^25)
+        ng.v[i] = 0u - g.v[i];
+        t0.v[i] = ng.v[i] << 1;      // -2 gamma
+    }
+    f29_mul_sqsub(r.y, al, t1, g, ng, t0);  // Y3 = (alpha/2)(beta - X3) - gamma^2: N
+    r.x = x3;
+}
+
 #ifndef SBFT_F29_IL
 #define SBFT_F29_IL 6
 #endif
 // SBFT_F29_IL bit 0/1/2: interleaved form of the doubling / Jacobian addition / mixed addition
 #ifndef SBFT_DBL_FORM
-#define SBFT_DBL_FORM 2  // 0: 6M + 2S (p29_dbl_s / _i), 1: 4M + 4S (p29_dbl_b), 2: p29_dbl_b fused (p29_dbl_f)
+#define SBFT_DBL_FORM 3  // 0: 6M + 2S (p29_dbl_s / _i), 1: 4M + 4S (p29_dbl_b), 2: p29_dbl_b fused (p29_dbl_f),
+                         // 3: halved representative (p29_dbl_h)
 #endif
 SBFT_DEV void p29_dbl(jp29& r, const jp29& p) {
-    if (SBFT_DBL_FORM == 2) p29_dbl_f(r, p);
+    if (SBFT_DBL_FORM == 3) p29_dbl_h(r, p);
+    else if (SBFT_DBL_FORM == 2) p29_dbl_f(r, p);
     else if (SBFT_DBL_FORM == 1) p29_dbl_b(r, p);
     else if (SBFT_F29_IL & 1) p29_dbl_i(r, p);
     else p29_dbl_s(r, p);

@@ -150,6 +150,50 @@ def triple(a):  # f29_triple (a product output)
     return [t[0] & MASK] + [fits32((t[i] & MASK) + c[i - 1]) for i in range(1, 8)] + [fits32(i32(t[8]) + c[7])]
 
 
+def mul_sqsub(a, b, c):  # f29_mul_sqsub: Mont(a b - c^2), c's terms negated in the same columns
+    nc = [fits32(-i32(x)) for x in c]
+    nc2 = [fits32(-2 * i32(x)) for x in c]
+    m = [0] * 9
+    out = [0] * 9
+    acc = 0
+    for k in range(17):
+        terms = []
+        for i in range(9):
+            j = k - i
+            if 0 <= j <= 8:
+                terms.append(i32(a[i]) * i32(b[j]))
+            if i < j <= 8:
+                terms.append(i32(c[i]) * i32(nc2[j]))
+            if j == i:
+                terms.append(i32(c[i]) * i32(nc[i]))
+        for off, cc in RED:
+            if k >= off and k - off <= 8:
+                terms.append(i32(m[k - off]) * cc)
+        fits64(abs(acc) + sum(abs(t) for t in terms))
+        acc = fits64(acc + sum(terms))
+        if k < 9:
+            m[k] = acc & MASK
+        else:
+            out[k - 9] = acc & MASK
+        acc >>= 29
+    out[8] = fits32(acc)
+    return out
+
+
+P29 = [0x1fffffff, 0x1fffffff, 0x1fffffff, 0x000001ff, 0, 0, 0x00040000, 0x1fe00000, 0x00ffffff]
+
+
+def triple_half(a):  # f29_triple_half: 3 a / 2 mod p for a product output
+    odd = a[0] & 1
+    t = [(a[i] + (P29[i] if odd else 0)) * 3 for i in range(8)]
+    assert all(0 <= x < 1 << 32 for x in t), "32-bit limb overflow"
+    t.append(fits32(3 * (i32(a[8]) + (P29[8] if odd else 0))))
+    c = [(t[i] & 0xFFFFFFFF) >> 29 for i in range(8)]
+    w = [t[0] & MASK] + [fits32((t[i] & MASK) + c[i - 1]) for i in range(1, 8)] + [fits32(i32(t[8]) + c[7])]
+    assert w[0] & 1 == 0
+    return [fits32((w[i] >> 1) + ((w[i + 1] & 1) << 28)) for i in range(8)] + [fits32(i32(w[8]) >> 1)]
+
+
 # ---- contracts ------------------------------------------------------------------------------
 def check_N(a):  # product output
     assert all(0 <= a[i] <= MASK for i in range(8)) and abs(val(a)) < 1 << 258
@@ -205,6 +249,25 @@ def dbl_f(X, Y, Z):
     return X3, Y3, Z3
 
 
+def dbl_h(X, Y, Z):  # p29_dbl_h: the representative scaled by 1/2
+    d = mont(Z, Z, sq=True)
+    g = mont(Y, Y, sq=True)
+    b = mont(X, g)
+    t1 = sub(X, d)
+    a1 = add(X, d)
+    a1 = mont(t1, a1)
+    al = triple_half(a1)
+    assert all(0 <= al[i] < (1 << 29) + 3 for i in range(8)) and abs(val(al)) < 2 ** 258.1
+    Z3 = mont(Y, Z)
+    X3 = mont(al, al, sq=True, addends=[(b, -2)], fold=True)
+    t = sub(b, X3)
+    Y3 = mul_sqsub(al, t, g)
+    for v in (d, g, b, a1, Z3, Y3):
+        check_N(v)
+    check_Np(X3)
+    return X3, Y3, Z3
+
+
 def add_aff_f(X, Y, Z, x2, y2):
     z1z1 = mont(Z, Z, sq=True)
     u2 = mont(x2, z1z1)
@@ -231,8 +294,9 @@ def jac_to_affine(X, Y, Z):
     return x * zi * zi % P, y * zi * zi * zi % P
 
 
+@pytest.mark.parametrize("dbl", ["f", "h"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_ladder_bounds_and_values(seed):
+def test_ladder_bounds_and_values(seed, dbl):
     """200 doublings and 50 mixed additions per seed, every operand re-limbed at the edges of
     its contract before use: no int64 column or int32 limb overflows, every output meets its
     stated contract, and the point matches the Python group law."""
@@ -255,7 +319,9 @@ def test_ladder_bounds_and_values(seed):
             ref = pyref.add(ref, q)
             Y = relimb(Y, rng, -(1 << 29) + 1, 1 << 29)  # N+- (a difference of products)
         else:
-            X, Y, Z = dbl_f(X, Y, Z)
+            if dbl == "h":
+                Y = relimb(Y, rng, -(1 << 29) + 1, 1 << 29)  # N+- (dbl_h's own Y3 is N)
+            X, Y, Z = (dbl_h if dbl == "h" else dbl_f)(X, Y, Z)
             ref = pyref.add(ref, ref)
         assert jac_to_affine(X, Y, Z) == ref, step
 
@@ -267,4 +333,8 @@ def test_extreme_operands():
     Np_max = [top] * 8 + [(1 << 24) - 1]
     N_max = [MASK] * 8 + [(1 << 24) - 1]
     X3, Y3, Z3 = dbl_f(Np_max, Np_max, N_max)
+    add_aff_f(X3, Y3, Z3, N_max, [(-MASK) & 0xFFFFFFFF] * 8 + [0])
+    X3, Y3, Z3 = dbl_h(Np_max, Np_max, N_max)
+    dbl_h(X3, Y3, Z3)
+    dbl_h(Np_max, [(-MASK) & 0xFFFFFFFF] * 8 + [(1 << 24) - 1], N_max)
     add_aff_f(X3, Y3, Z3, N_max, [(-MASK) & 0xFFFFFFFF] * 8 + [0])
