@@ -231,6 +231,9 @@ SBFT_DEV void f29_sqr2(f29& r0, const f29& a0, f29& r1, const f29& a1) {
 // Contract (f29_mul's, with both products in the column): 9 (A B + C D) + 2^60 < 2^63 for the
 // limb bounds (A B + C D <= 2^59.6; the uses have 2^29.2 x 2^29.2 + 2^29.2 x 2^29 = 2^59.3), and
 // |a b - c d| < 2^518 so that the output is normal (N).
+#ifndef SBFT_MULSUB_CHAIN
+#define SBFT_MULSUB_CHAIN 0  // 1: both products on one accumulator (no 64-bit add per column)
+#endif
 SBFT_DEV void f29_mul_sub(f29& r, const f29& a, const f29& b, const f29& c, const f29& d) {
     const f29_red K = f29_red_consts();
     u32 nd[9];
@@ -246,9 +249,10 @@ SBFT_DEV void f29_mul_sub(f29& r, const f29& a, const f29& b, const f29& c, cons
             const int j = k - i;
             if (j < 0 || j > 8) continue;
             acc = smad(a.v[i], b.v[j], acc);
-            acc1 = smad(c.v[i], nd[j], acc1);
+            if (SBFT_MULSUB_CHAIN) acc = smad(c.v[i], nd[j], acc);
+            else acc1 = smad(c.v[i], nd[j], acc1);
         }
-        acc += acc1;
+        if (!SBFT_MULSUB_CHAIN) acc += acc1;
         if (k >= 3 && k - 3 <= 8) acc = smad(m[k - 3], K.c9, acc);
         if (k >= 6 && k - 6 <= 8) acc = smad(m[k - 6], K.c18, acc);
         if (k >= 7 && k - 7 <= 8) acc = smad(m[k - 7], K.c7, acc);
