@@ -98,7 +98,9 @@ def _blobs(items: list[bytes], keep: list):
 
 def _infos(buf, count: int) -> list[RequestInfo]:
     parts = buf.raw.split(b"\0", 2 * count)  # bounded: the rest of the buffer is unused
-    return [RequestInfo(parts[2 * i].decode(), parts[2 * i + 1].decode()) for i in range(count)]
+    # ids are arbitrary bytes (Go strings): bytes that are not UTF-8 survive as surrogate escapes
+    return [RequestInfo(parts[2 * i].decode("utf-8", "surrogateescape"),
+                        parts[2 * i + 1].decode("utf-8", "surrogateescape")) for i in range(count)]
 
 
 _L = None
