@@ -191,3 +191,72 @@ def test_batch_entry_points_need_engine():
     with pytest.raises(plugin.VerifyError) as ei:
         v.VerifyRequests([req])
     assert ei.value.code == -2  # SBFT_GV_ENODEV
+
+
+def _ref_request(r: bytes):
+    """verifier.cpp parse_request restated: (client_id, id, key byte 0) or None."""
+    def u(at, n):
+        return int.from_bytes(r[at:at + n], "little") if at + n <= len(r) else None
+    if r[:4] != b"SBR1":
+        return None
+    a = u(4, 2)
+    if a is None or 6 + a > len(r):
+        return None
+    q = 6 + a
+    b = u(q, 2)
+    if b is None or q + 2 + b > len(r):
+        return None
+    cid, rid, q = r[6:6 + a], r[q + 2:q + 2 + b], q + 2 + b
+    c = u(q, 4)
+    if c is None or q + 4 + c + 129 != len(r) or b"\0" in cid or b"\0" in rid:
+        return None
+    return cid, rid, r[q + 4 + c]
+
+
+def _ref_msg(m: bytes):
+    """verifier.cpp parse_msg restated: the aux bytes or None."""
+    if m[:4] != b"SBC1" or len(m) < 6:
+        return None
+    a = int.from_bytes(m[4:6], "little")
+    if 6 + a + 4 > len(m):
+        return None
+    b = int.from_bytes(m[6 + a:10 + a], "little")
+    return m[10 + a:] if 10 + a + b == len(m) else None
+
+
+def test_random_request_and_message_mutations():
+    """Differential fuzz of the single-request and consenter-message formats: mutated requests
+    are EFORMAT in the batch form exactly when the restated format (or the SEC1 key prefix)
+    rejects them, and AuxiliaryData returns exactly the restated aux bytes."""
+    import numpy as np
+    rng = np.random.default_rng(23)
+    v = plugin.Verifier(None)
+    base = _fake_request("client-7", "req-19", b"payload bytes")
+    base = base[:-129] + b"\x04" + base[-128:]
+    aux = b"prepares-from"
+    msg = b"SBC1" + (32).to_bytes(2, "little") + b"d" * 32 + len(aux).to_bytes(4, "little") + aux
+    reqs, msgs = [], []
+    for n in range(400):
+        for src, dst in ((base, reqs), (msg, msgs)):
+            b = bytearray(src)
+            for _ in range(int(rng.integers(1, 3))):
+                at = int(rng.integers(0, len(b)))
+                k = int(rng.integers(0, 3))
+                if k == 0:
+                    b[at] ^= 1 << int(rng.integers(0, 8))
+                elif k == 1:
+                    del b[at]
+                else:
+                    b.insert(at, int(rng.integers(0, 256)))
+            dst.append(bytes(b))
+    for r in reqs:
+        want = _ref_request(r)
+        try:  # a well-formed request needs the engine: the parse-only verifier raises ENODEV
+            code = v.VerifyRequests([r])[0]
+        except plugin.VerifyError as e:
+            code = e.code
+        assert (code == plugin.EFORMAT) == (want is None or want[2] != 0x04)
+        assert code in (plugin.EFORMAT, -2)
+    for m in msgs:
+        assert plugin.AuxiliaryData(m) == _ref_msg(m)
+    v.close()
