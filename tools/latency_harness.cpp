@@ -22,6 +22,7 @@
 //       workers (one thread per vote when THREADS >= CALLERS), SHA-256(Msg) + ECDSA_do_verify
 //       each, keys pre-materialised.
 //   proposal-cpu REQUESTS DECISIONS THREADS
+//   proposal-gpu REQUESTS DECISIONS
 //       VerifyProposal (view.go:555) on the CPU: REQUESTS signed requests (distinct keys,
 //       64-256 B bodies) verified by THREADS workers pulling indices from an atomic counter:
 //       SHA-256(body) + ECDSA_do_verify each, keys pre-materialised (favours the CPU: a real
@@ -557,9 +558,80 @@ static int proposal_cpu(int requests, int decisions, int threads) {
     return 0;
 }
 
+// proposal-gpu REQUESTS DECISIONS: VerifyProposal through the C ABI on proposals of REQUESTS
+// signed requests (distinct client keys), each decision rotating over: the honest proposal
+// (generic path), one with a bad signature at a varying index, one truncated (malformed), and
+// the honest one again with every client registered (keyed path). Checks every verdict, count
+// and reported index; reports the honest generic call's p50/p99.
+static int proposal_gpu(int requests, int decisions) {
+    sbft_gv_ctx* ctx = nullptr;
+    if (sbft_gv_init(nullptr, &ctx)) {
+        std::fprintf(stderr, "no GPU\n");
+        return 1;
+    }
+    sbft_verifier* gen = sbft_verifier_new(ctx, 0);
+    sbft_verifier* reg = sbft_verifier_new(ctx, 0);
+    std::vector<uint8_t> payload(4), keys;
+    std::vector<size_t> sig_at;  // offset of each request's signature inside payload
+    uint32_t cnt = (uint32_t)requests;
+    std::memcpy(payload.data(), &cnt, 4);
+    for (int i = 0; i < requests; ++i) {
+        uint8_t d[32], pub[65], buf[1024];
+        priv_of(50'000 + i, d);
+        sbft_signer* c = sbft_signer_new(ctx, 1, d);
+        sbft_signer_public_key(c, pub);
+        keys.insert(keys.end(), pub, pub + 65);
+        std::string body(64 + i % 193, (char)('a' + i % 26));
+        const std::string cid = "client" + std::to_string(i), rid = "tx" + std::to_string(i);
+        const int64_t len = sbft_make_request(c, cid.c_str(), rid.c_str(), (const uint8_t*)body.data(), body.size(), buf,
+                                              sizeof buf);
+        sbft_signer_free(c);
+        if (len <= 0) return 3;
+        const uint32_t l = (uint32_t)len;
+        payload.insert(payload.end(), (const uint8_t*)&l, (const uint8_t*)&l + 4);
+        payload.insert(payload.end(), buf, buf + len);
+        sig_at.push_back(payload.size() - 64);
+    }
+    sbft_verifier_add_clients(reg, keys.data(), (size_t)requests);
+    std::vector<char> infos((size_t)requests * 40);
+    std::vector<double> t;
+    int wrong = 0;
+    char err[256];
+    auto call = [&](sbft_verifier* v, const std::vector<uint8_t>& pl, size_t& count, int64_t& bad) {
+        sbft_proposal p{pl.data(), pl.size(), (const uint8_t*)"h", 1, (const uint8_t*)"m", 1, 0};
+        return sbft_verifier_verify_proposal(v, &p, infos.data(), infos.size(), &count, &bad, err, sizeof err);
+    };
+    for (int g = -3; g < decisions; ++g) {
+        size_t count = 0;
+        int64_t bad = -1;
+        const auto t0 = Clock::now();
+        int rc = call(gen, payload, count, bad);
+        const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        if (g >= 0) t.push_back(us);
+        wrong += rc != 0 || count != (size_t)requests;
+        const int k = (g + 3) * 7919 % requests;
+        std::vector<uint8_t> pb = payload;
+        pb[sig_at[k] + 5] ^= 0x40;
+        rc = call(gen, pb, count, bad);
+        wrong += rc != SBFT_V_EVERIFY || bad != k;
+        pb.assign(payload.begin(), payload.end() - 1 - (g + 3) % 50);
+        rc = call(gen, pb, count, bad);
+        wrong += rc != SBFT_V_EFORMAT;
+        rc = call(reg, payload, count, bad);
+        wrong += rc != 0 || count != (size_t)requests;
+    }
+    std::printf("{\"mode\": \"proposal-gpu\", \"requests\": %d, \"decisions\": %d, \"p50_ms\": %.4f, "
+                "\"p99_ms\": %.4f, \"wrong_verdicts\": %d}\n",
+                requests, decisions, pct(t, 50) / 1e3, pct(t, 99) / 1e3, wrong);
+    sbft_verifier_free(reg);
+    sbft_verifier_free(gen);
+    sbft_gv_destroy(ctx);
+    return wrong ? 2 : 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-hook|sign|quorum-cpu|proposal-cpu ...\n", argv[0]);
+        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-hook|sign|quorum-cpu|proposal-cpu|proposal-gpu ...\n", argv[0]);
         return 1;
     }
     const std::string mode = argv[1];
@@ -570,6 +642,7 @@ int main(int argc, char** argv) {
     if (mode == "sign") return sign_both(arg(2, 200));
     if (mode == "quorum-cpu") return quorum_cpu(arg(2, 66), arg(3, 200), arg(4, 66));
     if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
+    if (mode == "proposal-gpu") return proposal_gpu(arg(2, 3000), arg(3, 20));
     std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
     return 1;
 }
