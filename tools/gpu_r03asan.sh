@@ -5,6 +5,8 @@
 # consenter coalescer (66 concurrent callers), the uncoalesced zero-copy lanes, the batch hook,
 # the processCommits collector, the signer and VerifyProposal (generic, bad signature, truncated,
 # registered clients). Any ASan report aborts the step (halt_on_error).
+# tools/asan_build (the ASan builds) is gpurun-ignored: drop that line from
+# .gpurunignore to run this again.
 mkdir -p gpurun_out
 out=gpurun_out/r03asan.txt
 : > $out

@@ -23,6 +23,7 @@
 //       each, keys pre-materialised.
 //   proposal-cpu REQUESTS DECISIONS THREADS
 //   proposal-gpu REQUESTS DECISIONS
+//   parse-cpu    REQUESTS ITERS
 //       VerifyProposal (view.go:555) on the CPU: REQUESTS signed requests (distinct keys,
 //       64-256 B bodies) verified by THREADS workers pulling indices from an atomic counter:
 //       SHA-256(body) + ECDSA_do_verify each, keys pre-materialised (favours the CPU: a real
@@ -629,9 +630,58 @@ static int proposal_gpu(int requests, int decisions) {
     return wrong ? 2 : 0;
 }
 
+// parse-cpu REQUESTS ITERS: RequestsFromProposal on a parse-only verifier (no GPU): a proposal of
+// REQUESTS format-only requests (garbage keys and signatures), parsed ITERS times -- the
+// 3-thread parse (verifier.cpp parse_payload_par and its helper pool) from several caller threads
+// at once, plus truncated copies. A race detector's workload, not a measurement.
+static int parse_cpu(int requests, int iters) {
+    std::vector<uint8_t> pl(4);
+    const uint32_t cnt = (uint32_t)requests;
+    std::memcpy(pl.data(), &cnt, 4);
+    for (int i = 0; i < requests; ++i) {
+        const std::string cid = "client" + std::to_string(i), rid = "tx" + std::to_string(i);
+        std::vector<uint8_t> r = {'S', 'B', 'R', '1'};
+        auto u = [&](uint64_t v, int n) {
+            for (int k = 0; k < n; ++k) r.push_back((uint8_t)(v >> (8 * k)));
+        };
+        u(cid.size(), 2);
+        r.insert(r.end(), cid.begin(), cid.end());
+        u(rid.size(), 2);
+        r.insert(r.end(), rid.begin(), rid.end());
+        const size_t body = 64 + i % 193;
+        u(body, 4);
+        r.insert(r.end(), body, (uint8_t)i);
+        r.push_back(0x04);
+        r.insert(r.end(), 64 + 64, 0x5a);
+        const uint32_t l = (uint32_t)r.size();
+        pl.insert(pl.end(), (const uint8_t*)&l, (const uint8_t*)&l + 4);
+        pl.insert(pl.end(), r.begin(), r.end());
+    }
+    sbft_verifier* v = sbft_verifier_new(nullptr, 0);
+    std::atomic<int> wrong{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < 3; ++t)
+        th.emplace_back([&, t] {
+            std::vector<char> infos((size_t)requests * 24);
+            for (int it = 0; it < iters; ++it) {
+                const bool cut = (it + t) % 4 == 3;
+                sbft_proposal p{pl.data(), pl.size() - (cut ? 1 + it % 7 : 0), (const uint8_t*)"h", 1,
+                                (const uint8_t*)"m", 1, 0};
+                size_t count = 0;
+                const int rc = sbft_verifier_requests_from_proposal(v, &p, infos.data(), infos.size(), &count);
+                if (cut ? rc != SBFT_V_EFORMAT : (rc != 0 || count != (size_t)requests)) wrong++;
+            }
+        });
+    for (auto& x : th) x.join();
+    sbft_verifier_free(v);
+    std::printf("{\"mode\": \"parse-cpu\", \"requests\": %d, \"iters\": %d, \"wrong\": %d}\n", requests, iters,
+                wrong.load());
+    return wrong.load() ? 2 : 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-hook|sign|quorum-cpu|proposal-cpu|proposal-gpu ...\n", argv[0]);
+        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-hook|sign|quorum-cpu|proposal-cpu|proposal-gpu|parse-cpu ...\n", argv[0]);
         return 1;
     }
     const std::string mode = argv[1];
@@ -643,6 +693,7 @@ int main(int argc, char** argv) {
     if (mode == "quorum-cpu") return quorum_cpu(arg(2, 66), arg(3, 200), arg(4, 66));
     if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
     if (mode == "proposal-gpu") return proposal_gpu(arg(2, 3000), arg(3, 20));
+    if (mode == "parse-cpu") return parse_cpu(arg(2, 6000), arg(3, 50));
     std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
     return 1;
 }
