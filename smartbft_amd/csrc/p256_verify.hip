@@ -1009,8 +1009,23 @@ SBFT_DEV fe load_be32_any(const uint8_t* p) {
     return r;
 }
 
+// SBFT_PAIR_COMB_WAVE (FRAMED pair kernel): u1*G on a third wavefront of the workgroup. The ladder
+// needs only u2 = r s^-1; the digest, and with it u1, only the comb. So a comb wavefront (one lane
+// per tuple) inverts s itself, waits for the digests at the table barrier, sums the K + 1 comb
+// entries (add_aff_fix after each: partial sums can meet +-entry, u1 = 0 ends at infinity) and
+// leaves the sum in LDS; the verify wavefront, its ladder done, adds it with one Jacobian addition
+// and the same in-place case split (u1 G = u2 Q: a doubling; = -u2 Q: infinity). The 13 comb
+// additions leave the verify wavefront's stream; the comb wavefront runs on another SIMD.
+#ifndef SBFT_PAIR_COMB_WAVE
+#define SBFT_PAIR_COMB_WAVE 0
+#endif
+template <int LPT, bool FRAMED>
+constexpr int small_kernel_threads() {
+    return !FRAMED ? 64 : (LPT == 2 && SBFT_PAIR_COMB_WAVE) ? 192 : 128;
+}
+
 template <int LPT, bool FRAMED = false>
-__global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(const uint8_t* __restrict__ digest,
+__global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_verify_small_kernel(const uint8_t* __restrict__ digest,
                                                                              const uint8_t* __restrict__ rr,
                                                                              const uint8_t* __restrict__ ss,
                                                                              const uint8_t* __restrict__ qxx,
@@ -1021,12 +1036,14 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
                                                                              FramedIn fr) {
     static_assert(LPT == 2 || LPT == 4, "two or four lanes per tuple");
     constexpr bool kQuad = LPT == 4;
+    constexpr bool kCombWave = FRAMED && !kQuad && SBFT_PAIR_COMB_WAVE;
     constexpr int kTuples = 64 / LPT;  // tuples per 64-lane verify wavefront
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     // [entry][x limbs 0..8, y limbs 0..8][tuple]: the lanes of a tuple read the same word, the
     // tuples of the wave consecutive words
     __shared__ u32 qtab[kQTab * 18 * kTuples];
     __shared__ u32 edig[FRAMED ? 8 * kTuples : 1];  // FRAMED: the hash wave's digests [word][tuple]
+    __shared__ u32 gsum[kCombWave ? 28 * kTuples : 1];  // the comb wave's u1 G: [x, y, z limbs, inf][tuple]
     inv::stage_divstep_table(dtab);  // ends with a barrier
 
     if constexpr (FRAMED) {
@@ -1045,12 +1062,53 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
 #pragma unroll
                 for (int k = 0; k < 8; ++k) edig[k * kTuples + lane] = h[k];
             }
-            // the verify wavefront's barriers: the Q table's, and the quad's two comb stagings
+            // the verify wavefront's barriers: the Q table's, and the quad's two comb stagings or
+            // the comb wave's hand-over
             __syncthreads();
             if constexpr (kQuad) {
                 __syncthreads();
                 __syncthreads();
             }
+            if constexpr (kCombWave) __syncthreads();
+            return;
+        }
+    }
+    if constexpr (kCombWave) {
+        if (threadIdx.x >= 128) {  // the comb wavefront (wave-uniform branch): one lane per tuple
+            const uint32_t lane = threadIdx.x - 128;
+            const uint32_t slot = lane < (uint32_t)kTuples ? lane : 0u;
+            const uint32_t tc = blockIdx.x * kTuples + slot;
+            const uint32_t ic = tc < n ? tc : n - 1;
+            const uint8_t* end = fr.blob + fr.off[ic] + fr.len[ic];
+            const fe rc = load_be32_any(end + fr.sig_rel), sc = load_be32_any(end + fr.sig_rel + 32);
+            const fe qxc = load_be32_any(end + fr.pub_rel), qyc = load_be32_any(end + fr.pub_rel + 32);
+            const bool vc = verify_inputs_valid(rc, sc, qxc, qyc);
+            fe x = fe_zero(), si;
+            x.v[0] = 1;
+            if (vc) x = sc;
+            inv::inv_mod(si.v, x.v, dtab, false);  // plain s^-1 mod n (1 for an invalid s)
+            __syncthreads();  // the table barrier: the hash wave's digests are in edig
+            fe ec, w, u1c, u2c;
+            bool n1, n2;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ec.v[7 - k] = edig[k * kTuples + slot];
+            fn_mul(w, si, fe_const(C_R2N));  // s^-1 R
+            verify_scalars(w, vc, ec, rc, u1c, u2c, n1, n2);
+            jp29 g;
+            g.x = g.y = g.z = f29_const(C29_ONE);
+            bool ginf = true;  // the first addition returns its addend (add_aff_fix)
+            comb_add_u1g(g, u1c, n1, gcomb, [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
+                         [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
+            if (lane < (uint32_t)kTuples) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    gsum[k * kTuples + lane] = g.x.v[k];
+                    gsum[(9 + k) * kTuples + lane] = g.y.v[k];
+                    gsum[(18 + k) * kTuples + lane] = g.z.v[k];
+                }
+                gsum[27 * kTuples + lane] = ginf ? 1u : 0u;
+            }
+            __syncthreads();  // hand-over to the verify wavefront
             return;
         }
     }
@@ -1270,6 +1328,30 @@ __global__ __launch_bounds__(FRAMED ? 128 : 64) void p256_verify_small_kernel(co
             g.z.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.z.v[k], 0xEE, 0xF, 0xF, false);
         }
         p29_add_jac_lean(acc, g);
+    } else if constexpr (kCombWave) {
+        __syncthreads();  // the comb wavefront's sum is in gsum
+        jp29 g;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            g.x.v[k] = gsum[k * kTuples + pr];
+            g.y.v[k] = gsum[(9 + k) * kTuples + pr];
+            g.z.v[k] = gsum[(18 + k) * kTuples + pr];
+        }
+        const bool ginf = gsum[27 * kTuples + pr] != 0;
+        const jp29 a0 = acc;
+        p29_add_jac_lean(acc, g);
+        // H == 0 (Z3 = Z1 Z2 H = 0): X3 = r^2, so r == 0 (u1 G == u2 Q: the result is a doubling)
+        // iff X3 == 0, else u1 G == -u2 Q and the result is infinity
+        const bool hz = !inf && !ginf && f29_zero_mod_p(acc.z);
+        if (__builtin_expect(__any(hz || inf || ginf), 0)) {
+            const bool twice = hz && f29_zero_mod_p_any(acc.x);
+            jp29 d = a0;
+            dblp(d);
+            if (twice) acc = d;
+            if (ginf) acc = a0;
+            if (inf) acc = g;
+            inf = (hz && !twice) || (inf && ginf);
+        }
     } else {
 #ifndef SBFT_PAIR_NO_COMB
         if (SBFT_PAIR_LANE_LOCAL) {
@@ -1666,7 +1748,8 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
     const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, pub_rel, d_dig, d_r, d_s, d_qx, d_qy, h_flagged};
     const unsigned tpw = 64 / (unsigned)lanes, sblocks = (n + tpw - 1) / tpw;
     if (lanes == 2)
-        hipLaunchKernelGGL((sbft::p256_verify_small_kernel<2, true>), dim3(sblocks), dim3(128), 0, stream, d_dig,
+        hipLaunchKernelGGL((sbft::p256_verify_small_kernel<2, true>), dim3(sblocks),
+                           dim3((sbft::small_kernel_threads<2, true>())), 0, stream, d_dig,
                            d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
     else
         hipLaunchKernelGGL((sbft::p256_verify_small_kernel<4, true>), dim3(sblocks), dim3(128), 0, stream, d_dig,
