@@ -1009,19 +1009,21 @@ SBFT_DEV fe load_be32_any(const uint8_t* p) {
     return r;
 }
 
-// SBFT_PAIR_COMB_WAVE (FRAMED pair kernel): u1*G on a third wavefront of the workgroup. The ladder
-// needs only u2 = r s^-1; the digest, and with it u1, only the comb. So a comb wavefront (one lane
-// per tuple) inverts s itself, waits for the digests at the table barrier, sums the K + 1 comb
-// entries (add_aff_fix after each: partial sums can meet +-entry, u1 = 0 ends at infinity) and
-// leaves the sum in LDS; the verify wavefront, its ladder done, adds it with one Jacobian addition
-// and the same in-place case split (u1 G = u2 Q: a doubling; = -u2 Q: infinity). The 13 comb
-// additions leave the verify wavefront's stream; the comb wavefront runs on another SIMD.
+// SBFT_PAIR_COMB_WAVE (FRAMED pair kernel): u1*G on the hash wavefront. The ladder needs only
+// u2 = r s^-1; the digest, and with it u1, only the comb. So the hash wavefront, its digests
+// published at the table barrier, goes on (one lane per tuple): it inverts s itself, sums the
+// K + 1 comb entries (add_aff_fix after each: partial sums can meet +-entry, u1 = 0 ends at
+// infinity) and leaves the sum in LDS; the verify wavefront, its ladder done, adds it with one
+// Jacobian addition and the same in-place case split (u1 G = u2 Q: a doubling; = -u2 Q:
+// infinity). The 13 comb additions leave the verify wavefront's stream; the hash wavefront runs
+// on another SIMD and was idle after hashing (a third wavefront instead put six on the CUs that
+// hold two workgroups: a worse tail, profiles/r03cw_comb_wave_lat.txt).
 #ifndef SBFT_PAIR_COMB_WAVE
 #define SBFT_PAIR_COMB_WAVE 0
 #endif
 template <int LPT, bool FRAMED>
 constexpr int small_kernel_threads() {
-    return !FRAMED ? 64 : (LPT == 2 && SBFT_PAIR_COMB_WAVE) ? 192 : 128;
+    return FRAMED ? 128 : 64;
 }
 
 template <int LPT, bool FRAMED = false>
@@ -1069,46 +1071,41 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
                 __syncthreads();
                 __syncthreads();
             }
-            if constexpr (kCombWave) __syncthreads();
-            return;
-        }
-    }
-    if constexpr (kCombWave) {
-        if (threadIdx.x >= 128) {  // the comb wavefront (wave-uniform branch): one lane per tuple
-            const uint32_t lane = threadIdx.x - 128;
-            const uint32_t slot = lane < (uint32_t)kTuples ? lane : 0u;
-            const uint32_t tc = blockIdx.x * kTuples + slot;
-            const uint32_t ic = tc < n ? tc : n - 1;
-            const uint8_t* end = fr.blob + fr.off[ic] + fr.len[ic];
-            const fe rc = load_be32_any(end + fr.sig_rel), sc = load_be32_any(end + fr.sig_rel + 32);
-            const fe qxc = load_be32_any(end + fr.pub_rel), qyc = load_be32_any(end + fr.pub_rel + 32);
-            const bool vc = verify_inputs_valid(rc, sc, qxc, qyc);
-            fe x = fe_zero(), si;
-            x.v[0] = 1;
-            if (vc) x = sc;
-            inv::inv_mod(si.v, x.v, dtab, false);  // plain s^-1 mod n (1 for an invalid s)
-            __syncthreads();  // the table barrier: the hash wave's digests are in edig
-            fe ec, w, u1c, u2c;
-            bool n1, n2;
+            if constexpr (kCombWave) {  // then u1 G for the same tuples, one lane each
+                const uint32_t slot = lane < (uint32_t)kTuples ? lane : 0u;
+                const uint32_t tc = blockIdx.x * kTuples + slot;
+                const uint32_t ic = tc < n ? tc : n - 1;
+                const uint8_t* end = fr.blob + fr.off[ic] + fr.len[ic];
+                const fe rc = load_be32_any(end + fr.sig_rel), sc = load_be32_any(end + fr.sig_rel + 32);
+                const fe qxc = load_be32_any(end + fr.pub_rel), qyc = load_be32_any(end + fr.pub_rel + 32);
+                const bool vc = verify_inputs_valid(rc, sc, qxc, qyc);
+                fe x = fe_zero(), si;
+                x.v[0] = 1;
+                if (vc) x = sc;
+                inv::inv_mod(si.v, x.v, dtab, false);  // plain s^-1 mod n (1 for an invalid s)
+                fe ec, w, u1c, u2c;
+                bool n1, n2;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) ec.v[7 - k] = edig[k * kTuples + slot];
-            fn_mul(w, si, fe_const(C_R2N));  // s^-1 R
-            verify_scalars(w, vc, ec, rc, u1c, u2c, n1, n2);
-            jp29 g;
-            g.x = g.y = g.z = f29_const(C29_ONE);
-            bool ginf = true;  // the first addition returns its addend (add_aff_fix)
-            comb_add_u1g(g, u1c, n1, gcomb, [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
-                         [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
-            if (lane < (uint32_t)kTuples) {
+                for (int k = 0; k < 8; ++k) ec.v[7 - k] = edig[k * kTuples + slot];
+                fn_mul(w, si, fe_const(C_R2N));  // s^-1 R
+                verify_scalars(w, vc, ec, rc, u1c, u2c, n1, n2);
+                jp29 g;
+                g.x = g.y = g.z = f29_const(C29_ONE);
+                bool ginf = true;  // the first addition returns its addend (add_aff_fix)
+                comb_add_u1g(g, u1c, n1, gcomb,
+                             [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
+                             [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
+                if (lane < (uint32_t)kTuples) {
 #pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    gsum[k * kTuples + lane] = g.x.v[k];
-                    gsum[(9 + k) * kTuples + lane] = g.y.v[k];
-                    gsum[(18 + k) * kTuples + lane] = g.z.v[k];
+                    for (int k = 0; k < 9; ++k) {
+                        gsum[k * kTuples + lane] = g.x.v[k];
+                        gsum[(9 + k) * kTuples + lane] = g.y.v[k];
+                        gsum[(18 + k) * kTuples + lane] = g.z.v[k];
+                    }
+                    gsum[27 * kTuples + lane] = ginf ? 1u : 0u;
                 }
-                gsum[27 * kTuples + lane] = ginf ? 1u : 0u;
+                __syncthreads();  // hand-over to the verify wavefront
             }
-            __syncthreads();  // hand-over to the verify wavefront
             return;
         }
     }
