@@ -1009,21 +1009,29 @@ SBFT_DEV fe load_be32_any(const uint8_t* p) {
     return r;
 }
 
-// SBFT_PAIR_COMB_WAVE (FRAMED pair kernel): u1*G on the hash wavefront. The ladder needs only
-// u2 = r s^-1; the digest, and with it u1, only the comb. So the hash wavefront, its digests
-// published at the table barrier, goes on (one lane per tuple): it inverts s itself, sums the
-// K + 1 comb entries (add_aff_fix after each: partial sums can meet +-entry, u1 = 0 ends at
-// infinity) and leaves the sum in LDS; the verify wavefront, its ladder done, adds it with one
-// Jacobian addition and the same in-place case split (u1 G = u2 Q: a doubling; = -u2 Q:
-// infinity). The 13 comb additions leave the verify wavefront's stream; the hash wavefront runs
-// on another SIMD and was idle after hashing (a third wavefront instead put six on the CUs that
-// hold two workgroups: a worse tail, profiles/r03cw_comb_wave_lat.txt).
+// SBFT_PAIR_COMB_WAVE (FRAMED pair kernel): u1*G on a wavefront of its own. The ladder needs only
+// u2 = r s^-1; the digest, and with it u1, only the comb. The workgroup is four wavefronts: two
+// verify wavefronts (64 tuples, two lanes each), the hash wavefront (one lane per tuple) and the
+// comb wavefront (one lane per tuple), which inverts s itself, reads the digests at the table
+// barrier, sums the K + 1 comb entries (add_aff_fix after each: partial sums can meet +-entry,
+// u1 = 0 ends at infinity) and leaves the sum in LDS; each verify wavefront, its ladder done, adds
+// it with one Jacobian addition and the same in-place case split (u1 G = u2 Q: a doubling;
+// = -u2 Q: infinity). The 13 comb additions leave the verify wavefronts' stream. With 64 tuples
+// per workgroup a 10k batch is 157 workgroups, at most one per CU, so every wavefront has a SIMD
+// of its own (three wavefronts of 32 tuples put six on the CUs holding two workgroups, and the
+// comb on the hash wavefront shares its SIMD's time: both were slower,
+// profiles/r03cw_comb_wave_lat.txt).
 #ifndef SBFT_PAIR_COMB_WAVE
-#define SBFT_PAIR_COMB_WAVE 0
+#define SBFT_PAIR_COMB_WAVE 1
 #endif
 template <int LPT, bool FRAMED>
 constexpr int small_kernel_threads() {
-    return FRAMED ? 128 : 64;
+    return !FRAMED ? 64 : (LPT == 2 && SBFT_PAIR_COMB_WAVE) ? 256 : 128;
+}
+// tuples per workgroup
+template <int LPT, bool FRAMED>
+constexpr int small_kernel_tuples() {
+    return (FRAMED && LPT == 2 && SBFT_PAIR_COMB_WAVE) ? 64 : 64 / LPT;
 }
 
 template <int LPT, bool FRAMED = false>
@@ -1039,7 +1047,8 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
     static_assert(LPT == 2 || LPT == 4, "two or four lanes per tuple");
     constexpr bool kQuad = LPT == 4;
     constexpr bool kCombWave = FRAMED && !kQuad && SBFT_PAIR_COMB_WAVE;
-    constexpr int kTuples = 64 / LPT;  // tuples per 64-lane verify wavefront
+    constexpr int kTuples = small_kernel_tuples<LPT, FRAMED>();  // tuples per workgroup
+    constexpr unsigned kVerifyThreads = kTuples * LPT;          // the verify wavefront(s)
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     // [entry][x limbs 0..8, y limbs 0..8][tuple]: the lanes of a tuple read the same word, the
     // tuples of the wave consecutive words
@@ -1049,8 +1058,8 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
     inv::stage_divstep_table(dtab);  // ends with a barrier
 
     if constexpr (FRAMED) {
-        if (threadIdx.x >= 64) {  // the hash wavefront (wave-uniform branch)
-            const uint32_t lane = threadIdx.x - 64, th = blockIdx.x * kTuples + lane;
+        if (threadIdx.x >= kVerifyThreads && threadIdx.x < kVerifyThreads + 64) {  // the hash wavefront
+            const uint32_t lane = threadIdx.x - kVerifyThreads, th = blockIdx.x * kTuples + lane;
             if (lane < (uint32_t)kTuples && th < n) {
                 const uint8_t* msg = fr.blob + fr.off[th];
                 const uint32_t L = fr.len[th], nb = sha256_nblocks(L);
@@ -1071,45 +1080,51 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
                 __syncthreads();
                 __syncthreads();
             }
-            if constexpr (kCombWave) {  // then u1 G for the same tuples, one lane each
-                const uint32_t slot = lane < (uint32_t)kTuples ? lane : 0u;
-                const uint32_t tc = blockIdx.x * kTuples + slot;
-                const uint32_t ic = tc < n ? tc : n - 1;
-                const uint8_t* end = fr.blob + fr.off[ic] + fr.len[ic];
-                const fe rc = load_be32_any(end + fr.sig_rel), sc = load_be32_any(end + fr.sig_rel + 32);
-                const fe qxc = load_be32_any(end + fr.pub_rel), qyc = load_be32_any(end + fr.pub_rel + 32);
-                const bool vc = verify_inputs_valid(rc, sc, qxc, qyc);
-                fe x = fe_zero(), si;
-                x.v[0] = 1;
-                if (vc) x = sc;
-                inv::inv_mod(si.v, x.v, dtab, false);  // plain s^-1 mod n (1 for an invalid s)
-                fe ec, w, u1c, u2c;
-                bool n1, n2;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) ec.v[7 - k] = edig[k * kTuples + slot];
-                fn_mul(w, si, fe_const(C_R2N));  // s^-1 R
-                verify_scalars(w, vc, ec, rc, u1c, u2c, n1, n2);
-                jp29 g;
-                g.x = g.y = g.z = f29_const(C29_ONE);
-                bool ginf = true;  // the first addition returns its addend (add_aff_fix)
-                comb_add_u1g(g, u1c, n1, gcomb,
-                             [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
-                             [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
-                if (lane < (uint32_t)kTuples) {
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) {
-                        gsum[k * kTuples + lane] = g.x.v[k];
-                        gsum[(9 + k) * kTuples + lane] = g.y.v[k];
-                        gsum[(18 + k) * kTuples + lane] = g.z.v[k];
-                    }
-                    gsum[27 * kTuples + lane] = ginf ? 1u : 0u;
-                }
-                __syncthreads();  // hand-over to the verify wavefront
-            }
+            if constexpr (kCombWave) __syncthreads();  // the comb wavefront's hand-over
             return;
         }
     }
 
+    if constexpr (kCombWave) {
+        if (threadIdx.x >= kVerifyThreads + 64) {  // the comb wavefront (wave-uniform branch)
+            const uint32_t lane = threadIdx.x - kVerifyThreads - 64;
+            const uint32_t slot = lane < (uint32_t)kTuples ? lane : 0u;
+            const uint32_t tc = blockIdx.x * kTuples + slot;
+            const uint32_t ic = tc < n ? tc : n - 1;
+            const uint8_t* end = fr.blob + fr.off[ic] + fr.len[ic];
+            const fe rc = load_be32_any(end + fr.sig_rel), sc = load_be32_any(end + fr.sig_rel + 32);
+            const fe qxc = load_be32_any(end + fr.pub_rel), qyc = load_be32_any(end + fr.pub_rel + 32);
+            const bool vc = verify_inputs_valid(rc, sc, qxc, qyc);
+            fe x = fe_zero(), si;
+            x.v[0] = 1;
+            if (vc) x = sc;
+            inv::inv_mod(si.v, x.v, dtab, false);  // plain s^-1 mod n (1 for an invalid s)
+            __syncthreads();  // the table barrier: the hash wavefront's digests are in edig
+            fe ec, w, u1c, u2c;
+            bool n1, n2;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ec.v[7 - k] = edig[k * kTuples + slot];
+            fn_mul(w, si, fe_const(C_R2N));  // s^-1 R
+            verify_scalars(w, vc, ec, rc, u1c, u2c, n1, n2);
+            jp29 g;
+            g.x = g.y = g.z = f29_const(C29_ONE);
+            bool ginf = true;  // the first addition returns its addend (add_aff_fix)
+            comb_add_u1g(g, u1c, n1, gcomb,
+                         [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
+                         [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
+            if (lane < (uint32_t)kTuples) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    gsum[k * kTuples + lane] = g.x.v[k];
+                    gsum[(9 + k) * kTuples + lane] = g.y.v[k];
+                    gsum[(18 + k) * kTuples + lane] = g.z.v[k];
+                }
+                gsum[27 * kTuples + lane] = ginf ? 1u : 0u;
+            }
+            __syncthreads();  // hand-over to the verify wavefronts
+            return;
+        }
+    }
     const int pr = threadIdx.x / LPT;
     const bool odd = (threadIdx.x & 1) != 0;
     const bool comb_role = kQuad && (threadIdx.x & 2) != 0;
@@ -1743,7 +1758,8 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
             cus = 256;
     }
     const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, pub_rel, d_dig, d_r, d_s, d_qx, d_qy, h_flagged};
-    const unsigned tpw = 64 / (unsigned)lanes, sblocks = (n + tpw - 1) / tpw;
+    const unsigned tpw = lanes == 2 ? (unsigned)sbft::small_kernel_tuples<2, true>() : 64 / (unsigned)lanes;
+    const unsigned sblocks = (n + tpw - 1) / tpw;
     if (lanes == 2)
         hipLaunchKernelGGL((sbft::p256_verify_small_kernel<2, true>), dim3(sblocks),
                            dim3((sbft::small_kernel_threads<2, true>())), 0, stream, d_dig,
