@@ -429,8 +429,11 @@ def sha_config5(gv, dev, n_msgs: int, e2e_msgs: int = 262144):
         return e0.elapsed_time(e1) / 1e3 / reps
 
     nbytes = c5.total + 32 * n
-    sec_h = timed(lambda: gv.sha256_dev(c5.blob, c5.d_off, c5.d_len, dig, stream))
-    hv = lambda: gv.sha256_verify_dev(c5.blob, c5.d_off, c5.d_len, c5.r, c5.s, c5.qx, c5.qy, ok, dig, stream)
+    # offsets validated by the untimed calls above: the timed ones skip the (stream-synchronising)
+    # bounds check so that only the kernels are in the event window
+    sec_h = timed(lambda: gv.sha256_dev(c5.blob, c5.d_off, c5.d_len, dig, stream, check=False))
+    hv = lambda: gv.sha256_verify_dev(c5.blob, c5.d_off, c5.d_len, c5.r, c5.s, c5.qx, c5.qy, ok, dig, stream,
+                                      check=False)
     sec_hv = timed(hv)
     want = (~c5.corrupted).to(torch.uint8)
     mism = int((ok != want).sum())

@@ -47,6 +47,9 @@ func (rv *RequestVerifier) VerifyRequest(val []byte) (types.RequestInfo, error) 
 	errbuf := make([]byte, 512)
 	if rc := C.sbft_request_batcher_verify(rv.b, p.bytes(val), C.size_t(len(val)),
 		(*C.char)(unsafe.Pointer(&info[0])), C.size_t(len(info)), cchar(errbuf), C.size_t(len(errbuf))); rc != 0 {
+		if engineFailure(rc) {
+			rv.failStop("VerifyRequest", rc)
+		}
 		return types.RequestInfo{}, &VerifyError{Code: int(rc), Index: -1, Msg: errText(errbuf)}
 	}
 	return splitInfos(info, 1)[0], nil

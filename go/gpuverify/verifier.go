@@ -26,6 +26,7 @@ import (
 	"bytes"
 	"errors"
 	"fmt"
+	"log"
 	"runtime"
 	"unsafe"
 
@@ -46,19 +47,42 @@ type Options struct {
 	// waits for company.
 	CoalesceConsenterSigs int
 	CoalesceWaitMicros    uint32
+	// OnEngineFailure is called when the engine itself fails (a negative SBFT_GV_E* code: a
+	// device fault, a failed launch or copy, an allocation failure) instead of returning a
+	// verdict. It must not return: nil means log.Fatalf, i.e. the node exits and the cluster sees
+	// a crashed replica. Returning an error instead would read as a Byzantine leader: the library
+	// treats any VerifyProposal error as a bad proposal (complain, sync, abort: view.go:386-393)
+	// and a failed vote as a bad signature (view.go:839-841), so a GPU fault on the leader would
+	// reject its own proposals and one on a follower would blame an honest leader.
+	OnEngineFailure func(op string, err error)
 }
 
 // Verifier implements api.Verifier on the GPU engine. It is safe for concurrent use.
 type Verifier struct {
-	ctx *C.sbft_gv_ctx
-	v   *C.sbft_verifier
+	ctx    *C.sbft_gv_ctx
+	v      *C.sbft_verifier
+	onFail func(op string, err error)
+}
+
+// engineFailure reports whether rc is an infrastructure code (SBFT_GV_E*, -1 .. -6), as opposed
+// to a verdict (0, or SBFT_V_EVERIFY / EFORMAT / EKEY / ESPACE, -10 .. -13).
+func engineFailure(rc C.int) bool { return rc < 0 && rc > C.SBFT_V_EVERIFY }
+
+// failStop hands an engine failure to the fail-stop hook; it does not return.
+func (v *Verifier) failStop(op string, rc C.int) {
+	err := &VerifyError{Code: int(rc), Index: -1, Msg: "gpu engine: " + C.GoString(C.sbft_gv_strerror(rc))}
+	if v.onFail != nil {
+		v.onFail(op, err)
+	}
+	log.Fatalf("gpuverify: %s: %v: stopping this replica (fail-stop, not a verification failure)", op, err)
 }
 
 var _ api.Verifier = (*Verifier)(nil)
 
-// VerifyError is the error every failed verification returns; Code is the engine's status
-// (SBFT_V_EVERIFY, SBFT_V_EFORMAT, SBFT_V_EKEY or a negative SBFT_GV_E* infrastructure code)
-// and Index the first failing request of a proposal (-1 otherwise).
+// VerifyError is the error every failed verification returns; Code is the verdict
+// (SBFT_V_EVERIFY, SBFT_V_EFORMAT, SBFT_V_EKEY) and Index the first failing request of a
+// proposal (-1 otherwise). Engine failures (negative SBFT_GV_E* codes) are never returned as a
+// VerifyError: they go to Options.OnEngineFailure (fail-stop).
 type VerifyError struct {
 	Code  int
 	Index int64
@@ -75,7 +99,7 @@ func New(opts Options, verificationSequence uint64, consenters map[uint64][]byte
 	if rc := C.sbft_gv_init(&o, &ctx); rc != 0 {
 		return nil, fmt.Errorf("gpuverify: init: %s", C.GoString(C.sbft_gv_strerror(rc)))
 	}
-	v := &Verifier{ctx: ctx, v: C.sbft_verifier_new(ctx, C.uint64_t(verificationSequence))}
+	v := &Verifier{ctx: ctx, v: C.sbft_verifier_new(ctx, C.uint64_t(verificationSequence)), onFail: opts.OnEngineFailure}
 	if v.v == nil {
 		C.sbft_gv_destroy(ctx)
 		return nil, errors.New("gpuverify: verifier allocation failed")
@@ -223,6 +247,9 @@ func (v *Verifier) VerifyProposal(pr types.Proposal) ([]types.RequestInfo, error
 	var bad C.int64_t
 	rc := C.sbft_verifier_verify_proposal(v.v, p.proposal(pr), cchar(infos), C.size_t(len(infos)), &count, &bad,
 		cchar(errbuf), C.size_t(len(errbuf)))
+	if engineFailure(rc) {
+		v.failStop("VerifyProposal", rc)
+	}
 	if rc != 0 {
 		return nil, &VerifyError{Code: int(rc), Index: int64(bad), Msg: errText(errbuf)}
 	}
@@ -250,6 +277,9 @@ func (v *Verifier) VerifyRequest(val []byte) (types.RequestInfo, error) {
 	errbuf := make([]byte, 512)
 	if rc := C.sbft_verifier_verify_request(v.v, p.bytes(val), C.size_t(len(val)), cchar(info), C.size_t(len(info)),
 		cchar(errbuf), C.size_t(len(errbuf))); rc != 0 {
+		if engineFailure(rc) {
+			v.failStop("VerifyRequest", rc)
+		}
 		return types.RequestInfo{}, &VerifyError{Code: int(rc), Index: -1, Msg: errText(errbuf)}
 	}
 	return splitInfos(info, 1)[0], nil
@@ -268,6 +298,9 @@ func (v *Verifier) VerifyConsenterSig(s types.Signature, pr types.Proposal) ([]b
 	var n C.size_t
 	if rc := C.sbft_verifier_verify_consenter_sig(v.v, &cs, p.proposal(pr), (*C.uint8_t)(unsafe.Pointer(&aux[0])),
 		C.size_t(len(aux)), &n, cchar(errbuf), C.size_t(len(errbuf))); rc != 0 {
+		if engineFailure(rc) {
+			v.failStop("VerifyConsenterSig", rc)
+		}
 		return nil, &VerifyError{Code: int(rc), Index: -1, Msg: errText(errbuf)}
 	}
 	return aux[:n], nil
@@ -286,11 +319,8 @@ func (v *Verifier) VerifyConsenterSigs(sigs []types.Signature, pr types.Proposal
 	status := make([]C.int32_t, len(sigs))
 	if rc := C.sbft_verifier_verify_consenter_sigs(v.v, p.signatures(sigs), C.size_t(len(sigs)), p.proposal(pr),
 		&status[0]); rc != 0 {
-		err := &VerifyError{Code: int(rc), Index: -1, Msg: "gpu engine: " + C.GoString(C.sbft_gv_strerror(rc))}
-		for i := range errs {
-			errs[i] = err
-		}
-		return auxes, errs
+		// every rc here is the engine's (per-signature verdicts come back in status)
+		v.failStop("VerifyConsenterSigs", rc)
 	}
 	for i, st := range status {
 		switch st {
@@ -316,6 +346,9 @@ func (v *Verifier) VerifySignature(s types.Signature) error {
 	p.Pin(&cs)
 	errbuf := make([]byte, 512)
 	if rc := C.sbft_verifier_verify_signature(v.v, &cs, cchar(errbuf), C.size_t(len(errbuf))); rc != 0 {
+		if engineFailure(rc) {
+			v.failStop("VerifySignature", rc)
+		}
 		return &VerifyError{Code: int(rc), Index: -1, Msg: errText(errbuf)}
 	}
 	return nil
@@ -358,7 +391,7 @@ func (v *Verifier) PruneSet(reqs [][]byte) ([]int, error) {
 	idx := make([]C.size_t, len(reqs))
 	var n C.size_t
 	if rc := C.sbft_pool_prune(v.v, &ptrs[0], &lens[0], C.size_t(len(reqs)), &idx[0], &n); rc != 0 {
-		return nil, fmt.Errorf("gpuverify: prune: %s", C.GoString(C.sbft_gv_strerror(rc)))
+		v.failStop("PruneSet", rc) // pruning would otherwise drop valid requests as revoked
 	}
 	out := make([]int, int(n))
 	for i := range out {

@@ -64,7 +64,11 @@ typedef struct sbft_gv_opts {
                                   placement, per-device host workers) runs on a single GPU. For
                                   testing the split; a deployment leaves it 0. The environment
                                   variable SBFT_GV_SLOTS_PER_DEVICE overrides it. */
-    uint32_t reserved32;
+    int32_t half_max;       /* per-device batches of at most this many tuples (and above quad_max)
+                               run the half-size-scalar latency kernel: four lanes per tuple, w Q and
+                               v R0 as two 128-bit ladders (p256_verify_half_kernel); 0 = default
+                               SBFT_GV_HALF_MAX_DEFAULT, < 0 = never. The environment variable
+                               SBFT_GV_HALF_MAX overrides it. */
     uint64_t reserved[2];
 } sbft_gv_opts;
 
@@ -77,6 +81,7 @@ typedef struct sbft_gv_opts {
  * (per-lane 68-byte block loads) need. */
 #define SBFT_GV_SHA_BLOB_PAD 256u
 #define SBFT_GV_QUAD_MAX_DEFAULT 0u
+#define SBFT_GV_HALF_MAX_DEFAULT 12288u
 
 /* Create a context (per-device stream + device/pinned staging grown on demand).
  * opts may be NULL. Replaces: the plugin construction a Go app does before handing its
@@ -223,6 +228,22 @@ int sbft_gv_kernel_time(sbft_gv_ctx* ctx, uint64_t* launches, double* ms);
  * smartbft_amd/csrc/p256_selftest.hip). a, b, out: n x 32 bytes big-endian. */
 int sbft_gv_selftest_field(sbft_gv_ctx* ctx, int op, const uint8_t* a, const uint8_t* b, size_t n,
                            uint8_t* out);
+
+/* Fault injection (tests of the error paths; not for production use). Arms a process-wide fault
+ * of `kind`: its next `count` fault points fail (count < 0: every one until disarmed with
+ * SBFT_GV_FAULT_OFF) as the runtime would fail there -- the staging allocations return
+ * SBFT_GV_ENOMEM, the kernel launchers fail before launching (SBFT_GV_ELAUNCH), the checked
+ * stream synchronisations report SBFT_GV_EDEVICE once the work has drained. Every entry point
+ * must then return the negative SBFT_GV_E* code (never a verdict) and the context stays usable:
+ * the next call after disarming succeeds. Contexts created while a fault is armed fail their
+ * self-test, so arm after sbft_gv_init. The environment variable
+ * SBFT_GV_FAULT=nomem|launch|sync[:count] arms one at the end of sbft_gv_init. Returns 0, or
+ * SBFT_GV_EINVAL for an unknown kind. */
+#define SBFT_GV_FAULT_OFF 0
+#define SBFT_GV_FAULT_NOMEM 1
+#define SBFT_GV_FAULT_LAUNCH 2
+#define SBFT_GV_FAULT_SYNC 3
+int sbft_gv_inject_fault(int kind, int count);
 
 /* Go-semantics host helpers (no GPU). */
 void sbft_gv_normalize_hash(const uint8_t* hash, size_t len, uint8_t out32[32]);

@@ -35,6 +35,32 @@ static inline void cpu_relax() {
 #endif
 }
 
+// ---- test-only fault injection (sbft_gv_inject_fault) ----
+// The armed kind fires at its fault points: the staging allocations (NOMEM), the kernel launchers
+// (LAUNCH: they return failure before launching) and the checked stream synchronisations after the
+// work has drained (SYNC), so every injected failure leaves the device quiescent, as a real
+// allocation or launch failure would. left > 0 counts down, < 0 fires until disarmed.
+static std::atomic<int> g_fault_kind{SBFT_GV_FAULT_OFF};
+static std::atomic<int> g_fault_left{0};
+extern "C" __attribute__((visibility("hidden"))) int sbft_fault_hit(int kind) {
+    if (g_fault_kind.load(std::memory_order_relaxed) != kind) return 0;
+    int left = g_fault_left.load(std::memory_order_relaxed);
+    for (;;) {
+        if (left < 0) return 1;
+        if (left == 0) return 0;
+        if (g_fault_left.compare_exchange_weak(left, left - 1)) return 1;
+    }
+}
+// hipStreamSynchronize, then the SYNC fault point (the stream has drained either way)
+static hipError_t stream_sync(hipStream_t st) {
+    const hipError_t e = hipStreamSynchronize(st);
+    return (e == hipSuccess && sbft_fault_hit(SBFT_GV_FAULT_SYNC)) ? hipErrorUnknown : e;
+}
+#define NOMEM_POINT()                                              \
+    do {                                                           \
+        if (sbft_fault_hit(SBFT_GV_FAULT_NOMEM)) return SBFT_GV_ENOMEM; \
+    } while (0)
+
 namespace {
 
 // One helper thread per context for host work that can overlap a caller's PCIe copy (the
@@ -165,6 +191,7 @@ struct Slot {
     std::map<hipStream_t, Workspace> ws;
 
     uint32_t* stream_workspace(hipStream_t st, size_t bytes) {
+        if (sbft_fault_hit(SBFT_GV_FAULT_NOMEM)) return nullptr;
         std::lock_guard<std::mutex> g(ws_mu);
         Workspace& w = ws[st];
         if (w.cap < bytes) {
@@ -227,6 +254,7 @@ struct Slot {
         size_t cap = 0;
         // caller holds mu and has selected the slot's device
         int reserve(size_t bytes) {
+            NOMEM_POINT();
             if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
                 stream = nullptr;
                 return SBFT_GV_EDEVICE;
@@ -267,6 +295,7 @@ struct Slot {
     uint8_t* vmap_dev = nullptr;
     size_t vmap_cap = 0;
     int reserve_vmap(size_t bytes) {
+        NOMEM_POINT();
         if (bytes <= vmap_cap) return SBFT_GV_OK;
         if (vmap) {
             (void)hipStreamSynchronize(stream);  // the last launches that read it have drained
@@ -331,6 +360,7 @@ struct Slot {
     }
 
     int reserve_pinned(size_t bytes) {
+        NOMEM_POINT();
         if (bytes <= pin_cap) return SBFT_GV_OK;
         if (pin) (void)hipHostFree(pin);
         pin = nullptr;
@@ -347,6 +377,7 @@ struct Slot {
     uint8_t* bbuf = nullptr;
     size_t bcap = 0;
     int reserve_blob(size_t bytes) {
+        NOMEM_POINT();
         if (bytes <= bcap) return SBFT_GV_OK;
         if (bbuf) (void)hipFree(bbuf);
         bbuf = nullptr;
@@ -373,6 +404,7 @@ struct Slot {
     };
     std::vector<StreamStage> stage;
     int reserve_stage(size_t b, size_t dev_bytes, size_t in_bytes, size_t out_bytes) {
+        NOMEM_POINT();
         if (stage.size() <= b) stage.resize(b + 1);
         StreamStage& st = stage[b];
         if (!st.cs && hipStreamCreateWithFlags(&st.cs, hipStreamNonBlocking) != hipSuccess) {
@@ -424,6 +456,7 @@ struct Slot {
 
     uint64_t dgen = 0;  // dbuf allocations so far (a new one may reuse the old address)
     int reserve(size_t bytes) {
+        NOMEM_POINT();
         if (bytes <= dcap) return SBFT_GV_OK;
         if (dbuf) (void)hipFree(dbuf);
         dbuf = nullptr;
@@ -467,8 +500,11 @@ struct sbft_gv_ctx {
     // kernel; 0 = never (sbft_gv_opts.pair_max)
     uint32_t pair_max = SBFT_GV_PAIR_MAX_DEFAULT;
     uint32_t quad_max = SBFT_GV_QUAD_MAX_DEFAULT;  // ... four lanes per tuple (sbft_gv_opts.quad_max)
+    uint32_t half_max = SBFT_GV_HALF_MAX_DEFAULT;  // ... half-size scalars (sbft_gv_opts.half_max)
     std::atomic<uint32_t> rr{0};
-    int lanes_for(size_t n) const { return n <= quad_max ? 4 : n <= pair_max ? 2 : 1; }
+    // verify kernel for a per-device batch of n: 4 = quad form of the pair kernel, 3 = half-size
+    // scalars, 2 = pair kernel, 1 = throughput kernel
+    int lanes_for(size_t n) const { return n <= quad_max ? 4 : n <= half_max ? 3 : n <= pair_max ? 2 : 1; }
     // keyed batches (per device) of at most this many signatures take the zero-copy path
     // (enqueue_keyed); SBFT_KEYED_ZC_MAX overrides (0 = never)
     size_t keyed_zc_max = 1024;
@@ -528,7 +564,7 @@ static int power_on_selftest(Slot* sl) {
     uint8_t* base = sl->dbuf;
     uint32_t* work = (uint32_t*)(base + 5 * f + fo);
     HIPCHK(hipMemcpyAsync(base, h.data(), 5 * f, hipMemcpyHostToDevice, sl->stream));
-    for (int lanes : {1, 2, 4}) {
+    for (int lanes : {1, 2, 3, 4}) {
         HIPCHK(hipMemsetAsync(base + 5 * f, 0xEE, n, sl->stream));
         if (sbft_launch_p256_verify(base, base + f, base + 2 * f, base + 3 * f, base + 4 * f, base + 5 * f, (uint32_t)n,
                                     work, gcomb, sl->stream, nullptr, nullptr, lanes))
@@ -564,6 +600,14 @@ static int power_on_selftest(Slot* sl) {
 
 extern "C" {
 
+int sbft_gv_inject_fault(int kind, int count) {
+    if (kind < SBFT_GV_FAULT_OFF || kind > SBFT_GV_FAULT_SYNC) return SBFT_GV_EINVAL;
+    g_fault_kind.store(SBFT_GV_FAULT_OFF);
+    g_fault_left.store(kind == SBFT_GV_FAULT_OFF ? 0 : count);
+    g_fault_kind.store(kind);
+    return SBFT_GV_OK;
+}
+
 const char* sbft_gv_strerror(int code) {
     switch (code) {
     case SBFT_GV_OK: return "ok";
@@ -588,6 +632,11 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     if (opts && opts->min_split) ctx->min_split = opts->min_split;
     if (opts && opts->pair_max) ctx->pair_max = opts->pair_max < 0 ? 0u : (uint32_t)opts->pair_max;
     if (opts && opts->quad_max) ctx->quad_max = opts->quad_max < 0 ? 0u : (uint32_t)opts->quad_max;
+    if (opts && opts->half_max) ctx->half_max = opts->half_max < 0 ? 0u : (uint32_t)opts->half_max;
+    if (const char* e = getenv("SBFT_GV_HALF_MAX")) {
+        const long v = strtol(e, nullptr, 10);
+        ctx->half_max = v < 0 ? 0u : (uint32_t)v;
+    }
     if (const char* e = getenv("SBFT_KEYED_ZC_MAX")) ctx->keyed_zc_max = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("SBFT_KEYED_LANES_MIN")) ctx->keyed_lanes_min = (size_t)strtoull(e, nullptr, 10);
     // slots per device (sbft_gv_opts.slots_per_device, SBFT_GV_SLOTS_PER_DEVICE): > 1 runs the
@@ -630,6 +679,14 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
                 return rc;
             }
         }
+    }
+    // SBFT_GV_FAULT=nomem|launch|sync[:count] (tests): armed once the self-test has passed
+    if (const char* e = getenv("SBFT_GV_FAULT")) {
+        const int kind = !std::strncmp(e, "nomem", 5) ? SBFT_GV_FAULT_NOMEM
+                         : !std::strncmp(e, "launch", 6) ? SBFT_GV_FAULT_LAUNCH
+                         : !std::strncmp(e, "sync", 4) ? SBFT_GV_FAULT_SYNC : SBFT_GV_FAULT_OFF;
+        const char* c = std::strchr(e, ':');
+        (void)sbft_gv_inject_fault(kind, c ? std::atoi(c + 1) : -1);
     }
     *out = ctx;
     return SBFT_GV_OK;
@@ -885,21 +942,52 @@ std::vector<Chunk> plan(sbft_gv_ctx* ctx, size_t n) {
 // Run f(i) for i in [0, m): i = 0 on the calling thread, the others on the context's persistent
 // workers (worker i drives share i), so each device's pageable H2D copies and its synchronisation are
 // driven independently instead of one device after another. Returns the first non-zero rc.
+// Nothing escapes as an exception (the callers are C entry points): a share that throws reports
+// SBFT_GV_ENOMEM (bad_alloc) or SBFT_GV_EDEVICE, a share whose post fails runs on the calling
+// thread, and the frame (rc, mu, cv, left, f) outlives every posted job: the wait below runs
+// whatever share 0 does.
 template <class F>
 int for_each_device(sbft_gv_ctx* ctx, size_t m, F&& f) {
-    if (m == 1) return f((size_t)0);
-    std::vector<int> rc(m, SBFT_GV_OK);
+    auto run = [&f](size_t i) noexcept -> int {
+        try {
+            return f(i);
+        } catch (const std::bad_alloc&) {
+            return SBFT_GV_ENOMEM;
+        } catch (...) {
+            return SBFT_GV_EDEVICE;
+        }
+    };
+    if (m == 1) return run((size_t)0);
+    std::vector<int> rc;
+    try {
+        rc.assign(m, SBFT_GV_OK);
+    } catch (...) {
+        return SBFT_GV_ENOMEM;
+    }
     std::mutex mu;
     std::condition_variable cv;
-    size_t left = m - 1;
-    for (size_t i = 1; i < m; ++i)
-        ctx->workers.post(i, [&, i] {
-            const int r = f(i);
+    size_t left = 0;  // posted shares still running
+    for (size_t i = 1; i < m; ++i) {
+        {
             std::lock_guard<std::mutex> g(mu);
-            rc[i] = r;
-            if (--left == 0) cv.notify_one();
-        });
-    rc[0] = f((size_t)0);
+            ++left;
+        }
+        try {
+            ctx->workers.post(i, [&, i] {
+                const int r = run(i);
+                std::lock_guard<std::mutex> g(mu);
+                rc[i] = r;
+                if (--left == 0) cv.notify_one();
+            });
+        } catch (...) {  // not queued (Workers::post throws before the push): run it here
+            {
+                std::lock_guard<std::mutex> g(mu);
+                --left;
+            }
+            rc[i] = run(i);
+        }
+    }
+    rc[0] = run((size_t)0);
     {
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return left == 0; });
@@ -1222,7 +1310,7 @@ int run_chunks(sbft_gv_ctx* ctx, size_t n, F&& enqueue) {
         std::lock_guard<std::mutex> lk(c.slot->mu);
         int rc = enqueue(c, i);
         (void)hipSetDevice(c.slot->device);
-        if (hipStreamSynchronize(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
+        if (stream_sync(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
         return rc;
     });
 }
@@ -1375,7 +1463,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         const char* e = getenv("SBFT_VP_SYNC");
         return e && e[0] == '1';
     }();
-    const int sync_rc = (!sync_after_copy || hipStreamSynchronize(sl->stream) == hipSuccess) && ce == hipSuccess
+    const int sync_rc = (!sync_after_copy || stream_sync(sl->stream) == hipSuccess) && ce == hipSuccess
                             ? SBFT_GV_OK
                             : SBFT_GV_EDEVICE;
     const auto t3 = TC::now();
@@ -1410,7 +1498,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     if (n >= ctx->min_split && ctx->slots.size() > 1) {  // large: the multi-device split path
         // each share copies its own slice of the payload: this slot's copy is not used
         drain.armed = false;
-        if (hipStreamSynchronize(sl->stream) != hipSuccess) return SBFT_GV_EDEVICE;
+        if (stream_sync(sl->stream) != hipSuccess) return SBFT_GV_EDEVICE;
         lk.unlock();
         if (during) during();
         Framing fr;
@@ -1455,7 +1543,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
                                                  nkeys, sl->vmap_dev + fo + 2 * fl, (uint32_t)n, sl->stream))
             return SBFT_GV_ELAUNCH;
         if (during) during();  // the caller's host work that does not need the verdicts
-        HIPCHK(hipStreamSynchronize(sl->stream));
+        HIPCHK(stream_sync(sl->stream));
         drain.armed = false;
         std::memcpy(ok.data(), sl->vmap + fo + 2 * fl, n);
         return SBFT_GV_OK;
@@ -1500,12 +1588,12 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
                                            (uint32_t*)(d_hok + align_up(n, 256))))
             return SBFT_GV_ELAUNCH;
         if (during) during();
-        HIPCHK(hipStreamSynchronize(sl->stream));
+        HIPCHK(stream_sync(sl->stream));
         if (*flag) {
             if (sbft_launch_p256_verify_fixup(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_hok, (const uint32_t*)d_work,
                                               (uint32_t)n, sl->stream))
                 return SBFT_GV_ELAUNCH;
-            HIPCHK(hipStreamSynchronize(sl->stream));
+            HIPCHK(stream_sync(sl->stream));
         }
         drain.armed = false;
         std::memcpy(ok.data(), h_ok, n);
@@ -1522,7 +1610,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     // verdict copy, which (into pageable memory) returns only once the kernel has finished
     if (during) during();
     HIPCHK(hipMemcpyAsync(ok.data(), d_ok, n, hipMemcpyDeviceToHost, sl->stream));
-    HIPCHK(hipStreamSynchronize(sl->stream));
+    HIPCHK(stream_sync(sl->stream));
     drain.armed = false;
     return SBFT_GV_OK;
 }
@@ -1781,7 +1869,7 @@ int build_tables(Slot* sl, const std::vector<std::array<uint8_t, 64>>& keys, siz
     }
     HIPCHK(hipMemcpyAsync(sl->d_keytab, sl->comb.data(), sl->comb.size() * sizeof(void*), hipMemcpyHostToDevice,
                           sl->stream));
-    HIPCHK(hipStreamSynchronize(sl->stream));
+    HIPCHK(stream_sync(sl->stream));
     return SBFT_GV_OK;
 }
 
@@ -1907,6 +1995,7 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
             }
         }
     }
+    if (sbft_fault_hit(SBFT_GV_FAULT_SYNC)) return SBFT_GV_EDEVICE;  // the kernel has finished
     for (size_t k = 0; k < n; ++k) ok_out[b + k] = okh[k] & 1u;
     if (trace) {
         const auto t4 = std::chrono::steady_clock::now();
@@ -1959,7 +2048,7 @@ int run_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* blob, size
             rc = enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, c.slot->d_keytab, nullptr,
                                ok_out, ctx->keyed_lanes_min);
         (void)hipSetDevice(c.slot->device);
-        if (hipStreamSynchronize(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
+        if (stream_sync(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
         // the verdicts sit in the slot's pinned staging, which the lock still protects
         if (rc == SBFT_GV_OK) std::memcpy(ok_out + c.begin, c.slot->pin + c.out_off, c.count);
         return rc;
@@ -1994,7 +2083,7 @@ int sign_wave(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_
                                    want_q ? o + f : nullptr, o + 2 * f, o + 3 * f, o + 4 * f, (uint32_t)n, sl->stream))
         return SBFT_GV_ELAUNCH;
     HIPCHK(hipMemcpyAsync(h + in_bytes, o, out_bytes, hipMemcpyDeviceToHost, sl->stream));
-    HIPCHK(hipStreamSynchronize(sl->stream));
+    HIPCHK(stream_sync(sl->stream));
     const uint8_t* ho = h + in_bytes;
     if (want_q) {
         std::memcpy(qx, ho, 32 * n);
@@ -2038,28 +2127,28 @@ int sbft_gv_register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy
         Slot* sl = ctx->slots[si];
         std::lock_guard<std::mutex> lk(sl->mu);
         std::vector<uint8_t> sst;
-        rc = build_tables(sl, ctx->keys, upto, &sst);
+        // G's table first, in a block of its own: concurrent zero-copy batches may already read it
+        // (run_keyed needs only key 0 to be built), so the rollback below must never free it
+        rc = ensure_tables(sl, 1);
+        if (rc == SBFT_GV_OK) rc = build_tables(sl, ctx->keys, upto, &sst);
         // a device that had not built G's table yet built [0, upto): keep this call's tail
         if (rc == SBFT_GV_OK && sl->comb.size() == upto && sst.size() >= upto - before)
             st.assign(sst.end() - (upto - before), sst.end());
     }
     if (rc == SBFT_GV_OK && st.size() != upto - before && upto > before) rc = SBFT_GV_EDEVICE;
     if (rc) {
-        // forget this call's keys everywhere (tables of the batch are freed with their block)
+        // forget this call's keys everywhere. Their tables share one block per slot, which holds
+        // nothing else (G's table was built apart, above), and no other call can reach them: key
+        // ids >= before are published only on success (ctx->nkeys), so the zero-copy lanes, which
+        // run outside sl->mu, never read this block.
         for (Slot* sl : ctx->slots) {
             std::lock_guard<std::mutex> lk(sl->mu);
-            if (sl->comb.size() > before) {
+            if (sl->comb.size() > before && before >= 1) {
                 (void)hipSetDevice(sl->device);
-                (void)hipStreamSynchronize(sl->stream);
-                void* block = sl->comb_alloc.back();
-                // a slot that had no table yet built [0, upto) in this block, G's included:
-                // forget them all, so G's table is rebuilt on next use instead of pointing
-                // at freed memory
-                const bool holds_g = !sl->comb.empty() && sl->comb[0] == block;
-                (void)hipFree(block);
+                (void)hipStreamSynchronize(sl->stream);  // the build kernel ran on the slot's stream
+                (void)hipFree(sl->comb_alloc.back());
                 sl->comb_alloc.pop_back();
-                if (holds_g) sl->comb.clear();
-                else sl->comb.resize(before);
+                sl->comb.resize(before);
             }
         }
         for (size_t id = before; id < upto; ++id) ctx->key_index.erase(ctx->keys[id]);

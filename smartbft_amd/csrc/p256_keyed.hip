@@ -676,6 +676,7 @@ __global__ __launch_bounds__(128) void p256_sign_wave_kernel(const uint8_t* __re
 extern "C" int sbft_launch_p256_sign_wave(const uint8_t* d_d, const uint8_t* d_k, const uint8_t* d_e,
                                           const void* const* d_keytab, uint8_t* d_qx, uint8_t* d_qy, uint8_t* d_r,
                                           uint8_t* d_s, uint8_t* d_status, uint32_t n, hipStream_t stream) {
+    if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
     hipLaunchKernelGGL(sbft::p256_sign_wave_kernel, dim3(n), dim3(128), 0, stream, d_d, d_k, d_e,
                        (const uint4* const*)d_keytab, d_qx, d_qy, d_r, d_s, d_status, n);
@@ -698,6 +699,7 @@ extern "C" int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint
                                              const uint32_t* d_len, const uint8_t* d_r, const uint8_t* d_s,
                                              const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
                                              uint8_t* d_ok, uint32_t n, uint8_t mark, hipStream_t stream) {
+    if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
     if (!d_digest && (!d_blob || !d_off || !d_len)) return -1;
     hipLaunchKernelGGL(sbft::p256_verify_keyed_wave_kernel, dim3(n), dim3(128), 0, stream, d_digest, d_blob, d_off,

@@ -82,6 +82,7 @@ __global__ __launch_bounds__(256) void p256_sign_kernel(const uint8_t* __restric
 extern "C" int sbft_launch_p256_sign(const uint8_t* d_d, const uint8_t* d_k, const uint8_t* d_e,
                                      uint8_t* d_qx, uint8_t* d_qy, uint8_t* d_r, uint8_t* d_s,
                                      uint8_t* d_status, uint32_t n, hipStream_t stream) {
+    if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned blocks = (n + threads - 1) / threads;

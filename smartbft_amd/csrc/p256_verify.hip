@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "p256_f29.hpp"
+#include "p256_halfgcd.hpp"
 #include "p256_inv.hpp"
 #include "p256_point.hpp"
 #include "sbft_kernels.h"
@@ -593,9 +594,26 @@ SBFT_DEV void build_q_table(f29 (&tx)[TAB], f29 (&ty)[TAB], const fe& qx, const 
 // per step (see p29_dbl_pair). Conversion 1 step instead of 2, DBLU 4 instead of 6, each ZADDU
 // 3 instead of 6, the product of the Z ratios a 4-step tree instead of a 7-product chain, and
 // each affine conversion 3 steps instead of 5.
+// The pair build from the point already in the radix-2^29 Montgomery domain (qxm, qym in N).
+template <class InvP>
+SBFT_DEV void build_q_table_pair_m(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29& qxm, const f29& qym, bool odd,
+                                   InvP inv_p);
 template <class InvP>
 SBFT_DEV void build_q_table_pair(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& qx, const fe& qy, bool valid,
                                  bool odd, InvP inv_p) {
+    const f29 r2 = f29_const(C29_R2);
+    f29 qxm, qym, o;
+    f29_mul_ilp(o, f29_pick(odd, f29_from_u256(qx), f29_from_u256(qy)), r2);
+    f29_unpair(o, qxm, qym);
+    if (!valid) {
+        qxm = f29_const(C29_G2X);
+        qym = f29_const(C29_G2Y);
+    }
+    build_q_table_pair_m(tx, ty, qxm, qym, odd, inv_p);
+}
+template <class InvP>
+SBFT_DEV void build_q_table_pair_m(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29& qxm, const f29& qym, bool odd,
+                                   InvP inv_p) {
     static_assert(kQTab == 8, "the Z-ratio product tree below is written for 7 ratios");
     // e = a0 b0 (even lane's product), d = a1 b1 (odd lane's), both in both lanes
     auto pmul = [odd](f29& e, f29& d, const f29& a0, const f29& b0, const f29& a1, const f29& b1) {
@@ -604,12 +622,6 @@ SBFT_DEV void build_q_table_pair(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const fe& q
         f29_unpair(o, e, d);
     };
     const f29 r2 = f29_const(C29_R2);
-    f29 qxm, qym;
-    pmul(qxm, qym, f29_from_u256(qx), r2, f29_from_u256(qy), r2);
-    if (!valid) {
-        qxm = f29_const(C29_G2X);
-        qym = f29_const(C29_G2Y);
-    }
     tx[0] = qxm;
     ty[0] = qym;
     f29 dx, dy, cx, cy, z;  // D = 2Q and the current odd multiple, co-Z (Z = z)
@@ -1413,6 +1425,419 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
         }
     }
 }
+// ---- half-size scalars: two 128-bit ladders side by side (p256_verify_half_kernel) ----
+// The latency kernels' time is one wavefront's instruction stream, and 4/5 of the pair
+// kernel's is the 256-doubling u2 Q ladder. With v u2 = w (mod n), |v|, w < 2^128
+// (p256_halfgcd.hpp, Antipa et al. 2005) and R0 = (r, sqrt(r^3 - 3r + b)):
+//   x((v u1) G + w Q) == x(v R0)  <=>  u1 G + u2 Q = +-R0  <=>  x(u1 G + u2 Q) == r,
+// for r >= p - n (below that, x = r + n is a second candidate; such r are adversarial). Both
+// sides are 128-bit ladders, so each tuple takes a quad: lanes 0-1 (pair A) run w Q, lanes 2-3
+// (pair B) run v R0, in the same instruction stream as the pair kernel's lane-local ladder, over
+// [1, 3, ..., 15]P tables of their own. The price is the square root (253 squarings, every lane)
+// in front of the table build. A workgroup is three verify wavefronts (48 tuples) and a helper
+// wavefront (one lane per tuple: the request hash, s^-1, u1, u2, the Euclid reduction to (v, w),
+// then (v u1) G on the fixed-base comb), so a 10k batch is 209 workgroups, one per CU, each
+// wavefront on a SIMD of its own.
+// Every ladder here is free of exceptional additions: the partial scalars m of an odd k < 2^129
+// stay odd and 16 m +- d < n, and an even k runs as k + 1 followed by one subtraction of the base
+// (exceptional only for k = 0 or -2 mod n). The comb sum joins w Q with the comb wavefront
+// kernel's case split. A tuple whose reduction gave up, or with r < p - n, is verified the
+// classic way inside the same launch (v = 1, w = u2: a 64-digit ladder for its wavefront,
+// verify_final's comparison with r and r + n), so a crafted batch costs at most what the pair
+// kernel costs.
+#ifndef SBFT_HALF_TUPLES
+#define SBFT_HALF_TUPLES 48
+#endif
+constexpr int kHalfTuples = SBFT_HALF_TUPLES;  // per workgroup
+static_assert(kHalfTuples % 16 == 0 && kHalfTuples <= 64, "16 quads per verify wavefront, one helper wavefront");
+constexpr int kHalfVerifyThreads = 4 * kHalfTuples;
+constexpr int kHalfThreads = kHalfVerifyThreads + 64;
+constexpr int kHalfDigits = 32;  // radix-16 digits of an odd k < 2^129
+// b 2^261 mod p (radix 2^29) and p - n (8 x 32, < 2^127); tests/test_abi.py checks both
+__device__ __constant__ static const u32 C29_B[9] = {0x1897bbfbu, 0x1cdf6229u, 0x018486c4u, 0x01732821u, 0x1dad59e0u,
+                                                     0x0abf7212u, 0x1a06d110u, 0x17721d20u, 0x008600c3u};
+__device__ __constant__ static const u32 P256_PMN[8] = {0x039cdaaeu, 0x0c46353du, 0x58e8617bu, 0x43190553u, 0u, 0u, 0u, 0u};
+
+SBFT_DEV void f29_sqr_n(f29& t, int k) {
+#pragma unroll 1
+    for (int i = 0; i < k; ++i) f29_sqr_ilp(t, t);
+}
+// y = x^((p+1)/4), (p+1)/4 = ((2^64 - 2^32 + 1) 2^96 + 1) 2^94: 253 squarings, 7 products (the
+// Montgomery forms of x in and y out; y^2 == x iff x is a square)
+SBFT_DEV void f29_sqrt_chain(f29& y, const f29& x) {
+    f29 t, x2, x4, x8, x16;
+    f29_sqr_ilp(t, x);
+    f29_mul_ilp(x2, t, x);  // x^(2^2 - 1)
+    t = x2;
+    f29_sqr_n(t, 2);
+    f29_mul_ilp(x4, t, x2);  // 2^4 - 1
+    t = x4;
+    f29_sqr_n(t, 4);
+    f29_mul_ilp(x8, t, x4);  // 2^8 - 1
+    t = x8;
+    f29_sqr_n(t, 8);
+    f29_mul_ilp(x16, t, x8);  // 2^16 - 1
+    t = x16;
+    f29_sqr_n(t, 16);
+    f29_mul_ilp(t, t, x16);  // 2^32 - 1
+    f29_sqr_n(t, 32);
+    f29_mul_ilp(t, t, x);  // 2^64 - 2^32 + 1
+    f29_sqr_n(t, 96);
+    f29_mul_ilp(t, t, x);
+    f29_sqr_n(t, 94);
+    y = t;
+}
+
+template <bool FRAMED>
+__global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const uint8_t* __restrict__ digest,
+                                                                    const uint8_t* __restrict__ rr,
+                                                                    const uint8_t* __restrict__ ss,
+                                                                    const uint8_t* __restrict__ qxx,
+                                                                    const uint8_t* __restrict__ qyy,
+                                                                    uint8_t* __restrict__ ok, uint32_t n,
+                                                                    uint32_t* __restrict__ work,
+                                                                    const uint4* __restrict__ gcomb, FramedIn fr) {
+    constexpr int T = kHalfTuples;
+    __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
+    __shared__ u32 qtab[kQTab * 18 * 2 * T];    // [entry][x limbs, y limbs][pair A | pair B][tuple]
+    __shared__ u32 edig[FRAMED ? 8 * T : 1];    // FRAMED: the helper's digests [word][tuple]
+    __shared__ u32 hsc[17 * T];                 // the helper's scalars: [k_A 0..7, k_B 0..7, flags][tuple]
+    __shared__ u32 gsum[28 * T];                // the helper's (v u1) G: [x, y, z limbs, inf][tuple]
+    inv::stage_divstep_table(dtab);  // ends with a barrier
+
+    auto load_tuple = [&](uint32_t idx, fe& r, fe& s, fe& qx, fe& qy) {
+        if constexpr (FRAMED) {
+            const uint8_t* end = fr.blob + fr.off[idx] + fr.len[idx];
+            r = load_be32_any(end + fr.sig_rel);
+            s = load_be32_any(end + fr.sig_rel + 32);
+            qx = load_be32_any(end + fr.pub_rel);
+            qy = load_be32_any(end + fr.pub_rel + 32);
+        } else {
+            r = load_be32(rr + 32ull * idx);
+            s = load_be32(ss + 32ull * idx);
+            qx = load_be32(qxx + 32ull * idx);
+            qy = load_be32(qyy + 32ull * idx);
+        }
+    };
+    auto mod_n_neg = [](const fe& a) {  // n - a (a in [0, n])
+        fe t;
+        u64 b = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const u64 d = (u64)P256_N[k] - a.v[k] - b;
+            t.v[k] = lo32(d);
+            b = d >> 63;
+        }
+        return t;
+    };
+
+    if (threadIdx.x >= kHalfVerifyThreads) {  // the helper wavefront (wave-uniform branch)
+        const uint32_t lane = threadIdx.x - kHalfVerifyThreads;
+        const bool mine = lane < (uint32_t)T;
+        const uint32_t slot = mine ? lane : 0u;
+        const uint32_t tc = blockIdx.x * T + slot;
+        const uint32_t ic = tc < n ? tc : n - 1;
+        fe e_raw, r, s, qx, qy;
+        load_tuple(ic, r, s, qx, qy);
+        if constexpr (FRAMED) {
+            uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+            if (mine && tc < n) {
+                const uint8_t* msg = fr.blob + fr.off[ic];
+                const uint32_t L = fr.len[ic], nb = sha256_nblocks(L);
+                uint32_t w[16];
+                for (uint32_t b = 0; b < nb; ++b) {
+                    sha256_block_at(msg, L, b, w);
+                    compress(h, w);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                e_raw.v[7 - k] = h[k];
+                if (mine) edig[k * T + lane] = h[k];
+            }
+        } else {
+            e_raw = load_be32(digest + 32ull * ic);
+        }
+        const bool valid = verify_inputs_valid(r, s, qx, qy);
+        fe one = fe_zero();
+        one.v[0] = 1;
+        fe si, wm, e, u1, u2;
+        inv::inv_mod(si.v, (valid ? s : one).v, dtab, false);  // plain s^-1 mod n
+        fn_mul(wm, si, fe_const(C_R2N));                          // s^-1 R
+        fn_canon(e, e_raw);
+        fn_mul(u1, e, wm);
+        fn_canon(u1, u1);
+        fn_mul(u2, r, wm);
+        fn_canon(u2, u2);
+        if (!valid) u2 = one;
+        hgcd::state hs;
+        hgcd::init(hs, u2.v);
+#pragma unroll 1
+        for (int it = 0; it < 400; ++it) {
+            const bool go = hgcd::more(hs);
+            if (!__any(go)) break;
+            if (go) hgcd::step(hs);
+        }
+        fe w, va;
+        bool vneg;
+        hgcd::result(hs, w.v, va.v, vneg);
+        fe vr, c;
+        fn_mul(vr, va, fe_const(C_R2N));  // |v| R
+        bool good = hs.ok && !hgcd::more(hs) && !fe_is_zero_raw(w);
+        {  // v u2 == +-w (mod n): the result is used only when it provably holds
+            fe t;
+            fn_mul(t, vr, u2);
+            fn_canon(t, t);
+            good = good && fe_eq(t, vneg ? mod_n_neg(w) : w);
+        }
+        fn_mul(c, vr, u1);  // |v| u1
+        fn_canon(c, c);
+        if (vneg && !fe_is_zero_raw(c)) c = mod_n_neg(c);
+        const bool fb = valid && (!good || fe_lt(r, P256_PMN));  // the classic way: v = 1, w = u2
+        fe ka = w, kb = va;
+        if (fb || !valid) {
+            ka = u2;
+            kb = one;
+            c = u1;
+            vneg = false;
+        }
+        if (mine) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                hsc[k * T + lane] = ka.v[k];
+                hsc[(8 + k) * T + lane] = kb.v[k];
+            }
+            hsc[16 * T + lane] = (vneg ? 1u : 0u) | (fb ? 2u : 0u);
+        }
+        __syncthreads();  // #1: the scalars are in hsc (the verify wavefronts' tables in qtab)
+        // c G on the comb, in comb_add_u1g's odd recoding (even c -> n - c, base negated; c = 0
+        // becomes n, whose comb sum cancels to infinity)
+        const bool neg1 = (c.v[0] & 1u) == 0;
+        if (neg1) c = mod_n_neg(c);
+        jp29 g;
+        g.x = g.y = g.z = f29_const(C29_ONE);
+        bool ginf = true;  // the first addition returns its addend (add_aff_fix)
+        comb_add_u1g(g, c, neg1, gcomb, [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
+                     [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
+        if (mine) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                gsum[k * T + lane] = g.x.v[k];
+                gsum[(9 + k) * T + lane] = g.y.v[k];
+                gsum[(18 + k) * T + lane] = g.z.v[k];
+            }
+            gsum[27 * T + lane] = ginf ? 1u : 0u;
+        }
+        __syncthreads();  // #2: hand-over to the verify wavefronts
+        return;
+    }
+
+    const int tid = threadIdx.x;
+    const int pr = tid >> 2;                // tuple in the workgroup
+    const int role = (tid >> 1) & 1;        // 0: pair A (w Q), 1: pair B (v R0)
+    const bool odd = (tid & 1) != 0;
+    const int col = role * T + pr;          // this pair's column of qtab
+    const uint32_t t = blockIdx.x * T + pr;
+    const bool active = t < n;
+    const uint32_t idx = active ? t : (n - 1);
+    fe r, s, qx, qy;
+    load_tuple(idx, r, s, qx, qy);
+    const bool valid = verify_inputs_valid(r, s, qx, qy);
+
+    // R0 = (r, y0), y0 = (r^3 - 3r + b)^((p+1)/4) (every lane: pair B uses it)
+    const f29 r2c = f29_const(C29_R2);
+    f29 rm, rhs, y0;
+    f29_mul_ilp(rm, f29_from_u256(r), r2c);  // |r R| < 2^256.1 (product output)
+    {
+        f29 t2, t3;
+        const f29 b = f29_const(C29_B);
+        f29_sqr_ilp(t2, rm);
+        f29_mul_ilp(t3, t2, rm);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) rhs.v[i] = t3.v[i] - 3u * rm.v[i] + b.v[i];  // |limb| < 2^31, |.| < 2^259
+        f29_normalize(rhs, rhs);                                                  // N'
+    }
+    f29_sqrt_chain(y0, rhs);
+    bool has_r0;  // x = r is on the curve
+    {
+        f29 yy, d;
+        f29_sqr_ilp(yy, y0);
+        f29_sub(d, yy, rhs);  // |limb| < 2^30, |.| < 2^259
+        has_r0 = f29_zero_mod_p_any(d);
+    }
+    {
+        f29 qxm, qym, o;
+        f29_mul_ilp(o, f29_pick(odd, f29_from_u256(qx), f29_from_u256(qy)), r2c);
+        f29_unpair(o, qxm, qym);
+        f29 px = role ? rm : qxm, py = role ? y0 : qym;
+        if (!(valid && (role == 0 || has_r0))) {  // stand-in base 2G (verdict masked or rejected)
+            px = f29_const(C29_G2X);
+            py = f29_const(C29_G2Y);
+        }
+        f29 tx[kQTab], ty[kQTab];
+        build_q_table_pair_m(tx, ty, px, py, odd, [&](const fe& zp) {
+            fe zi;
+            inv::inv_mod(zi.v, zp.v, dtab, true);
+            return zi;
+        });
+#pragma unroll
+        for (int m = 0; m < kQTab; ++m)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {  // both lanes of the pair store the same words
+                qtab[(m * 18 + k) * 2 * T + col] = tx[m].v[k];
+                qtab[(m * 18 + 9 + k) * 2 * T + col] = ty[m].v[k];
+            }
+    }
+    __syncthreads();  // #1: tables in qtab, the helper's scalars in hsc
+
+    const u32 flags = hsc[16 * T + pr];
+    const bool fb = (flags & 2u) != 0;
+    const bool negb = role == 1 && (flags & 1u) != 0;  // v < 0: v R0 = |v| (-R0)
+    fe k;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k.v[i] = hsc[(role * 8 + i) * T + pr];
+    const bool keven = (k.v[0] & 1u) == 0;
+    if (keven) {  // k + 1 (k < n: no carry out)
+        u64 c = 1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            c += k.v[i];
+            k.v[i] = lo32(c);
+            c >>= 32;
+        }
+    }
+    const int L = __any(fb) ? kQDigits : kHalfDigits;  // wave-uniform
+
+    auto tab_entry = [&](int m, f29& x, f29& y) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            x.v[i] = qtab[(m * 18 + i) * 2 * T + col];
+            y.v[i] = qtab[(m * 18 + 9 + i) * 2 * T + col];
+        }
+    };
+    auto qentry = [&](int i, f29& x, f29& y) {
+        const int d = q_digit(k, i);
+        tab_entry((d < 0 ? -d : d) >> 1, x, y);
+        if ((d < 0) != negb) f29_neg(y, y);
+    };
+    auto dblp = [odd](jp29& p) { p29_dbl_pair(p, p, odd); };
+    jp29 acc;
+    tab_entry(0, acc.x, acc.y);  // the top term 16^L (k = 16^L + sum d_i 16^i)
+    acc.z = f29_const(C29_ONE);
+    if (negb) f29_neg(acc.y, acc.y);
+    bool inf = false;  // only a classic (fb) ladder can meet infinity, at its last addition
+    {
+        pl29 q = pl29_from(acc, odd);
+#pragma unroll 1
+        for (int i = L - 1; i >= 1; --i) {
+#pragma unroll
+            for (int d = 0; d < kQWin; ++d) p29_dbl_pl(q, odd);
+            f29 x2, y2;
+            qentry(i, x2, y2);
+            p29_add_aff_pl(q, x2, y2);
+        }
+#pragma unroll
+        for (int d = 0; d < kQWin; ++d) p29_dbl_pl(q, odd);
+        pl29_to(acc, q);
+        f29 x2, y2;
+        qentry(0, x2, y2);
+        p29_add_aff_pair(acc, x2, y2, odd);
+        add_aff_fix(acc, inf, dblp, [&](f29& x, f29& y) { qentry(0, x, y); });
+    }
+    if (__any(keven)) {  // k + 1 ran: subtract the base once
+        auto base_neg = [&](f29& x, f29& y) {
+            tab_entry(0, x, y);
+            if (!negb) f29_neg(y, y);
+        };
+        jp29 a2 = acc;
+        bool inf2 = inf;
+        f29 x2, y2;
+        base_neg(x2, y2);
+        p29_add_aff_pair(a2, x2, y2, odd);
+        add_aff_fix(a2, inf2, dblp, base_neg);
+        if (keven) {
+            acc = a2;
+            inf = inf2;
+        }
+    }
+    jp29 V;  // pair B's v R0 on pair A's lanes (quad_perm [2,3,2,3])
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        V.x.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)acc.x.v[i], 0xEE, 0xF, 0xF, false);
+        V.z.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)acc.z.v[i], 0xEE, 0xF, 0xF, false);
+    }
+
+    __syncthreads();  // #2: the helper's (v u1) G is in gsum
+    {
+        jp29 g;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            g.x.v[i] = gsum[i * T + pr];
+            g.y.v[i] = gsum[(9 + i) * T + pr];
+            g.z.v[i] = gsum[(18 + i) * T + pr];
+        }
+        const bool ginf = gsum[27 * T + pr] != 0;
+        const jp29 a0 = acc;
+        p29_add_jac_lean(acc, g);
+        // H == 0 (Z3 = 0): a doubling if X3 == 0 (c G == w Q), else infinity (c G == -w Q)
+        const bool hz = !inf && !ginf && f29_zero_mod_p(acc.z);
+        if (__builtin_expect(__any(hz || inf || ginf), 0)) {
+            const bool twice = hz && f29_zero_mod_p_any(acc.x);
+            jp29 d = a0;
+            dblp(d);
+            if (twice) acc = d;
+            if (ginf) acc = a0;
+            if (inf) acc = g;
+            inf = (hz && !twice) || (inf && ginf);
+        }
+    }
+    // T = acc (pair A), V: accept iff T != infinity and X_T Z_V^2 == X_V Z_T^2
+    bool accept, exc;
+    {
+        f29 zt2, zv2, lhs, rhs2, d;
+        f29_sqr(zt2, acc.z);
+        f29_sqr(zv2, V.z);
+        f29_mul(lhs, acc.x, zv2);
+        f29_mul(rhs2, V.x, zt2);
+        f29_sub(d, lhs, rhs2);  // |limb| < 2^29.2, |.| < 2^257
+        accept = has_r0 && f29_zero_mod_p_any(d);
+        exc = has_r0 && (f29_zero_mod_p(acc.z) || f29_zero_mod_p(V.z));  // never expected: fixup net
+    }
+    if (__builtin_expect(__any(fb), 0)) {
+        bool exc_f;
+        const bool acc_f = verify_final(acc, r, exc_f);
+        if (fb) {
+            accept = acc_f;
+            exc = exc_f;
+        }
+    }
+    if (inf) {  // R = infinity: rejected, not an exceptional tuple
+        accept = false;
+        exc = false;
+    }
+    if (active && (tid & 3) == 0) {
+        if (exc && valid) {
+            if constexpr (FRAMED) {  // the fixup kernel's inputs
+                fe e_raw;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) e_raw.v[7 - i] = edig[i * T + pr];
+                store_be32(fr.dig + 32ull * t, e_raw);
+                store_be32(fr.r + 32ull * t, r);
+                store_be32(fr.s + 32ull * t, s);
+                store_be32(fr.qx + 32ull * t, qx);
+                store_be32(fr.qy + 32ull * t, qy);
+            }
+            const uint32_t slot = atomicAdd(work, 1u);
+            work[1 + slot] = t;
+            if constexpr (FRAMED) {
+                if (fr.flagged) *(volatile uint32_t*)fr.flagged = 1u;
+            }
+        } else {
+            ok[t] = (valid && accept) ? 1 : 0;
+        }
+    }
+}
+
 // ---- registered keys, large batches: four lanes per signature (p256_verify_keyed_lanes) ----
 // For batches too large for one wavefront per signature (p256_keyed.hip's latency kernel),
 // each signature takes a quad: lane j sums 16 comb entries with lean mixed additions in
@@ -1611,6 +2036,7 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
                                        const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
                                        uint32_t n, uint32_t* d_work, const void* d_gcomb, hipStream_t stream,
                                        hipEvent_t ev0, hipEvent_t ev1, int lanes, int work_zeroed) {
+    if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned blocks = (n + threads - 1) / threads;
@@ -1652,7 +2078,11 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
         SBFT_STEP("totals");
     }
     if (ev0 && hipEventRecord(ev0, stream) != hipSuccess) return -1;
-    if (lanes == 2 || lanes == 4) {  // 64-lane workgroups of 32 or 16 tuples
+    if (lanes == 3) {  // half-size scalars: 48 tuples per workgroup (three quad wavefronts + a helper)
+        const unsigned hblocks = (n + sbft::kHalfTuples - 1) / sbft::kHalfTuples;
+        hipLaunchKernelGGL(sbft::p256_verify_half_kernel<false>, dim3(hblocks), dim3(sbft::kHalfThreads), 0, stream,
+                           d_digest, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, sbft::FramedIn{});
+    } else if (lanes == 2 || lanes == 4) {  // 64-lane workgroups of 32 or 16 tuples
         const unsigned tpw = 64 / lanes, sblocks = (n + tpw - 1) / tpw;
         if (lanes == 2)
             hipLaunchKernelGGL(sbft::p256_verify_small_kernel<2>, dim3(sblocks), dim3(64), 0, stream, d_digest,
@@ -1694,6 +2124,7 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
 extern "C" int sbft_launch_p256_verify_keyed_lanes(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                                    const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
                                                    uint8_t* d_ok, uint32_t n, hipStream_t stream) {
+    if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
     const unsigned threads = 256;
     const unsigned kblocks = (unsigned)((4ull * n + threads - 1) / threads);
@@ -1706,6 +2137,7 @@ extern "C" int sbft_launch_p256_verify_keyed_framed(const uint8_t* d_blob, const
                                                     const uint32_t* d_len, int32_t sig_rel, const uint32_t* d_key,
                                                     const void* const* d_keytab, uint32_t nkeys, uint8_t* d_ok,
                                                     uint32_t n, hipStream_t stream) {
+    if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
     const unsigned kblocks = (unsigned)((n + 63) / 64);  // 64 signatures per workgroup
     const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -1748,8 +2180,9 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
                                               uint8_t* d_r, uint8_t* d_s, uint8_t* d_qx, uint8_t* d_qy,
                                               uint8_t* d_ok, uint32_t* d_work, const void* d_gcomb,
                                               hipStream_t stream, int lanes, uint32_t* h_flagged) {
+    if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
-    if (lanes != 2 && lanes != 4) return -1;
+    if (lanes != 2 && lanes != 3 && lanes != 4) return -1;
     static int cus = 0;
     if (!cus) {
         int dev = 0;
@@ -1758,9 +2191,14 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
             cus = 256;
     }
     const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, pub_rel, d_dig, d_r, d_s, d_qx, d_qy, h_flagged};
-    const unsigned tpw = lanes == 2 ? (unsigned)sbft::small_kernel_tuples<2, true>() : 64 / (unsigned)lanes;
+    const unsigned tpw = lanes == 3   ? (unsigned)sbft::kHalfTuples
+                         : lanes == 2 ? (unsigned)sbft::small_kernel_tuples<2, true>()
+                                      : 64 / (unsigned)lanes;
     const unsigned sblocks = (n + tpw - 1) / tpw;
-    if (lanes == 2)
+    if (lanes == 3)
+        hipLaunchKernelGGL((sbft::p256_verify_half_kernel<true>), dim3(sblocks), dim3(sbft::kHalfThreads), 0, stream,
+                           d_dig, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
+    else if (lanes == 2)
         hipLaunchKernelGGL((sbft::p256_verify_small_kernel<2, true>), dim3(sblocks),
                            dim3((sbft::small_kernel_threads<2, true>())), 0, stream, d_dig,
                            d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);

@@ -19,6 +19,10 @@
 #endif
 #define SBFT_VERIFY_QTAB_BYTES (80 << (SBFT_TQWIN - 1))
 
+// Test-only fault injection (gpuverify.cpp, sbft_gv_inject_fault): nonzero when the armed fault
+// of this kind fires at this pass. The launchers below return failure then, before launching.
+extern "C" int sbft_fault_hit(int kind);
+
 extern "C" {
 // bytes of device workspace one sbft_launch_p256_verify call of n tuples needs
 size_t sbft_verify_work_bytes(size_t n);

@@ -535,6 +535,7 @@ extern "C" int sbft_launch_gather_framed(const uint8_t* d_blob, const uint64_t* 
 extern "C" int sbft_launch_sha256(const uint8_t* d_blob, const uint64_t* d_off, const uint32_t* d_len,
                                   const uint32_t* d_order, uint8_t* d_dig, uint32_t n, uint32_t* d_ctr,
                                   hipStream_t stream, int ctr_zeroed) {
+    if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
     static int cus = 0;
     if (!cus) {

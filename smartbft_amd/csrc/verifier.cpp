@@ -1243,7 +1243,10 @@ void sbft_verifier_set_verification_sequence(sbft_verifier* v, uint64_t seq) {
 // VerifyProposal parses on one: there the payload's DMA staging runs on another core at the same
 // time, and on the GPU box (16-core share of a 256-thread host) three parse threads took the
 // parse from ~92 to ~155 us and the call's p50 from 0.92 to 0.98 ms
-// (profiles/r03h_parse_threads_ab.txt).
+// (profiles/r03h_parse_threads_ab.txt). RequestsFromProposal parses on one as well: that A/B
+// is the only measurement on the box, and the helpers yield-spin for 0.5 ms after every job,
+// which costs the job's CPU quota (the throttling behind r03w's coalescer tail). A deployment
+// with cores to spare sets SBFT_PARSE_THREADS.
 static int parse_threads_for(int dflt) {
     const char* e = getenv("SBFT_PARSE_THREADS");
     return e ? std::max(1, std::atoi(e)) : dflt;
@@ -1254,7 +1257,7 @@ int sbft_verifier_requests_from_proposal(sbft_verifier* v, const sbft_proposal* 
     if (!v || !p || !count) return SBFT_GV_EINVAL;
     std::vector<Req>& reqs = proposal_scratch().reqs;
     *count = 0;
-    static const int parse_threads = parse_threads_for(3);
+    static const int parse_threads = parse_threads_for(1);
     if (!parse_payload_par(p->payload, p->payload_len, reqs, parse_threads, [](size_t) {}, [](uint32_t, uint32_t) {}))
         return SBFT_V_EFORMAT;
     char* w = infos;

@@ -23,7 +23,7 @@ EXPORTS = [
     "sbft_gv_register_key", "sbft_gv_verify_p256_keyed", "sbft_gv_sha256_verify_p256_keyed",
     "sbft_gv_kernel_timing", "sbft_gv_kernel_time", "sbft_gv_register_keys",
     "sbft_gv_sha256_verify_p256_framed", "sbft_gv_host_alloc", "sbft_gv_host_free",
-    "sbft_gv_plan_split", "sbft_gv_sha256_verify_p256_stream",
+    "sbft_gv_plan_split", "sbft_gv_sha256_verify_p256_stream", "sbft_gv_inject_fault",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -37,7 +37,7 @@ class GpuVerifyError(RuntimeError):
 class Opts(ctypes.Structure):
     _fields_ = [("device_mask", ctypes.c_uint32), ("min_split", ctypes.c_uint32),
                 ("pair_max", ctypes.c_int32), ("quad_max", ctypes.c_int32),
-                ("slots_per_device", ctypes.c_uint32), ("reserved32", ctypes.c_uint32),
+                ("slots_per_device", ctypes.c_uint32), ("half_max", ctypes.c_int32),
                 ("reserved", ctypes.c_uint64 * 2)]
 
 
@@ -79,6 +79,7 @@ def load_library():
     L.sbft_gv_verify_workspace_bytes.argtypes = [ctypes.c_size_t]
     L.sbft_gv_verify_workspace_bytes.restype = ctypes.c_size_t
     L.sbft_gv_selftest_field.argtypes = [_vp, ctypes.c_int, _u8p, _u8p, ctypes.c_size_t, _u8p]
+    L.sbft_gv_inject_fault.argtypes = [ctypes.c_int, ctypes.c_int]
     L.sbft_gv_kernel_timing.argtypes = [_vp, ctypes.c_int]
     L.sbft_gv_kernel_time.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]
     L.sbft_gv_normalize_hash.argtypes = [_u8p, ctypes.c_size_t, _u8p]
@@ -202,19 +203,31 @@ def normalize_scalar(be: bytes) -> bytes | None:
     return bytes(out) if L.sbft_gv_normalize_scalar(buf, len(be), out) else None
 
 
+FAULT_OFF, FAULT_NOMEM, FAULT_LAUNCH, FAULT_SYNC = 0, 1, 2, 3
+
+
+def inject_fault(kind: int, count: int = -1) -> None:
+    """Arm a process-wide engine fault (sbft_gv_inject_fault; tests of the error paths): the next
+    `count` fault points of `kind` fail (-1: every one until inject_fault(FAULT_OFF))."""
+    rc = load_library().sbft_gv_inject_fault(kind, count)
+    if rc:
+        raise GpuVerifyError(f"sbft_gv_inject_fault: {rc}")
+
+
 class GpuVerifier:
     """One sbft_gv_ctx. Host-array calls are synchronous; *_dev calls take torch tensors
     (device-resident) and enqueue on the given (or current) stream."""
 
     def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0, quad_max: int = 0,
-                 slots_per_device: int = 0):
+                 slots_per_device: int = 0, half_max: int = 0):
         """pair_max / quad_max: per-device batches of at most this many tuples run the latency
-        kernel with two / four lanes per tuple (0 = library default, negative = never).
+        kernel with two / four lanes per tuple (0 = library default, negative = never); half_max:
+        ... the half-size-scalar kernel (four lanes: two 128-bit ladders).
         slots_per_device > 1: that many engine slots per GPU, each taking a share of a split
         batch as a separate device would (runs the multi-device split on one GPU)."""
         self.L = load_library()
         ctx = _vp()
-        opts = Opts(device_mask, min_split, pair_max, quad_max, slots_per_device)
+        opts = Opts(device_mask, min_split, pair_max, quad_max, slots_per_device, half_max)
         rc = self.L.sbft_gv_init(ctypes.byref(opts), ctypes.byref(ctx))
         if rc:
             raise GpuVerifyError(f"sbft_gv_init: {self.L.sbft_gv_strerror(rc).decode()} ({rc})")
@@ -377,6 +390,22 @@ class GpuVerifier:
         s = stream if stream is not None else torch.cuda.current_stream(device)
         return ctypes.c_void_p(s.cuda_stream)
 
+    @staticmethod
+    def _check_blob_bounds(d_blob, d_off, d_len, stream, device):
+        """Every message [off, off + len) inside the blob. The reduction runs on the launch stream
+        (so offsets still being written there are read after their producer) and its result is
+        read back, which synchronises that stream: callers that need the launch to stay
+        asynchronous validate their offsets themselves and pass check=False. uint64 offsets at
+        or above 2^63 are rejected, not wrapped."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(device)
+        with torch.cuda.stream(s):
+            off = d_off.view(torch.int64) if d_off.dtype == torch.uint64 else d_off.to(torch.int64)
+            ln = d_len.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+            bad = (off < 0) | (off + ln > d_blob.numel())
+            if bool(bad.any()):
+                raise ValueError("a message extends past the end of the blob (or its offset is >= 2^63)")
+
     def verify_dev(self, d_digest, d_r, d_s, d_qx, d_qy, d_ok, stream=None):
         n = d_ok.numel()
         dev = d_ok.device.index
@@ -385,17 +414,20 @@ class GpuVerifier:
         self._check(self.L.sbft_gv_verify_p256_dev(
             self.ctx, dev, *p, n, _dev(d_ok, n, "ok"), self._stream(stream, d_ok.device)), "sbft_gv_verify_p256_dev")
 
-    def sha256_verify_dev(self, d_blob, d_off, d_len, d_r, d_s, d_qx, d_qy, d_ok, d_dig, stream=None):
+    def sha256_verify_dev(self, d_blob, d_off, d_len, d_r, d_s, d_qx, d_qy, d_ok, d_dig, stream=None,
+                          check: bool = True):
         """Device-resident hash + verify (sbft_gv_sha256_verify_p256_dev): digests of the
-        messages land in d_dig and feed the verify of the same tuples on the same stream."""
+        messages land in d_dig and feed the verify of the same tuples on the same stream.
+        check=True validates the offsets against the blob first (_check_blob_bounds: this
+        synchronises the launch stream)."""
         import torch
         n = d_ok.numel()
         if d_off.dtype not in (torch.int64, torch.uint64) or d_len.dtype not in (torch.int32, torch.uint32):
             raise ValueError("offsets must be 64-bit and lengths 32-bit integers")
         if d_blob.dtype != torch.uint8 or not d_blob.is_contiguous() or not d_blob.is_cuda:
             raise ValueError("blob: expected a contiguous uint8 device tensor")
-        if n and int((d_off.to(torch.int64) + d_len.to(torch.int64)).max()) > d_blob.numel():
-            raise ValueError("a message extends past the end of the blob")
+        if n and check:
+            self._check_blob_bounds(d_blob, d_off, d_len, stream, d_ok.device)
         p = [_dev(t, 32 * n, w) for t, w in ((d_r, "r"), (d_s, "s"), (d_qx, "qx"), (d_qy, "qy"))]
         self._check(self.L.sbft_gv_sha256_verify_p256_dev(
             self.ctx, d_ok.device.index, d_blob.data_ptr(), _dev(d_off, n, "offsets", d_off.dtype),
@@ -412,10 +444,11 @@ class GpuVerifier:
         self._check(self.L.sbft_gv_kernel_time(self.ctx, ctypes.byref(n), ctypes.byref(ms)), "sbft_gv_kernel_time")
         return n.value, ms.value
 
-    def sha256_dev(self, d_blob, d_off, d_len, d_dig, stream=None, d_order=None):
+    def sha256_dev(self, d_blob, d_off, d_len, d_dig, stream=None, d_order=None, check: bool = True):
         """d_off int64/uint64 offsets, d_len int32 lengths, d_order (optional) int32 permutation;
         the hash kernel reads nothing outside the 16-byte granules holding message bytes, so
-        the blob needs no padding; offsets + lengths are checked against its size here."""
+        the blob needs no padding; check=True validates offsets + lengths against its size on the
+        launch stream first (_check_blob_bounds: this synchronises that stream)."""
         import torch
         n = d_off.numel()
         if d_blob.dtype != torch.uint8 or not d_blob.is_contiguous() or not d_blob.is_cuda:
@@ -423,9 +456,11 @@ class GpuVerifier:
         if d_off.dtype not in (torch.int64, torch.uint64):
             raise ValueError(f"offsets: expected 64-bit integers, got {d_off.dtype}")
         p_off = _dev(d_off, n, "offsets", d_off.dtype)
-        if n and int((d_off.to(torch.int64) + d_len.to(torch.int64)).max()) > d_blob.numel():
-            raise ValueError("a message extends past the end of the blob")
-        p_len = _dev(d_len, n, "lengths", d_len.dtype if d_len.dtype in (torch.int32, torch.uint32) else torch.int32)
+        if d_len.dtype not in (torch.int32, torch.uint32):
+            raise ValueError(f"lengths: expected 32-bit integers, got {d_len.dtype}")
+        if n and check:
+            self._check_blob_bounds(d_blob, d_off, d_len, stream, d_dig.device)
+        p_len = _dev(d_len, n, "lengths", d_len.dtype)
         p_ord = _dev(d_order, n, "order", d_order.dtype if d_order.dtype in (torch.int32, torch.uint32)
                      else torch.int32) if d_order is not None else None
         self._check(self.L.sbft_gv_sha256_dev(self.ctx, d_dig.device.index, d_blob.data_ptr(), p_off, p_len,

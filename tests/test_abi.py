@@ -129,3 +129,23 @@ def test_power_on_selftest_vectors_match_fixtures():
     dig = text[text.index("kPostShaDigest"):]
     digs = [bytes(int(x, 16) for x in m.split(",")) for m in re.findall(r"\{([0-9a-fx,]+)\}", dig)]
     assert [hashlib.sha256(blob[o:o + n]).digest() for o, n in zip(off, ln)] == digs
+
+
+def test_half_kernel_constants():
+    """The constants p256_verify_half_kernel carries in its source: b 2^261 mod p in radix 2^29
+    (the curve's b in the ladder's Montgomery domain), p - n (the bound below which x(R) = r + n
+    is a second candidate), and the group order of p256_halfgcd.hpp."""
+    import re
+    P = 2**256 - 2**224 + 2**192 + 2**96 - 1
+    N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+    B = 0x5AC635D8AA3A93E7B3EBBD55769886BC651D06B0CC53B0F63BCE3C3E27D2604B
+    src = open(os.path.join(ROOT, "smartbft_amd", "csrc", "p256_verify.hip")).read()
+
+    def words(name, radix):
+        m = re.search(name + r"\[\d+\] = \{([^}]*)\}", src)
+        return sum(int(w.strip().rstrip("u"), 16) << (radix * i) for i, w in enumerate(m.group(1).split(",")))
+    assert words("C29_B", 29) == B * 2**261 % P
+    assert words("P256_PMN", 32) == P - N
+    hg = open(os.path.join(ROOT, "smartbft_amd", "csrc", "p256_halfgcd.hpp")).read()
+    m = re.search(r"#define SBFT_HGCD_N \{([^}]*)\}", hg)
+    assert sum(int(w.strip().rstrip("u"), 16) << (32 * i) for i, w in enumerate(m.group(1).split(","))) == N

@@ -53,3 +53,37 @@ def test_patch_lines_are_gofmt_indented():
             if line.startswith("+") and not line.startswith("+++"):
                 body = line[1:].rstrip("\n")
                 assert not re.match(r"^ +\S", body), f"{p}: space-indented line {body!r}"
+
+
+def test_commit_hook_overlaps_and_guards_result_counts(tmp_path):
+    """The processCommits hook keeps up to two VerifyConsenterSigs calls in flight (a decision
+    with a bad vote overlaps its follow-up batch instead of serialising it), its result channel
+    holds every in-flight batch (an aborted View leaves no goroutine blocked), and both hooks
+    survive a batch verifier that returns the wrong number of results (no index panic)."""
+    files = sorted({f for p in PATCHES for f in _touched(p)})
+    for f in files:
+        os.makedirs(tmp_path / os.path.dirname(f), exist_ok=True)
+        shutil.copy(os.path.join(REF, f), tmp_path / f)
+    for p in PATCHES:
+        subprocess.run(["git", "apply", os.path.join(ROOT, "go", "patches", p)], cwd=tmp_path, check=True)
+    view = (tmp_path / "internal/bft/view.go").read_text()
+    support = (tmp_path / "internal/bft/support.go").read_text()
+    assert "const maxCommitBatches = 2" in view
+    assert "batchDone := make(chan commitBatch, maxCommitBatches)" in view
+    assert "inFlight < maxCommitBatches" in view
+    assert "if len(res.errs) != len(res.sigs)" in view
+    assert "batch verifier returned %d results for %d signatures" in view
+    assert "len(auxes) == len(errs) ==" in support
+
+
+def test_go_binding_fails_stop_on_engine_errors():
+    """pkg/gpuverify never returns an engine failure (negative SBFT_GV_E* code) as a verification
+    error: every entry point that can see one hands it to failStop."""
+    src = open(os.path.join(ROOT, "go", "gpuverify", "verifier.go")).read()
+    bat = open(os.path.join(ROOT, "go", "gpuverify", "batcher.go")).read()
+    assert "func engineFailure(rc C.int) bool { return rc < 0 && rc > C.SBFT_V_EVERIFY }" in src
+    for op in ("VerifyProposal", "VerifyRequest", "VerifyConsenterSig", "VerifyConsenterSigs", "VerifySignature",
+               "PruneSet"):
+        assert f'v.failStop("{op}", rc)' in src, op
+    assert 'rv.failStop("VerifyRequest", rc)' in bat
+    assert "log.Fatalf" in src

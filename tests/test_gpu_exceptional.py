@@ -44,10 +44,16 @@ def crafted():
     return cols, tags, want
 
 
-@pytest.mark.parametrize("mode", ["lane", "pair"])
+MODE_OPTS = {"lane": dict(pair_max=-1, quad_max=-1, half_max=-1),
+             "pair": dict(pair_max=1 << 30, quad_max=-1, half_max=-1),
+             "quad": dict(quad_max=1 << 30),
+             "half": dict(half_max=1 << 30, quad_max=-1)}
+
+
+@pytest.mark.parametrize("mode", ["lane", "pair", "half"])
 def test_crafted_exceptional_verdicts(crafted, mode):
     from smartbft_amd import GpuVerifier
-    opts = dict(pair_max=-1, quad_max=-1) if mode == "lane" else dict(pair_max=1 << 30, quad_max=-1)
+    opts = MODE_OPTS[mode]
     gv = GpuVerifier(**opts)
     try:
         cols, tags, want = crafted
@@ -61,13 +67,14 @@ def test_crafted_exceptional_verdicts(crafted, mode):
         gv.close()
 
 
-def test_crafted_exceptional_framed(crafted):
+@pytest.mark.parametrize("mode", ["pair", "half"])
+def test_crafted_exceptional_framed(crafted, mode):
     """The same tuples as framed requests (VerifyProposal's fused hash + verify launch): the
     digest is SHA-256 of the body, so the crafted scalars need e = SHA-256(body): re-derive s and
     r for each body (u1 = e/s, u2 = r/s kept by choosing s = e/u1, r = u2 s)."""
     from smartbft_amd import GpuVerifier
     cols, tags, want = crafted
-    gv = GpuVerifier()
+    gv = GpuVerifier(**MODE_OPTS[mode])
     try:
         rng = np.random.default_rng(3)
         parts, off, lens, exp = [], [], [], []
@@ -104,7 +111,7 @@ def _sbr1(i: int, pl: bytes, qx: bytes, qy: bytes) -> bytes:
             len(pl).to_bytes(4, "little") + pl + b"\x04" + qx + qy)
 
 
-@pytest.mark.parametrize("mode", ["pair", "quad"])
+@pytest.mark.parametrize("mode", ["pair", "quad", "half"])
 def test_crafted_exceptional_proposal(crafted, mode):
     """The crafted tuples as signed requests inside a VerifyProposal of honest ones
     (sbft_gv_framed_overlapped: fused hash + verify launch, verdicts in mapped host memory).
@@ -118,7 +125,7 @@ def test_crafted_exceptional_proposal(crafted, mode):
     skipped fix-up would show as an accepted proposal; the error must name that request."""
     from smartbft_amd import GpuVerifier, plugin
     cols, tags, want = crafted
-    opts = dict(pair_max=1 << 30, quad_max=-1) if mode == "pair" else dict(quad_max=1 << 30)
+    opts = MODE_OPTS[mode]
     gv = GpuVerifier(**opts)
     v = plugin.Verifier(gv)
     try:

@@ -288,9 +288,11 @@ def test_throughput_grid_shapes(gpu, n):
 
 # ---- every verify kernel at every size: the one-lane throughput kernel and the small-batch
 # latency kernel with two and four lanes per tuple (p256_verify_small_kernel<2|4>, forced on
-# for big batches too)
-KERNEL_OPTS = {"lane": dict(pair_max=-1, quad_max=-1), "pair": dict(pair_max=1 << 30, quad_max=-1),
-               "quad": dict(quad_max=1 << 30)}
+# for big batches too) and the half-size-scalar kernel (p256_verify_half_kernel)
+KERNEL_OPTS = {"lane": dict(pair_max=-1, quad_max=-1, half_max=-1),
+               "pair": dict(pair_max=1 << 30, quad_max=-1, half_max=-1),
+               "quad": dict(quad_max=1 << 30),
+               "half": dict(half_max=1 << 30, quad_max=-1)}
 
 
 @pytest.fixture(scope="module", params=list(KERNEL_OPTS))
@@ -504,3 +506,31 @@ def test_all_exceptional_batches(gpu_kernel, p256_vectors, n):
     idx = np.resize(np.nonzero(sel)[0], n)
     got = gpu_kernel.verify(*split_fields(f[idx]))
     assert np.array_equal(got, exp[idx])
+
+
+def test_device_hash_bounds_checked_on_launch_stream(gpu):
+    """The device-resident hash entries validate every message against the blob on the launch
+    stream before the launch: a message past the end and a uint64 offset >= 2^63 (which would
+    wrap negative as int64) are refused; offsets produced on a side stream are read after their
+    producer; check=False skips the validation (the caller's responsibility then)."""
+    import torch
+    dev = torch.device("cuda:0")
+    blob = torch.arange(256, dtype=torch.int32, device=dev).to(torch.uint8)
+    ln = torch.tensor([10, 20], dtype=torch.int32, device=dev)
+    dig = torch.zeros((2, 32), dtype=torch.uint8, device=dev)
+    side = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        off = torch.tensor([0, 236], dtype=torch.int64, device=dev)
+        torch.cuda._sleep(20_000_000)  # the producer is still running when the check is enqueued
+        off.add_(1)                    # 1, 237: the second message ends at 257 > 256
+    with pytest.raises(ValueError):
+        gpu.sha256_dev(blob, off, ln, dig, stream=side)
+    with pytest.raises(ValueError):
+        gpu.sha256_dev(blob, torch.tensor([0, 1 << 63], dtype=torch.uint64, device=dev), ln, dig)
+    ok_off = torch.tensor([1, 200], dtype=torch.int64, device=dev)
+    gpu.sha256_dev(blob, ok_off, ln, dig)
+    gpu.sha256_dev(blob, ok_off, ln, dig, check=False)
+    torch.cuda.synchronize()
+    host = bytes(range(256))
+    assert dig[0].cpu().numpy().tobytes() == hashlib.sha256(host[1:11]).digest()
+    assert dig[1].cpu().numpy().tobytes() == hashlib.sha256(host[200:220]).digest()

@@ -57,3 +57,51 @@ def test_host_mod_n_arithmetic(tmp_path):
         m, s = line.split()
         assert int(m, 16) == ar * br % N, (hex(a), hex(b))
         assert int(s, 16) == (ar + br) % N, (hex(a), hex(b))
+
+
+def _euclid_half(u):
+    """Exact restatement: Euclid on (n, u) stopped at the first remainder below 2^128 -> (w, v)
+    with v u = w (mod n), plus the largest quotient met (the kernel gives up at >= 2^31)."""
+    a, b, ta, tb, qmax = N, u, 0, 1, 0
+    while b >= 1 << 128:
+        q = a // b
+        qmax = max(qmax, q)
+        a, b, ta, tb = b, a - q * b, tb, ta - q * tb
+    return b, tb, qmax
+
+
+def test_half_gcd_matches_euclid(tmp_path):
+    """p256_halfgcd.hpp (the half-size scalars of p256_verify_half_kernel) against exact Euclid:
+    the same (w, v) whenever every quotient is below 2^31, a give-up otherwise, and always
+    v u = w (mod n), 0 < w < 2^128, |v| < 2^128 on success."""
+    exe = str(tmp_path / "hgcd_test")
+    subprocess.run(["g++", "-O2", "-Wall", "-Werror", "-o", exe,
+                    os.path.join(ROOT, "tests", "native", "hgcd_test.cpp")], check=True)
+    rng = random.Random(11)
+    us = [1, 2, 3, N - 1, N - 2, N // 2, N // 3, (N + 1) // 2, (1 << 128) - 1, 1 << 128, (1 << 128) + 1,
+          (1 << 255) % N, 0xFFFFFFFF, 1 << 200, N - (1 << 128)]
+    us += [N // k for k in (5, 7, 1000, 1 << 20, (1 << 31) - 1, 1 << 31, (1 << 31) + 1, 1 << 40)]
+    us += [rng.randrange(1, N) for _ in range(20000)]
+    # Fibonacci-like (all quotients 1: the longest runs) and near-multiples (large quotients)
+    f0, f1 = 1, 2
+    while f1 < N:
+        f0, f1 = f1, f0 + f1
+    us += [f0 % N, (f0 * 3) % N]
+    us += [(N * k) // (k * 1000 + 1) for k in range(1, 50)]
+    us += [(rng.randrange(1, 1 << 100) << 150) % N or 1 for _ in range(200)]
+    out = subprocess.run([exe], input="".join("%064x\n" % u for u in us), capture_output=True, text=True,
+                         check=True).stdout.split("\n")
+    nfail = 0
+    for u, line in zip(us, out):
+        w_x, v_x, qmax = _euclid_half(u)
+        f = line.split()
+        if f[0] == "0":
+            assert qmax >= 1 << 31, (hex(u), "gave up although every quotient is small")
+            nfail += 1
+            continue
+        assert qmax < 1 << 31, hex(u)
+        w, v, neg = int(f[1], 16), int(f[2], 16), f[3] == "1"
+        sv = -v if neg else v
+        assert (w, sv) == (w_x, v_x), hex(u)
+        assert (sv * u - w) % N == 0 and 0 < w < 1 << 128 and 0 < v < 1 << 128, hex(u)
+    assert nfail < 60  # only the crafted large-quotient inputs

@@ -3,9 +3,9 @@ walked from several candidate request boundaries at once and joined where the ch
 must accept and reject exactly the payloads the sequential parse does, report the same first
 bad request, and survive payloads crafted to defeat the speculation (request-looking bytes
 inside payloads). CPU only: RequestsFromProposal and a parse-only VerifyProposal (no engine).
-RequestsFromProposal parses on 3 threads by default, VerifyProposal on 1 (verifier.cpp
-parse_threads_for); SBFT_PARSE_THREADS sets both, once per process, so the VerifyProposal cases
-run again in a child process with it set."""
+RequestsFromProposal and VerifyProposal parse on 1 thread by default (verifier.cpp
+parse_threads_for); SBFT_PARSE_THREADS sets both, once per process, so every case runs again in a
+child process with 3 threads."""
 import os
 import subprocess
 import sys
@@ -126,13 +126,14 @@ def test_first_bad_key_reported_in_order(bad):
 
 
 def test_verify_proposal_parallel_prepare_in_child():
-    """The VerifyProposal cases above with SBFT_PARSE_THREADS=3 (the parallel prepare: per-range
-    format checks, first bad key by atomic minimum)."""
+    """Every case above with SBFT_PARSE_THREADS=3: the parallel walk and join of
+    RequestsFromProposal, and VerifyProposal's parallel prepare (per-range format checks, first
+    bad key by atomic minimum)."""
     env = dict(os.environ, SBFT_PARSE_THREADS="3")
     here = os.path.dirname(os.path.abspath(__file__))
     code = ("import sys; sys.path.insert(0, %r); import pytest; "
             "sys.exit(pytest.main(['-q', '-p', 'no:cacheprovider', %r, '-k', "
-            "'first_bad_key or malformed or in_order or random']))" % (here, os.path.join(here, "test_parse_parallel.py")))
+            "'not in_child']))" % (here, os.path.join(here, "test_parse_parallel.py")))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600,
                        cwd=os.path.dirname(here))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

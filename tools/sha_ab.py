@@ -40,7 +40,7 @@ e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=Tr
 reps = 5
 e0.record()
 for _ in range(reps):
-    gv.sha256_dev(blob, d_off, d_len, dig)
+    gv.sha256_dev(blob, d_off, d_len, dig, check=False)
 e1.record()
 torch.cuda.synchronize()
 sec = e0.elapsed_time(e1) / 1e3 / reps
