@@ -54,9 +54,8 @@ typedef struct sbft_gv_opts {
     uint32_t min_split;     /* batches smaller than this stay on one device (0 = default 65536) */
     int32_t pair_max;       /* per-device batches of at most this many tuples run the latency kernel
                                (two lanes per tuple); 0 = default SBFT_GV_PAIR_MAX_DEFAULT, < 0 = never */
-    int32_t quad_max;       /* ... and of at most this many, its four-lane form (the u1*G comb on
-                               lanes 2-3; measured no faster than the pair form, so off by default);
-                               0 = default SBFT_GV_QUAD_MAX_DEFAULT, < 0 = never */
+    int32_t quad_max;       /* ignored (round 3's four-lane form of the pair kernel, measured no
+                               faster, is gone; half_max selects the four-lane kernel now) */
     uint32_t slots_per_device; /* engine slots per selected device (0 = 1). Each slot owns a stream,
                                   staging, G's comb table and the registered-key tables, and takes
                                   one share of a split batch, exactly as a separate GPU would: with
@@ -80,7 +79,6 @@ typedef struct sbft_gv_opts {
  * blob with this much slack, which the hash-measurement variants selected by SBFT_SHA_VARIANT
  * (per-lane 68-byte block loads) need. */
 #define SBFT_GV_SHA_BLOB_PAD 256u
-#define SBFT_GV_QUAD_MAX_DEFAULT 0u
 #define SBFT_GV_HALF_MAX_DEFAULT 12288u
 
 /* Create a context (per-device stream + device/pinned staging grown on demand).

@@ -499,12 +499,11 @@ struct sbft_gv_ctx {
     // batches (per device) of at most this many tuples use the two-lanes-per-tuple latency
     // kernel; 0 = never (sbft_gv_opts.pair_max)
     uint32_t pair_max = SBFT_GV_PAIR_MAX_DEFAULT;
-    uint32_t quad_max = SBFT_GV_QUAD_MAX_DEFAULT;  // ... four lanes per tuple (sbft_gv_opts.quad_max)
     uint32_t half_max = SBFT_GV_HALF_MAX_DEFAULT;  // ... half-size scalars (sbft_gv_opts.half_max)
     std::atomic<uint32_t> rr{0};
-    // verify kernel for a per-device batch of n: 4 = quad form of the pair kernel, 3 = half-size
-    // scalars, 2 = pair kernel, 1 = throughput kernel
-    int lanes_for(size_t n) const { return n <= quad_max ? 4 : n <= half_max ? 3 : n <= pair_max ? 2 : 1; }
+    // verify kernel for a per-device batch of n: 3 = half-size scalars (four lanes per tuple),
+    // 2 = pair kernel, 1 = throughput kernel
+    int lanes_for(size_t n) const { return n <= half_max ? 3 : n <= pair_max ? 2 : 1; }
     // keyed batches (per device) of at most this many signatures take the zero-copy path
     // (enqueue_keyed); SBFT_KEYED_ZC_MAX overrides (0 = never)
     size_t keyed_zc_max = 1024;
@@ -551,7 +550,18 @@ static const std::array<uint8_t, 64> kGXY = {
 // range-visible form): a toolchain or driver that breaks it makes the context refuse to start
 // (SBFT_GV_ESELFTEST) instead of returning wrong verdicts.
 static int power_on_selftest(Slot* sl) {
-    HIPCHK(hipSetDevice(sl->device));
+    // SBFT_POST_TRACE=1: report the failing step on stderr (diagnostics)
+    static const bool trace = getenv("SBFT_POST_TRACE") != nullptr;
+#define POSTCHK(x, what)                                                                                  \
+    do {                                                                                                  \
+        const hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) {                                                                           \
+            if (trace) fprintf(stderr, "sbft POST: %s failed: %s (lanes %d)\n", what, hipGetErrorString(e_), cur); \
+            return SBFT_GV_EDEVICE;                                                                       \
+        }                                                                                                 \
+    } while (0)
+    int cur = 0;
+    POSTCHK(hipSetDevice(sl->device), "set device");
     const size_t n = SBFT_POST_N;
     const size_t f = align_up(32 * n, 256), fo = align_up(n, 256);
     int rc = sl->reserve(5 * f + fo + sbft_verify_work_bytes(n));
@@ -563,16 +573,20 @@ static int power_on_selftest(Slot* sl) {
         for (int fld = 0; fld < 5; ++fld) std::memcpy(&h[fld * f + 32 * k], kPostVectors[k] + 32 * fld, 32);
     uint8_t* base = sl->dbuf;
     uint32_t* work = (uint32_t*)(base + 5 * f + fo);
-    HIPCHK(hipMemcpyAsync(base, h.data(), 5 * f, hipMemcpyHostToDevice, sl->stream));
-    for (int lanes : {1, 2, 3, 4}) {
-        HIPCHK(hipMemsetAsync(base + 5 * f, 0xEE, n, sl->stream));
+    POSTCHK(hipMemcpyAsync(base, h.data(), 5 * f, hipMemcpyHostToDevice, sl->stream), "tuple copy");
+    for (int lanes : {1, 2, 3}) {
+        cur = lanes;
+        POSTCHK(hipMemsetAsync(base + 5 * f, 0xEE, n, sl->stream), "verdict memset");
         if (sbft_launch_p256_verify(base, base + f, base + 2 * f, base + 3 * f, base + 4 * f, base + 5 * f, (uint32_t)n,
                                     work, gcomb, sl->stream, nullptr, nullptr, lanes))
             return SBFT_GV_ELAUNCH;
-        HIPCHK(hipMemcpyAsync(ok.data(), base + 5 * f, n, hipMemcpyDeviceToHost, sl->stream));
-        HIPCHK(hipStreamSynchronize(sl->stream));
+        POSTCHK(hipMemcpyAsync(ok.data(), base + 5 * f, n, hipMemcpyDeviceToHost, sl->stream), "verdict copy");
+        POSTCHK(hipStreamSynchronize(sl->stream), "verify");
         for (size_t k = 0; k < n; ++k)
-            if (ok[k] != kPostVectors[k][160]) return SBFT_GV_ESELFTEST;
+            if (ok[k] != kPostVectors[k][160]) {
+                if (trace) fprintf(stderr, "sbft POST: lanes %d: tuple %zu verdict %d, expected %d\n", lanes, k, ok[k], kPostVectors[k][160]);
+                return SBFT_GV_ESELFTEST;
+            }
     }
     // SHA-256: blob (+ the kernel's over-read pad) | off | len | counter | digests
     const size_t m = SBFT_POST_SHA_N, fb = align_up(SBFT_POST_SHA_BLOB + SBFT_GV_SHA_BLOB_PAD, 256);
@@ -593,10 +607,12 @@ static int power_on_selftest(Slot* sl) {
     if (sbft_launch_sha256(b, (const uint64_t*)(b + fb), (const uint32_t*)(b + fb + 256), nullptr, b + fb + 768,
                            (uint32_t)m, (uint32_t*)(b + fb + 512), sl->stream))
         return SBFT_GV_ELAUNCH;
-    HIPCHK(hipMemcpyAsync(dig, b + fb + 768, sizeof dig, hipMemcpyDeviceToHost, sl->stream));
-    HIPCHK(hipStreamSynchronize(sl->stream));
+    cur = 0;
+    POSTCHK(hipMemcpyAsync(dig, b + fb + 768, sizeof dig, hipMemcpyDeviceToHost, sl->stream), "digest copy");
+    POSTCHK(hipStreamSynchronize(sl->stream), "sha256");
     return std::memcmp(dig, kPostShaDigest, sizeof dig) == 0 ? SBFT_GV_OK : SBFT_GV_ESELFTEST;
 }
+#undef POSTCHK
 
 extern "C" {
 
@@ -631,7 +647,6 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     if (!ctx) return SBFT_GV_ENOMEM;
     if (opts && opts->min_split) ctx->min_split = opts->min_split;
     if (opts && opts->pair_max) ctx->pair_max = opts->pair_max < 0 ? 0u : (uint32_t)opts->pair_max;
-    if (opts && opts->quad_max) ctx->quad_max = opts->quad_max < 0 ? 0u : (uint32_t)opts->quad_max;
     if (opts && opts->half_max) ctx->half_max = opts->half_max < 0 ? 0u : (uint32_t)opts->half_max;
     if (const char* e = getenv("SBFT_GV_HALF_MAX")) {
         const long v = strtol(e, nullptr, 10);

@@ -976,18 +976,14 @@ __global__ __launch_bounds__(256, SBFT_VERIFY_WAVES) void p256_verify_kernel(con
     }
 }
 
-// Latency kernels for small batches (sbft_launch_p256_verify with lanes = 2 or 4). A batch of
-// a few thousand tuples gives each busy SIMD one wave, so the launch takes one wave's
-// instruction stream; these kernels shorten that stream at the price of more lanes.
-//   LPT = 2 (pair): one verify on two adjacent lanes, the doublings and mixed additions split
-//     between them (p29_dbl_pair, p29_add_aff_pair); u1*G by the comb after the ladder.
-//   LPT = 4 (quad): lanes 0-1 of the quad run the Q ladder as the pair does, while lanes 2-3
-//     run the same instruction stream on the comb: their accumulator starts at the first comb
-//     entry and takes one comb entry at each of the first 16 digits' mixed additions (their
-//     doublings and later additions are discarded by a select). One lean Jacobian addition of
-//     the two halves ends it: the K + 1 comb additions leave the critical path.
-// Setup (checks, Q table, scalars) and the final comparison run redundantly on all lanes of a
-// tuple. The Q table lives in LDS (one copy per tuple). One wavefront per workgroup spreads a
+// Latency kernel for small batches (sbft_launch_p256_verify with lanes = 2). A batch of a few
+// thousand tuples gives each busy SIMD one wave, so the launch takes one wave's instruction
+// stream; this kernel shortens that stream at the price of more lanes: one verify on two
+// adjacent lanes, the doublings and mixed additions split between them (p29_dbl_pair,
+// p29_add_aff_pair); u1*G by the comb after the ladder. (Round 3's four-lane form, the comb on
+// lanes 2-3 of a quad, measured no faster and is gone; the four-lane kernel now is
+// p256_verify_half_kernel.) Setup (checks, Q table, scalars) and the final comparison run
+// redundantly on both lanes of a tuple. The Q table lives in LDS (one copy per tuple). One wavefront per workgroup spreads a
 // small batch over as many CUs as possible.
 //
 // FRAMED (sbft_launch_p256_verify_framed): the tuples come straight from a framed payload, and
@@ -1056,9 +1052,8 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
                                                                              uint32_t* __restrict__ work,
                                                                              const uint4* __restrict__ gcomb,
                                                                              FramedIn fr) {
-    static_assert(LPT == 2 || LPT == 4, "two or four lanes per tuple");
-    constexpr bool kQuad = LPT == 4;
-    constexpr bool kCombWave = FRAMED && !kQuad && SBFT_PAIR_COMB_WAVE;
+    static_assert(LPT == 2, "two lanes per tuple");
+    constexpr bool kCombWave = FRAMED && SBFT_PAIR_COMB_WAVE;
     constexpr int kTuples = small_kernel_tuples<LPT, FRAMED>();  // tuples per workgroup
     constexpr unsigned kVerifyThreads = kTuples * LPT;          // the verify wavefront(s)
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
@@ -1085,14 +1080,9 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
 #pragma unroll
                 for (int k = 0; k < 8; ++k) edig[k * kTuples + lane] = h[k];
             }
-            // the verify wavefront's barriers: the Q table's, and the quad's two comb stagings or
-            // the comb wave's hand-over
+            // the verify wavefront's barriers: the Q table's and the comb wave's hand-over
             __syncthreads();
-            if constexpr (kQuad) {
-                __syncthreads();
-                __syncthreads();
-            }
-            if constexpr (kCombWave) __syncthreads();  // the comb wavefront's hand-over
+            if constexpr (kCombWave) __syncthreads();
             return;
         }
     }
@@ -1139,7 +1129,6 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
     }
     const int pr = threadIdx.x / LPT;
     const bool odd = (threadIdx.x & 1) != 0;
-    const bool comb_role = kQuad && (threadIdx.x & 2) != 0;
     const uint32_t t = blockIdx.x * kTuples + pr;
     const bool active = t < n;
     const uint32_t idx = active ? t : (n - 1);
@@ -1243,33 +1232,6 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
     }
     acc.z = f29_const(C29_ONE);
     if (neg2) f29_neg(acc.y, acc.y);
-    // quad: the tuple's K + 1 comb points (signs applied) staged in LDS over the divstep table,
-    // which the inversions are done with: [entry][x limbs, y limbs][tuple]
-    u32* const ctab = dtab;
-    static_assert(!kQuad || (kGK + 1) * 18 * kTuples <= SBFT_DIVSTEP5_WORDS, "comb points fit the divstep table");
-    static_assert(!kQuad || kGK <= kQDigits, "the comb lanes take one entry per ladder digit");
-    if constexpr (kQuad) {
-        __syncthreads();  // every lane of the workgroup is past its inversions
-        for (int e = threadIdx.x & 3; e < kGK + 1; e += 4) {
-            uint4 en[5];
-            bool dn;
-            comb_entry(e, en, dn);
-            f29 gx, gy;
-            entry_point(en, dn, gx, gy);
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                ctab[(e * 18 + k) * kTuples + pr] = gx.v[k];
-                ctab[(e * 18 + 9 + k) * kTuples + pr] = gy.v[k];
-            }
-        }
-        __syncthreads();
-        if (comb_role)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                acc.x.v[k] = ctab[k * kTuples + pr];
-                acc.y.v[k] = ctab[(9 + k) * kTuples + pr];
-            }
-    }
     const fe k2 = u2;
     bool inf = false;  // acc is the point at infinity (add_aff_fix; the pair form only)
     auto dblp = [odd](jp29& p) { p29_dbl_pair(p, p, odd); };
@@ -1286,73 +1248,37 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
         }
         if ((d2 < 0) != neg2) f29_neg(y, y);
     };
-    if constexpr (!kQuad) {
-        if (SBFT_PAIR_LANE_LOCAL && SBFT_PAIR_LADDER_DIGITS > 0) {
-            // the ladder in the lane-local form; the last digit's addition (the only one that can
-            // be exceptional) in the both-lanes form, for add_aff_fix
-            pl29 q = pl29_from(acc, odd);
+    if (SBFT_PAIR_LANE_LOCAL && SBFT_PAIR_LADDER_DIGITS > 0) {
+        // the ladder in the lane-local form; the last digit's addition (the only one that can
+        // be exceptional) in the both-lanes form, for add_aff_fix
+        pl29 q = pl29_from(acc, odd);
 #pragma unroll 1
-            for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 1; --i) {
-#pragma unroll
-                for (int d = 0; d < kQWin; ++d) p29_dbl_pl(q, odd);
-                f29 x2, y2;
-                qentry(i, x2, y2);
-                p29_add_aff_pl(q, x2, y2);
-            }
+        for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 1; --i) {
 #pragma unroll
             for (int d = 0; d < kQWin; ++d) p29_dbl_pl(q, odd);
-            pl29_to(acc, q);
             f29 x2, y2;
-            qentry(0, x2, y2);
-            p29_add_aff_pair(acc, x2, y2, odd);
-            add_aff_fix(acc, inf, dblp, [&](f29& x, f29& y) { qentry(0, x, y); });
-        } else {
-#pragma unroll 1
-            for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 0; --i) {
-#pragma unroll
-                for (int d = 0; d < kQWin; ++d) p29_dbl_pair(acc, acc, odd);
-                f29 x2, y2;
-                qentry(i, x2, y2);
-                p29_add_aff_pair(acc, x2, y2, odd);
-                if (i == 0) add_aff_fix(acc, inf, dblp, [&](f29& x, f29& y) { qentry(0, x, y); });
-            }
+            qentry(i, x2, y2);
+            p29_add_aff_pl(q, x2, y2);
         }
+#pragma unroll
+        for (int d = 0; d < kQWin; ++d) p29_dbl_pl(q, odd);
+        pl29_to(acc, q);
+        f29 x2, y2;
+        qentry(0, x2, y2);
+        p29_add_aff_pair(acc, x2, y2, odd);
+        add_aff_fix(acc, inf, dblp, [&](f29& x, f29& y) { qentry(0, x, y); });
     } else {
 #pragma unroll 1
         for (int i = SBFT_PAIR_LADDER_DIGITS - 1; i >= 0; --i) {
-            const int j = SBFT_PAIR_LADDER_DIGITS - 1 - i;  // additions done so far
 #pragma unroll
-            for (int d = 0; d < kQWin; ++d) {
-                jp29 tt;
-                p29_dbl_pair(tt, acc, odd);
-                if (!comb_role) acc = tt;
-            }
+            for (int d = 0; d < kQWin; ++d) p29_dbl_pair(acc, acc, odd);
             f29 x2, y2;
             qentry(i, x2, y2);
-            // comb lanes: entry j + 1 while j + 1 <= K, then their accumulator is final
-            const int ce = j + 1 <= kGK ? j + 1 : kGK;
-            if (comb_role)
-#pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    x2.v[k] = ctab[(ce * 18 + k) * kTuples + pr];
-                    y2.v[k] = ctab[(ce * 18 + 9 + k) * kTuples + pr];
-                }
-            jp29 tt = acc;
-            p29_add_aff_pair(tt, x2, y2, odd);
-            if (!comb_role || j + 1 <= kGK) acc = tt;
+            p29_add_aff_pair(acc, x2, y2, odd);
+            if (i == 0) add_aff_fix(acc, inf, dblp, [&](f29& x, f29& y) { qentry(0, x, y); });
         }
     }
-    if constexpr (kQuad) {
-        // lanes 0-1 add lanes 2-3's u1*G (quad_perm [2,3,2,3]); lanes 2-3 compute a discarded copy
-        jp29 g;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            g.x.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.x.v[k], 0xEE, 0xF, 0xF, false);
-            g.y.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.y.v[k], 0xEE, 0xF, 0xF, false);
-            g.z.v[k] = (u32)__builtin_amdgcn_mov_dpp((int)acc.z.v[k], 0xEE, 0xF, 0xF, false);
-        }
-        p29_add_jac_lean(acc, g);
-    } else if constexpr (kCombWave) {
+    if constexpr (kCombWave) {
         __syncthreads();  // the comb wavefront's sum is in gsum
         jp29 g;
 #pragma unroll
@@ -2082,14 +2008,10 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
         const unsigned hblocks = (n + sbft::kHalfTuples - 1) / sbft::kHalfTuples;
         hipLaunchKernelGGL(sbft::p256_verify_half_kernel<false>, dim3(hblocks), dim3(sbft::kHalfThreads), 0, stream,
                            d_digest, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, sbft::FramedIn{});
-    } else if (lanes == 2 || lanes == 4) {  // 64-lane workgroups of 32 or 16 tuples
-        const unsigned tpw = 64 / lanes, sblocks = (n + tpw - 1) / tpw;
-        if (lanes == 2)
-            hipLaunchKernelGGL(sbft::p256_verify_small_kernel<2>, dim3(sblocks), dim3(64), 0, stream, d_digest,
-                               d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, sbft::FramedIn{});
-        else
-            hipLaunchKernelGGL(sbft::p256_verify_small_kernel<4>, dim3(sblocks), dim3(64), 0, stream, d_digest,
-                               d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, sbft::FramedIn{});
+    } else if (lanes == 2) {  // 64-lane workgroups of 32 tuples
+        const unsigned sblocks = (n + 31) / 32;
+        hipLaunchKernelGGL(sbft::p256_verify_small_kernel<2>, dim3(sblocks), dim3(64), 0, stream, d_digest, d_r, d_s,
+                           d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, sbft::FramedIn{});
     } else {
         // Waves are issue-bound at 4 per SIMD, and all take the same time. When the last
         // resident round would be mostly full, a whole number of rounds with the tuples spread
@@ -2182,7 +2104,7 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
                                               hipStream_t stream, int lanes, uint32_t* h_flagged) {
     if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
-    if (lanes != 2 && lanes != 3 && lanes != 4) return -1;
+    if (lanes != 2 && lanes != 3) return -1;
     static int cus = 0;
     if (!cus) {
         int dev = 0;
@@ -2191,19 +2113,14 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
             cus = 256;
     }
     const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, pub_rel, d_dig, d_r, d_s, d_qx, d_qy, h_flagged};
-    const unsigned tpw = lanes == 3   ? (unsigned)sbft::kHalfTuples
-                         : lanes == 2 ? (unsigned)sbft::small_kernel_tuples<2, true>()
-                                      : 64 / (unsigned)lanes;
+    const unsigned tpw = lanes == 3 ? (unsigned)sbft::kHalfTuples : (unsigned)sbft::small_kernel_tuples<2, true>();
     const unsigned sblocks = (n + tpw - 1) / tpw;
     if (lanes == 3)
         hipLaunchKernelGGL((sbft::p256_verify_half_kernel<true>), dim3(sblocks), dim3(sbft::kHalfThreads), 0, stream,
                            d_dig, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
-    else if (lanes == 2)
+    else
         hipLaunchKernelGGL((sbft::p256_verify_small_kernel<2, true>), dim3(sblocks),
                            dim3((sbft::small_kernel_threads<2, true>())), 0, stream, d_dig,
-                           d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
-    else
-        hipLaunchKernelGGL((sbft::p256_verify_small_kernel<4, true>), dim3(sblocks), dim3(128), 0, stream, d_dig,
                            d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
     if (hipGetLastError() != hipSuccess) return -1;
     if (h_flagged) return 0;  // the caller launches the fixup if a tuple was flagged

@@ -220,9 +220,10 @@ class GpuVerifier:
 
     def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0, quad_max: int = 0,
                  slots_per_device: int = 0, half_max: int = 0):
-        """pair_max / quad_max: per-device batches of at most this many tuples run the latency
-        kernel with two / four lanes per tuple (0 = library default, negative = never); half_max:
-        ... the half-size-scalar kernel (four lanes: two 128-bit ladders).
+        """pair_max / half_max: per-device batches of at most this many tuples run the pair
+        latency kernel (two lanes per tuple) / the half-size-scalar kernel (four lanes: two 128-bit
+        ladders), half_max taking precedence (0 = library default, negative = never). quad_max is
+        accepted and ignored (round 3's four-lane pair form is gone).
         slots_per_device > 1: that many engine slots per GPU, each taking a share of a split
         batch as a separate device would (runs the multi-device split on one GPU)."""
         self.L = load_library()

@@ -23,9 +23,9 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 
-KERNEL_OPTS = {"lane": dict(pair_max=-1, quad_max=-1, half_max=-1),
-               "pair": dict(pair_max=1 << 30, quad_max=-1, half_max=-1),
-               "half": dict(half_max=1 << 30, quad_max=-1)}
+KERNEL_OPTS = {"lane": dict(pair_max=-1, half_max=-1),
+               "pair": dict(pair_max=1 << 30, half_max=-1),
+               "half": dict(half_max=1 << 30)}
 
 
 # ---------------------------------------------------------------- config 3

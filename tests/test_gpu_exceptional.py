@@ -44,10 +44,9 @@ def crafted():
     return cols, tags, want
 
 
-MODE_OPTS = {"lane": dict(pair_max=-1, quad_max=-1, half_max=-1),
-             "pair": dict(pair_max=1 << 30, quad_max=-1, half_max=-1),
-             "quad": dict(quad_max=1 << 30),
-             "half": dict(half_max=1 << 30, quad_max=-1)}
+MODE_OPTS = {"lane": dict(pair_max=-1, half_max=-1),
+             "pair": dict(pair_max=1 << 30, half_max=-1),
+             "half": dict(half_max=1 << 30)}
 
 
 @pytest.mark.parametrize("mode", ["lane", "pair", "half"])
@@ -111,16 +110,16 @@ def _sbr1(i: int, pl: bytes, qx: bytes, qy: bytes) -> bytes:
             len(pl).to_bytes(4, "little") + pl + b"\x04" + qx + qy)
 
 
-@pytest.mark.parametrize("mode", ["pair", "quad", "half"])
+@pytest.mark.parametrize("mode", ["pair", "half"])
 def test_crafted_exceptional_proposal(crafted, mode):
     """The crafted tuples as signed requests inside a VerifyProposal of honest ones
     (sbft_gv_framed_overlapped: fused hash + verify launch, verdicts in mapped host memory).
     SBR1 signs the client's key, so a crafted request keeps u1 = e/s and u2 = r/s (the scalars
     that make the ladder or the comb meet an exceptional addition) but not a valid r: each is a
-    rejection. The four-lane kernel joins u2 Q and u1 G with one lean Jacobian addition and has
-    no in-place repair, so these tuples are flagged and the fix-up kernel must run -- launched
-    only because the verify kernel raised the mapped flag; the two-lane kernel repairs them in
-    place. Each crafted request replaces an honest one of an all-valid proposal of the same size
+    rejection. The two-lane kernel repairs them in place; the half-size-scalar kernel meets no
+    exceptional addition on its 128-bit ladders and repairs its comb join in place, and any tuple
+    either flags goes to the fix-up kernel, launched only because the verify kernel raised the
+    mapped flag. Each crafted request replaces an honest one of an all-valid proposal of the same size
     verified just before (whose verdict bytes, all 1, are still in the mapped buffer), so a
     skipped fix-up would show as an accepted proposal; the error must name that request."""
     from smartbft_amd import GpuVerifier, plugin

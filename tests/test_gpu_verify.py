@@ -289,10 +289,9 @@ def test_throughput_grid_shapes(gpu, n):
 # ---- every verify kernel at every size: the one-lane throughput kernel and the small-batch
 # latency kernel with two and four lanes per tuple (p256_verify_small_kernel<2|4>, forced on
 # for big batches too) and the half-size-scalar kernel (p256_verify_half_kernel)
-KERNEL_OPTS = {"lane": dict(pair_max=-1, quad_max=-1, half_max=-1),
-               "pair": dict(pair_max=1 << 30, quad_max=-1, half_max=-1),
-               "quad": dict(quad_max=1 << 30),
-               "half": dict(half_max=1 << 30, quad_max=-1)}
+KERNEL_OPTS = {"lane": dict(pair_max=-1, half_max=-1),
+               "pair": dict(pair_max=1 << 30, half_max=-1),
+               "half": dict(half_max=1 << 30)}
 
 
 @pytest.fixture(scope="module", params=list(KERNEL_OPTS))
@@ -400,7 +399,7 @@ def test_framed_hash_then_verify(mode):
 @pytest.mark.parametrize("mode", list(KERNEL_OPTS))
 def test_framed_exceptional_tuples(mode):
     """Framed tuples whose Shamir sum meets an exceptional addition, through the fused
-    hash-and-verify launch (pair, quad) and the three-kernel chain (lane): the verify kernel
+    hash-and-verify launch (pair, half) and the three-kernel chain (lane): the verify kernel
     writes the flagged tuples' fields out for the fix-up kernel. With u1 = e/s, u2 = r/s:
     Q = -(e/r) G makes R = u1 G + u2 Q infinity (reject); Q = (e/r) G with s = 2e/k and
     r = x(kG) makes u2 Q = u1 G, a doubling, and the signature valid. Verdicts equal the oracle's."""

@@ -12,8 +12,12 @@
 //       SBFT_V_EVERIFY with the reference's text, everyone else 0.
 //   quorum-batch VOTES DECISIONS
 //       the batch hook: one sbft_verifier_verify_consenter_sigs call per decision.
-//   quorum-hook VOTERS NEED DECISIONS
-//       the processCommits batch hook with arriving votes (go/patches/internal_bft_commits.patch).
+//   quorum-hook VOTERS NEED DECISIONS INFLIGHT
+//       the processCommits batch hook with arriving votes (go/patches/internal_bft_commits.patch),
+//       at most INFLIGHT (default 2) batch calls in flight.
+//   quorum-pipe CHANNELS DECISIONS gpu|cpu
+//       pipelined decisions: CHANNELS consensus instances on one node, each deciding back to
+//       back (prev-commit batch, then the commit votes), all in flight at once.
 //   sign CALLS
 //       one signature at a time from one thread: sbft_signer_sign (RFC 6979, and with the
 //       pre-signature pool of 1,024) vs OpenSSL ECDSA_do_sign.
@@ -37,6 +41,7 @@
 #include <linux/futex.h>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/resource.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -138,6 +143,13 @@ static CgroupCpu cgroup_cpu() {
     }
     std::fclose(f);
     return c;
+}
+
+// this process's CPU time (user + system), microseconds
+static double proc_cpu_us() {
+    rusage ru{};
+    getrusage(RUSAGE_SELF, &ru);
+    return (ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) * 1e6 + ru.ru_utime.tv_usec + ru.ru_stime.tv_usec;
 }
 
 static void priv_of(uint64_t tag, uint8_t out[32]) {
@@ -280,126 +292,253 @@ static int quorum_gpu(int callers, int decisions, int cmax, int cwait) {
     return wrong.load() ? 2 : 0;
 }
 
-// quorum-hook VOTERS NEED DECISIONS: the patched processCommits (go/patches/internal_bft_commits.patch):
-// VOTERS threads deliver one commit vote each per decision, released together (the votes of a
-// decision arriving from the network); the collector (this thread, the View goroutine) takes
-// them in arrival order and, as soon as the valid votes so far plus the pending ones can complete
-// the quorum, verifies the pending ones with ONE sbft_verifier_verify_consenter_sigs call; after a
-// bad vote the votes that arrived meanwhile form the next call. Latency = release -> NEED valid
-// votes collected. Every 10th decision carries one bad vote (voter 7), so VOTERS = NEED + 1 lets
-// the spare vote complete that quorum, as a 67th replica's vote would at n = 100.
-static int quorum_hook(int voters, int need, int decisions) {
+// ---- the processCommits batch hook (go/patches/internal_bft_commits.patch) with arriving votes ----
+// Shared by quorum-hook and quorum-pipe. A channel (one consensus instance: its View goroutine
+// and the replicas voting in it) owns VOTERS voter threads that deliver one commit vote each per
+// decision, released together (the votes arriving from the network), and BatchWorkers that run
+// the hook's VerifyConsenterSigs calls as the patch's goroutines do, so the collector keeps
+// taking arrivals while a batch is in flight.
+struct BatchWorker {
+    std::thread th;
+    std::atomic<int> st{0};  // 0 idle, 1 posted, 2 done, 3 stop
+    sbft_verifier* v = nullptr;
+    const sbft_proposal* p = nullptr;
+    std::vector<sbft_signature> batch;
+    std::vector<int> who;
+    std::vector<int32_t> res;
+    int rc = 0;
+    void start() {
+        th = std::thread([this] {
+            for (;;) {
+                int s;
+                const auto t0 = Clock::now();
+                while ((s = st.load(std::memory_order_acquire)) != 1 && s != 3) {
+                    if (Clock::now() - t0 < std::chrono::microseconds(50)) {  // a batch follows an
+                        __builtin_ia32_pause();                               // arrival closely
+                        continue;
+                    }
+                    futex(&st, FUTEX_WAIT_PRIVATE, s);
+                }
+                if (s == 3) return;
+                res.assign(batch.size(), 0);
+                rc = sbft_verifier_verify_consenter_sigs(v, batch.data(), batch.size(), p, res.data());
+                st.store(2, std::memory_order_release);
+            }
+        });
+    }
+    void post() {
+        st.store(1, std::memory_order_release);
+        futex(&st, FUTEX_WAKE_PRIVATE, 1);
+    }
+    void stop() {
+        st.store(3, std::memory_order_release);
+        futex(&st, FUTEX_WAKE_PRIVATE, 1);
+        th.join();
+    }
+};
+
+struct HookChannel {
+    int voters, need, inflight;
+    sbft_verifier* v;
+    const std::vector<sbft_proposal>* props;
+    const std::vector<std::vector<std::vector<uint8_t>>>*msgs, *vals, *bads;
+    std::unique_ptr<std::atomic<int>[]> order;
+    std::atomic<int> arrived{0}, gen{-1};
+    std::atomic<bool> stop_{false};
+    std::vector<std::thread> th;
+    std::vector<std::unique_ptr<BatchWorker>> w;
+    int launches = 0, wrong = 0;
+
+    void start() {
+        order.reset(new std::atomic<int>[voters]);
+        for (int i = 0; i < voters; ++i) order[i].store(0);
+        for (int i = 0; i < voters; ++i)
+            th.emplace_back([this, i] {
+                int seen = -1;
+                for (;;) {
+                    int g;
+                    bool slept = false;
+                    while ((g = gen.load(std::memory_order_acquire)) == seen && !stop_.load()) {
+                        futex(&gen, FUTEX_WAIT_PRIVATE, seen);
+                        slept = true;
+                    }
+                    if (slept) futex(&gen, FUTEX_WAKE_PRIVATE, 2);  // the release is a wake-up tree
+                    if (stop_.load()) return;
+                    seen = g;
+                    const int k = arrived.fetch_add(1, std::memory_order_acq_rel);
+                    order[k].store(i + 1, std::memory_order_release);
+                }
+            });
+        for (int k = 0; k < std::max(1, inflight); ++k) {
+            w.emplace_back(new BatchWorker());
+            w.back()->v = v;
+            w.back()->start();
+        }
+    }
+    void finish() {
+        stop_.store(true);
+        gen.fetch_add(1);
+        futex(&gen, FUTEX_WAKE_PRIVATE, INT_MAX);
+        for (auto& x : th) x.join();
+        for (auto& x : w) x->stop();
+    }
+    // One decision on proposal b (voter 7's vote is bad when bad_dec): release the votes, collect
+    // NEED valid ones through the hook. Returns release -> quorum in microseconds.
+    double decide(int g, int b, bool bad_dec) {
+        for (int k = 0; k < voters; ++k) order[k].store(0, std::memory_order_relaxed);
+        arrived.store(0, std::memory_order_release);
+        const auto t0 = Clock::now();
+        gen.store(g, std::memory_order_release);
+        futex(&gen, FUTEX_WAKE_PRIVATE, 2);
+        int valid = 0, consumed = 0, in_flight = 0, in_votes = 0;
+        std::vector<int> pending;
+        auto harvest = [&](BatchWorker& x) {
+            if (x.rc) wrong++;
+            for (size_t k = 0; k < x.batch.size(); ++k) {
+                const bool is_bad = bad_dec && x.who[k] == 7;
+                if (is_bad != (x.res[k] != 0)) wrong++;
+                if (!x.res[k] && valid < need) ++valid;
+            }
+            in_flight--;
+            in_votes -= (int)x.batch.size();
+            x.st.store(0, std::memory_order_release);
+        };
+        while (valid < need) {
+            bool progress = false;
+            for (auto& x : w)
+                if (x->st.load(std::memory_order_acquire) == 2) {
+                    harvest(*x);
+                    progress = true;
+                }
+            if (valid >= need) break;
+            const int a = arrived.load(std::memory_order_acquire);
+            for (; consumed < a; ++consumed) {
+                int i;
+                while ((i = order[consumed].load(std::memory_order_acquire)) == 0) __builtin_ia32_pause();
+                pending.push_back(i - 1);
+                progress = true;
+            }
+            // the patch's canLaunch: quorum reachable, a batch slot free
+            if (!pending.empty() && in_flight < inflight && valid + in_votes + (int)pending.size() >= need) {
+                BatchWorker* x = nullptr;
+                for (auto& y : w)
+                    if (y->st.load(std::memory_order_acquire) == 0) x = y.get();
+                x->p = &(*props)[b];
+                x->batch.clear();
+                x->who.clear();
+                for (int i : pending) {
+                    const auto& val = (bad_dec && i == 7) ? (*bads)[b][i] : (*vals)[b][i];
+                    x->batch.push_back(
+                        sbft_signature{(uint64_t)(i + 2), val.data(), 64, (*msgs)[b][i].data(), (*msgs)[b][i].size()});
+                    x->who.push_back(i);
+                }
+                pending.clear();
+                in_flight++;
+                in_votes += (int)x->batch.size();
+                ++launches;
+                x->post();
+                progress = true;
+            }
+            if (!progress) {
+                if (a == voters && in_flight == 0 && pending.empty()) break;  // all in, quorum short
+                __builtin_ia32_pause();
+            }
+        }
+        const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        if (valid != need) wrong++;
+        // drain: batches still in flight and the remaining arrivals (outside the latency)
+        for (auto& x : w)
+            while (x->st.load(std::memory_order_acquire) != 0) {
+                if (x->st.load(std::memory_order_acquire) == 2) harvest(*x);
+                else __builtin_ia32_pause();
+            }
+        while (arrived.load(std::memory_order_acquire) < voters) __builtin_ia32_pause();
+        for (int k = 0; k < voters; ++k)
+            while (order[k].load(std::memory_order_acquire) == 0) __builtin_ia32_pause();
+        return us;
+    }
+};
+
+// Signed commit votes of NB proposals by consenters 2..VOTERS+1 (and a corrupted copy of each).
+struct VoteSet {
+    static constexpr int NB = 8;
+    std::vector<sbft_signer*> signers;
+    std::vector<std::string> payloads;
+    std::vector<sbft_proposal> props;
+    std::vector<std::vector<std::vector<uint8_t>>> msgs, vals, bads;
+    VoteSet(sbft_gv_ctx* ctx, sbft_verifier* v, int voters, uint64_t tag) : payloads(NB), props(NB), msgs(NB), vals(NB), bads(NB) {
+        for (int i = 1; i <= voters + 1; ++i) {
+            uint8_t d[32], pub[65];
+            priv_of(tag + i, d);
+            signers.push_back(sbft_signer_new(ctx, i, d));
+            sbft_signer_public_key(signers.back(), pub);
+            sbft_verifier_add_consenter(v, i, pub);
+        }
+        for (int b = 0; b < NB; ++b) {
+            payloads[b] = std::string(1300, (char)('a' + b + (int)(tag % 7)));
+            props[b] = sbft_proposal{(const uint8_t*)payloads[b].data(), payloads[b].size(), (const uint8_t*)"h", 1,
+                                     (const uint8_t*)"m", 1, 1};
+            for (int i = 0; i < voters; ++i) {
+                std::vector<uint8_t> m(256), sig(64);
+                size_t ml = 0;
+                sbft_signer_sign_proposal(signers[i + 1], &props[b], nullptr, 0, m.data(), m.size(), &ml, sig.data());
+                m.resize(ml);
+                msgs[b].push_back(m);
+                vals[b].push_back(sig);
+                sig[40] ^= 1;
+                bads[b].push_back(sig);
+            }
+        }
+    }
+    ~VoteSet() {
+        for (auto* s : signers) sbft_signer_free(s);
+    }
+};
+
+// quorum-hook VOTERS NEED DECISIONS INFLIGHT: the patched processCommits. VOTERS threads deliver one
+// commit vote each per decision, released together; the collector (this thread, the View
+// goroutine) takes them in arrival order and, once the valid votes so far plus the ones in flight
+// and pending can complete the quorum, hands the pending ones to a batch worker (one
+// sbft_verifier_verify_consenter_sigs call), with at most INFLIGHT calls in flight: votes that
+// arrive during a call go out as the next one at once (INFLIGHT = 1: they wait for it, the round-3
+// hook). Latency = release -> NEED valid votes collected. Every 10th decision carries one bad
+// vote (voter 7), so VOTERS = NEED + 1 lets the spare vote complete that quorum, as a 67th
+// replica's vote would at n = 100.
+static int quorum_hook(int voters, int need, int decisions, int inflight) {
     sbft_gv_ctx* ctx = nullptr;
     if (sbft_gv_init(nullptr, &ctx)) {
         std::fprintf(stderr, "no GPU\n");
         return 1;
     }
     sbft_verifier* v = sbft_verifier_new(ctx, 1);
-    std::vector<sbft_signer*> signers;
-    for (int i = 1; i <= voters + 1; ++i) {
-        uint8_t d[32], pub[65];
-        priv_of(1000 + i, d);
-        signers.push_back(sbft_signer_new(ctx, i, d));
-        sbft_signer_public_key(signers.back(), pub);
-        sbft_verifier_add_consenter(v, i, pub);
-    }
-    const int NB = 8;
-    std::vector<std::string> payloads(NB);
-    std::vector<sbft_proposal> props(NB);
-    std::vector<std::vector<std::vector<uint8_t>>> msgs(NB), vals(NB), bads(NB);
-    for (int b = 0; b < NB; ++b) {
-        payloads[b] = std::string(1300, 'a' + b);
-        props[b] = sbft_proposal{(const uint8_t*)payloads[b].data(), payloads[b].size(), (const uint8_t*)"h", 1,
-                                 (const uint8_t*)"m", 1, 1};
-        for (int i = 0; i < voters; ++i) {
-            std::vector<uint8_t> m(256), sig(64);
-            size_t ml = 0;
-            sbft_signer_sign_proposal(signers[i + 1], &props[b], nullptr, 0, m.data(), m.size(), &ml, sig.data());
-            m.resize(ml);
-            msgs[b].push_back(m);
-            vals[b].push_back(sig);
-            sig[40] ^= 1;
-            bads[b].push_back(sig);
-        }
-    }
-    std::unique_ptr<std::atomic<int>[]> order(new std::atomic<int>[voters]);
-    std::atomic<int> arrived{0}, gen{-1};
-    std::atomic<bool> stop{false};
-    std::vector<std::thread> th;
-    for (int i = 0; i < voters; ++i)
-        th.emplace_back([&, i] {
-            int seen = -1;
-            for (;;) {
-                int g;
-                bool slept = false;
-                while ((g = gen.load(std::memory_order_acquire)) == seen && !stop.load()) {
-                    futex(&gen, FUTEX_WAIT_PRIVATE, seen);
-                    slept = true;
-                }
-                if (slept) futex(&gen, FUTEX_WAKE_PRIVATE, 2);  // the release is a wake-up tree
-                if (stop.load()) return;
-                seen = g;
-                const int k = arrived.fetch_add(1, std::memory_order_acq_rel);
-                order[k].store(i + 1, std::memory_order_release);
-            }
-        });
-    std::vector<double> t;
     int wrong = 0, launches = 0;
-    std::vector<sbft_signature> batch;
-    std::vector<int> who;
-    std::vector<int32_t> st;
-    for (int g = -5; g < decisions; ++g) {
-        const int b = (g + 80) % NB;
-        const bool bad_dec = g % 10 == 9;
-        for (int k = 0; k < voters; ++k) order[k].store(0, std::memory_order_relaxed);
-        arrived.store(0, std::memory_order_release);
-        const auto t0 = Clock::now();
-        gen.store(g + 5, std::memory_order_release);
-        futex(&gen, FUTEX_WAKE_PRIVATE, 2);
-        int valid = 0, consumed = 0;
-        while (valid < need) {
-            const int a = arrived.load(std::memory_order_acquire);
-            if (a == consumed || valid + (a - consumed) < need) {
-                if (a == voters) break;  // every vote is in and the quorum is still short
-                __builtin_ia32_pause();
-                continue;
-            }
-            batch.clear();
-            who.clear();
-            for (int k = consumed; k < a; ++k) {
-                int i;
-                while ((i = order[k].load(std::memory_order_acquire)) == 0) __builtin_ia32_pause();
-                --i;
-                const auto& val = (bad_dec && i == 7) ? bads[b][i] : vals[b][i];
-                batch.push_back(sbft_signature{(uint64_t)(i + 2), val.data(), 64, msgs[b][i].data(), msgs[b][i].size()});
-                who.push_back(i);
-            }
-            consumed = a;
-            st.assign(batch.size(), 0);
-            if (sbft_verifier_verify_consenter_sigs(v, batch.data(), batch.size(), &props[b], st.data())) wrong++;
-            ++launches;
-            for (size_t k = 0; k < batch.size(); ++k) {
-                const bool is_bad = bad_dec && who[k] == 7;
-                if (is_bad != (st[k] != 0)) wrong++;
-                if (!st[k] && valid < need) ++valid;
-            }
+    std::vector<double> t;
+    {
+        VoteSet vs(ctx, v, voters, 1000);
+        HookChannel ch;
+        ch.voters = voters;
+        ch.need = need;
+        ch.inflight = std::max(1, inflight);
+        ch.v = v;
+        ch.props = &vs.props;
+        ch.msgs = &vs.msgs;
+        ch.vals = &vs.vals;
+        ch.bads = &vs.bads;
+        ch.start();
+        for (int g = -5; g < decisions; ++g) {
+            if (g == 0) ch.launches = 0;
+            const double us = ch.decide(g + 5, (g + 80) % VoteSet::NB, g % 10 == 9);
+            if (g >= 0) t.push_back(us);
         }
-        const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
-        if (valid != need) wrong++;
-        while (arrived.load(std::memory_order_acquire) < voters) __builtin_ia32_pause();
-        for (int k = 0; k < voters; ++k)
-            while (order[k].load(std::memory_order_acquire) == 0) __builtin_ia32_pause();
-        if (g >= 0) t.push_back(us);
-        else launches = 0;
+        ch.finish();
+        wrong = ch.wrong;
+        launches = ch.launches;
     }
-    stop.store(true);
-    gen.fetch_add(1);
-    futex(&gen, FUTEX_WAKE_PRIVATE, INT_MAX);
-    for (auto& x : th) x.join();
-    std::printf("{\"mode\": \"quorum-hook\", \"voters\": %d, \"need\": %d, \"decisions\": %d, \"p50_ms\": %.4f, "
-                "\"p99_ms\": %.4f, \"launches_per_decision\": %.2f, \"wrong_verdicts\": %d}\n",
-                voters, need, decisions, pct(t, 50) / 1e3, pct(t, 99) / 1e3, (double)launches / decisions, wrong);
-    for (auto* s : signers) sbft_signer_free(s);
+    std::printf("{\"mode\": \"quorum-hook\", \"voters\": %d, \"need\": %d, \"decisions\": %d, \"inflight\": %d, "
+                "\"p50_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f, \"launches_per_decision\": %.2f, "
+                "\"wrong_verdicts\": %d}\n",
+                voters, need, decisions, std::max(1, inflight), pct(t, 50) / 1e3, pct(t, 99) / 1e3, pct(t, 100) / 1e3,
+                (double)launches / decisions, wrong);
     sbft_verifier_free(v);
     sbft_gv_destroy(ctx);
     return wrong ? 2 : 0;
@@ -478,6 +617,173 @@ static int quorum_cpu(int callers, int decisions, int threads) {
                 "\"p99_ms\": %.4f, \"rejected\": %d}\n",
                 callers, decisions, nt, pct(t, 50) / 1e3, pct(t, 99) / 1e3, bad.load());
     return 0;
+}
+
+// quorum-pipe CHANNELS DECISIONS gpu|cpu: pipelined decisions at n = 100 (config 4). CHANNELS
+// consensus instances on one node (e.g. one SmartBFT orderer per channel, sharing the node's
+// cores and GPU) each decide back to back, so CHANNELS decisions are always in flight. A
+// decision is what the View verifies per block: the previous decision's 67 commit signatures
+// (verifyPrevCommitSignatures, view.go:606-647), then 66 of the 67 arriving commit votes
+// (processCommits, view.go:519-551; every 10th decision has a bad vote).
+//   gpu: the patched library: one VerifyConsenterSigs call for the 67 prev-commit signatures,
+//        the processCommits hook (quorum-hook, two batches in flight) for the votes.
+//   cpu: the stock library with an OpenSSL plugin: the prev-commit loop verifies serially on
+//        the View goroutine; every vote is verified by its own goroutine (a voter thread here),
+//        and the View continues once 66 are valid.
+// Reports decisions/s over all channels, p50/p99 per decision and CPU ms per decision (cgroup).
+static int quorum_pipe(int channels, int decisions, bool gpu) {
+    const int voters = 67, need = 66;
+    channels = std::max(1, channels);
+    std::vector<std::vector<double>> lat(channels);
+    std::atomic<int> wrong{0};
+    double wall_s = 0, cpu0 = 0, cpu1 = 0;
+    CgroupCpu cg0, cg1;
+    int launches = 0;
+    if (gpu) {
+        sbft_gv_ctx* ctx = nullptr;
+        if (sbft_gv_init(nullptr, &ctx)) {
+            std::fprintf(stderr, "no GPU\n");
+            return 1;
+        }
+        std::vector<sbft_verifier*> vs;
+        std::vector<std::unique_ptr<VoteSet>> sets;
+        std::vector<std::unique_ptr<HookChannel>> chs;
+        for (int c = 0; c < channels; ++c) {
+            vs.push_back(sbft_verifier_new(ctx, 1));
+            sets.emplace_back(new VoteSet(ctx, vs[c], voters, 5000 + 1000 * (uint64_t)c));
+            chs.emplace_back(new HookChannel());
+            HookChannel& ch = *chs.back();
+            ch.voters = voters;
+            ch.need = need;
+            ch.inflight = 2;
+            ch.v = vs[c];
+            ch.props = &sets[c]->props;
+            ch.msgs = &sets[c]->msgs;
+            ch.vals = &sets[c]->vals;
+            ch.bads = &sets[c]->bads;
+            ch.start();
+        }
+        auto run = [&](int c, int from, int to) {
+            HookChannel& ch = *chs[c];
+            VoteSet& s = *sets[c];
+            std::vector<sbft_signature> prev(voters);
+            std::vector<int32_t> st(voters);
+            for (int g = from; g < to; ++g) {
+                const int b = (g + 80) % VoteSet::NB, pb = (g + 79) % VoteSet::NB;
+                const auto t0 = Clock::now();
+                for (int i = 0; i < voters; ++i)  // the previous block's commit signatures
+                    prev[i] = sbft_signature{(uint64_t)(i + 2), s.vals[pb][i].data(), 64, s.msgs[pb][i].data(),
+                                             s.msgs[pb][i].size()};
+                if (sbft_verifier_verify_consenter_sigs(vs[c], prev.data(), voters, &s.props[pb], st.data())) wrong++;
+                for (int i = 0; i < voters; ++i) wrong += st[i] != 0;
+                ch.decide(g + 10, b, g % 10 == 9);
+                if (g >= 0) lat[c].push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+            }
+        };
+        {  // warm-up
+            std::vector<std::thread> th;
+            for (int c = 0; c < channels; ++c) th.emplace_back(run, c, -5, 0);
+            for (auto& t : th) t.join();
+        }
+        for (auto& ch : chs) ch->launches = 0;
+        cg0 = cgroup_cpu();
+        cpu0 = proc_cpu_us();
+        const auto t0 = Clock::now();
+        {
+            std::vector<std::thread> th;
+            for (int c = 0; c < channels; ++c) th.emplace_back(run, c, 0, decisions);
+            for (auto& t : th) t.join();
+        }
+        wall_s = std::chrono::duration<double>(Clock::now() - t0).count();
+        cpu1 = proc_cpu_us();
+        cg1 = cgroup_cpu();
+        for (auto& ch : chs) {
+            ch->finish();
+            wrong += ch->wrong;
+            launches += ch->launches;
+        }
+        sets.clear();
+        for (auto* v : vs) sbft_verifier_free(v);
+        sbft_gv_destroy(ctx);
+    } else {
+        // per channel: 67 prev-commit tuples (serial loop) and 67 vote tuples (one thread each)
+        std::vector<std::vector<CpuTuple>> prev(channels), votes(channels);
+        for (int c = 0; c < channels; ++c) {
+            prev[c] = cpu_tuples(voters, 128, 128);
+            votes[c] = cpu_tuples(voters, 128, 128);
+        }
+        const int total = decisions + 5;
+        std::vector<std::unique_ptr<std::atomic<int>[]>> valid(channels);
+        for (int c = 0; c < channels; ++c) {
+            valid[c].reset(new std::atomic<int>[total]);
+            for (int k = 0; k < total; ++k) valid[c][k].store(0);
+        }
+        std::vector<std::unique_ptr<std::atomic<int>>> gen;
+        for (int c = 0; c < channels; ++c) gen.emplace_back(new std::atomic<int>(-1));
+        std::atomic<bool> stop{false};
+        std::vector<std::thread> vth;
+        for (int c = 0; c < channels; ++c)
+            for (int i = 0; i < voters; ++i)
+                vth.emplace_back([&, c, i] {
+                    int seen = -1;
+                    for (;;) {
+                        int g;
+                        while ((g = gen[c]->load(std::memory_order_acquire)) == seen && !stop.load())
+                            futex(gen[c].get(), FUTEX_WAIT_PRIVATE, seen);
+                        if (stop.load()) return;
+                        for (int k = seen + 1; k <= g; ++k) {  // every decision released since
+                            const bool bad = k % 10 == 4 && i == 7;
+                            if (cpu_verify(votes[c][i]) && !bad) valid[c][k].fetch_add(1, std::memory_order_acq_rel);
+                        }
+                        seen = g;
+                    }
+                });
+        auto run = [&](int c, int from, int to) {
+            for (int g = from; g < to; ++g) {
+                const auto t0 = Clock::now();
+                for (int i = 0; i < voters; ++i) wrong += !cpu_verify(prev[c][i]);  // serial (view.go:630-644)
+                gen[c]->store(g, std::memory_order_release);
+                futex(gen[c].get(), FUTEX_WAKE_PRIVATE, INT_MAX);
+                while (valid[c][g].load(std::memory_order_acquire) < need) __builtin_ia32_pause();
+                if (g >= 5) lat[c].push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+            }
+        };
+        {
+            std::vector<std::thread> th;
+            for (int c = 0; c < channels; ++c) th.emplace_back(run, c, 0, 5);
+            for (auto& t : th) t.join();
+        }
+        cg0 = cgroup_cpu();
+        cpu0 = proc_cpu_us();
+        const auto t0 = Clock::now();
+        {
+            std::vector<std::thread> th;
+            for (int c = 0; c < channels; ++c) th.emplace_back(run, c, 5, total);
+            for (auto& t : th) t.join();
+        }
+        wall_s = std::chrono::duration<double>(Clock::now() - t0).count();
+        cpu1 = proc_cpu_us();
+        cg1 = cgroup_cpu();
+        stop.store(true);
+        for (int c = 0; c < channels; ++c) {
+            gen[c]->fetch_add(1);
+            futex(gen[c].get(), FUTEX_WAKE_PRIVATE, INT_MAX);
+        }
+        for (auto& t : vth) t.join();
+        for (int c = 0; c < channels; ++c)
+            for (int k = 5; k < total; ++k)
+                if (valid[c][k].load() < need) wrong++;
+    }
+    std::vector<double> all;
+    for (auto& l : lat) all.insert(all.end(), l.begin(), l.end());
+    const double nd = (double)channels * decisions;
+    std::printf("{\"mode\": \"quorum-pipe\", \"backend\": \"%s\", \"channels\": %d, \"decisions_per_channel\": %d, "
+                "\"decisions_per_s\": %.1f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"cpu_ms_per_decision\": %.3f, "
+                "\"launches_per_decision\": %.2f, \"cgroup_throttled\": %lld, \"wrong_verdicts\": %d}\n",
+                gpu ? "gpu" : "cpu", channels, decisions, nd / wall_s, pct(all, 50) / 1e3, pct(all, 99) / 1e3,
+                (cpu1 - cpu0) / 1e3 / nd, gpu ? 1.0 + (double)launches / nd : 0.0,
+                cg1.nr_throttled - cg0.nr_throttled, wrong.load());
+    return wrong.load() ? 2 : 0;
 }
 
 // sign CALLS: SignProposal's signing (view.go:481) one message at a time from one thread:
@@ -681,15 +987,16 @@ static int parse_cpu(int requests, int iters) {
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-hook|sign|quorum-cpu|proposal-cpu|proposal-gpu|parse-cpu ...\n", argv[0]);
+        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-hook|quorum-pipe|sign|quorum-cpu|proposal-cpu|proposal-gpu|parse-cpu ...\n", argv[0]);
         return 1;
     }
     const std::string mode = argv[1];
     auto arg = [&](int i, int def) { return argc > i ? std::atoi(argv[i]) : def; };
     if (mode == "quorum-gpu") return quorum_gpu(arg(2, 66), arg(3, 200), arg(4, 0), arg(5, 0));
     if (mode == "quorum-batch") return quorum_batch(arg(2, 67), arg(3, 200));
-    if (mode == "quorum-hook") return quorum_hook(arg(2, 67), arg(3, 66), arg(4, 200));
+    if (mode == "quorum-hook") return quorum_hook(arg(2, 67), arg(3, 66), arg(4, 200), arg(5, 2));
     if (mode == "sign") return sign_both(arg(2, 200));
+    if (mode == "quorum-pipe") return quorum_pipe(arg(2, 2), arg(3, 200), !(argc > 4 && !std::strcmp(argv[4], "cpu")));
     if (mode == "quorum-cpu") return quorum_cpu(arg(2, 66), arg(3, 200), arg(4, 66));
     if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
     if (mode == "proposal-gpu") return proposal_gpu(arg(2, 3000), arg(3, 20));

@@ -10,9 +10,9 @@ from smartbft_amd.workload import make_workload
 
 check = "--no-check" not in sys.argv
 sizes = [int(x) for x in sys.argv[1:] if not x.startswith("--")] or [64, 1000, 4096, 10000, 20000, 32768, 49152, 65536, 131072]
-g = {"lane": GpuVerifier(device_mask=1, pair_max=-1, quad_max=-1),
-     "pair": GpuVerifier(device_mask=1, pair_max=1 << 30, quad_max=-1),
-     "quad": GpuVerifier(device_mask=1, quad_max=1 << 30)}
+g = {"lane": GpuVerifier(device_mask=1, pair_max=-1, half_max=-1),
+     "pair": GpuVerifier(device_mask=1, pair_max=1 << 30, half_max=-1),
+     "half": GpuVerifier(device_mask=1, half_max=1 << 30)}
 wl = make_workload(g["lane"], max(sizes))
 dev = torch.device("cuda:0")
 for n in sizes:
