@@ -56,10 +56,11 @@ def parse():
                     help="skip the multi-stream sustained rate (its concurrent launches would mix into a profile)")
     ap.add_argument("--sha-messages", type=int, default=2_097_152,
                     help="config 5: 16M requests over 8 GPUs = 2M per GPU (~68 GB of payload in HBM)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="process group for the barrier and the max-time reduction (no data-path "
-                         "collective); gloo lets a one-GPU box rehearse the torchrun path with "
-                         "several ranks on its one device")
+    ap.add_argument("--dist-backend", default="gloo", choices=["gloo", "nccl"],
+                    help="process group for the barrier and the max-time reduction, the only "
+                         "cross-rank traffic (no data-path collective: SURVEY.md 8(e)). gloo (host "
+                         "TCP, default) keeps RCCL out of the process entirely, as north_star has "
+                         "it; nccl (= RCCL) is kept for A/B only")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_verify_latest.json"))
     ap.add_argument("--logical-slots", type=int, default=1,
                     help="rehearsal of the multi-device path on one GPU: K engine slots on the device "
@@ -320,6 +321,11 @@ def latency_configs(gv, calls: int):
     arr = (plugin._Signature * q)(*[plugin._sig(sg, keep) for sg in sigs])
     st = (ctypes.c_int32 * q)()
     cblock = plugin._prop(block, keep)
+    # warm-up: small keyed batches rotate over the engine's four zero-copy lanes, and a lane's
+    # first call allocates its mapped buffer (~0.3-0.6 ms): three first calls inside 200 timed
+    # ones were the 0.34-0.65 ms p99 of rounds 2-3 (the C harness warms up, hence its 0.065)
+    for _ in range(8):
+        assert v.L.sbft_verifier_verify_consenter_sigs(v.h, arr, q, ctypes.byref(cblock), st) == 0
     ts, tp = [], []
     for _ in range(calls):
         t0 = time.perf_counter()
@@ -349,13 +355,25 @@ def latency_configs(gv, calls: int):
     # (:834), released together per decision (tools/latency_harness quorum-gpu); stock = one
     # launch per call, coalesced = sbft_verifier_coalesce_consenter_sigs(66, 50 us)
     # the patched processCommits (go/patches/internal_bft_commits.patch): 67 votes arrive per
-    # decision, the collector verifies them in one call once 66 can complete the quorum (a
-    # second call after a bad vote); latency = release -> 66 valid votes
-    hook = _harness("quorum-hook", 67, 66, calls)
+    # decision, the collector hands them to one call once 66 can complete the quorum, and votes
+    # arriving while it is in flight to a second, overlapped one (a decision with a bad vote);
+    # latency = release -> 66 valid votes
+    hook = _harness("quorum-hook", 67, 66, calls, 2)
     if hook:
         assert hook["wrong_verdicts"] == 0
         out["commit_quorum_n100_hook"] = dict(hook, path="sbft_verifier_verify_consenter_sigs from the collector "
-                                                         "as votes arrive (processCommits batch hook)")
+                                                         "as votes arrive (processCommits batch hook, 2 in flight)")
+    # pipelined decisions (config 4): 2 consensus instances deciding back to back on the node
+    # (prev-commit batch of 67, then 66 arriving votes each); GPU (patched library) against
+    # OpenSSL (stock library: serial prev-commit loop, a thread per vote) on the same cores
+    pipe = {b: _harness("quorum-pipe", 2, max(100, calls), b) for b in ("gpu", "cpu")}
+    if pipe["gpu"] and pipe["cpu"]:
+        assert pipe["gpu"]["wrong_verdicts"] == 0 and pipe["cpu"]["wrong_verdicts"] == 0
+        out["commit_quorum_n100_pipelined"] = {
+            "gpu": pipe["gpu"], "cpu_openssl": pipe["cpu"],
+            "decisions_per_s_vs_cpu": round(pipe["gpu"]["decisions_per_s"] / pipe["cpu"]["decisions_per_s"], 2),
+            "path": "tools/latency_harness quorum-pipe: 2 channels x back-to-back decisions, each = "
+                    "verifyPrevCommitSignatures (67) + processCommits (66 of 67 arriving votes)"}
     stock = _harness("quorum-gpu", 66, calls, 0, 0)
     coal = _harness("quorum-gpu", 66, calls, 66, 50)
     if stock and coal:

@@ -685,15 +685,26 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     // key id 0: the generator G (its comb table serves u1*G on the keyed path)
     ctx->keys.push_back(kGXY);
     ctx->key_valid.push_back(1);
+    // The self-test (which also builds each device's 2 GB G comb, ~0.43 s) runs on every slot at
+    // once, one host thread per slot: an 8-GPU node starts in one device's time, not eight.
+    // Slots of one device share its comb (built once, under the owner's lock).
     const char* st = getenv("SBFT_GV_SELFTEST");
     if (!st || std::strcmp(st, "0") != 0) {
-        for (Slot* sl : ctx->slots) {
-            const int rc = power_on_selftest(sl);
+        std::vector<int> rcs(ctx->slots.size(), SBFT_GV_OK);
+        std::vector<std::thread> th;
+        try {
+            for (size_t i = 1; i < ctx->slots.size(); ++i)
+                th.emplace_back([&, i] { rcs[i] = power_on_selftest(ctx->slots[i]); });
+        } catch (...) {  // no thread: the remaining slots are tested on this one
+            for (size_t i = th.size() + 1; i < ctx->slots.size(); ++i) rcs[i] = power_on_selftest(ctx->slots[i]);
+        }
+        rcs[0] = power_on_selftest(ctx->slots[0]);
+        for (auto& t : th) t.join();
+        for (int rc : rcs)
             if (rc) {
                 sbft_gv_destroy(ctx);
                 return rc;
             }
-        }
     }
     // SBFT_GV_FAULT=nomem|launch|sync[:count] (tests): armed once the self-test has passed
     if (const char* e = getenv("SBFT_GV_FAULT")) {

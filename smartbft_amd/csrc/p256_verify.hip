@@ -1430,6 +1430,15 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     __shared__ u32 hsc[17 * T];                 // the helper's scalars: [k_A 0..7, k_B 0..7, flags][tuple]
     __shared__ u32 gsum[28 * T];                // the helper's (v u1) G: [x, y, z limbs, inf][tuple]
     inv::stage_divstep_table(dtab);  // ends with a barrier
+#ifdef SBFT_HALF_PROBE  // development: phase times of workgroup 0 (tools/half_probe.py), 100 MHz ticks
+    const uint64_t probe_t0 = __builtin_amdgcn_s_memrealtime();
+    auto probe = [&](const char* what, bool me) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        if (me && blockIdx.x == 0) printf("half-probe %s %llu\n", what, (unsigned long long)(t - probe_t0));
+    };
+#else
+    auto probe = [](const char*, bool) {};
+#endif
 
     auto load_tuple = [&](uint32_t idx, fe& r, fe& s, fe& qx, fe& qy) {
         if constexpr (FRAMED) {
@@ -1484,6 +1493,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         } else {
             e_raw = load_be32(digest + 32ull * ic);
         }
+        probe("helper_hash", lane == 0);
         const bool valid = verify_inputs_valid(r, s, qx, qy);
         fe one = fe_zero();
         one.v[0] = 1;
@@ -1496,6 +1506,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         fn_mul(u2, r, wm);
         fn_canon(u2, u2);
         if (!valid) u2 = one;
+        probe("helper_sinv", lane == 0);
         hgcd::state hs;
         hgcd::init(hs, u2.v);
 #pragma unroll 1
@@ -1516,6 +1527,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             fn_canon(t, t);
             good = good && fe_eq(t, vneg ? mod_n_neg(w) : w);
         }
+        probe("helper_hgcd", lane == 0);
         fn_mul(c, vr, u1);  // |v| u1
         fn_canon(c, c);
         if (vneg && !fe_is_zero_raw(c)) c = mod_n_neg(c);
@@ -1535,7 +1547,9 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             }
             hsc[16 * T + lane] = (vneg ? 1u : 0u) | (fb ? 2u : 0u);
         }
+        probe("helper_published", lane == 0);
         __syncthreads();  // #1: the scalars are in hsc (the verify wavefronts' tables in qtab)
+        probe("helper_barrier1", lane == 0);
         // c G on the comb, in comb_add_u1g's odd recoding (even c -> n - c, base negated; c = 0
         // becomes n, whose comb sum cancels to infinity)
         const bool neg1 = (c.v[0] & 1u) == 0;
@@ -1554,6 +1568,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             }
             gsum[27 * T + lane] = ginf ? 1u : 0u;
         }
+        probe("helper_comb", lane == 0);
         __syncthreads();  // #2: hand-over to the verify wavefronts
         return;
     }
@@ -1583,7 +1598,9 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         for (int i = 0; i < 9; ++i) rhs.v[i] = t3.v[i] - 3u * rm.v[i] + b.v[i];  // |limb| < 2^31, |.| < 2^259
         f29_normalize(rhs, rhs);                                                  // N'
     }
+    probe("verify_inputs", tid == 0);
     f29_sqrt_chain(y0, rhs);
+    probe("verify_sqrt", tid == 0);
     bool has_r0;  // x = r is on the curve
     {
         f29 yy, d;
@@ -1614,7 +1631,9 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                 qtab[(m * 18 + 9 + k) * 2 * T + col] = ty[m].v[k];
             }
     }
+    probe("verify_tables", tid == 0);
     __syncthreads();  // #1: tables in qtab, the helper's scalars in hsc
+    probe("verify_barrier1", tid == 0);
 
     const u32 flags = hsc[16 * T + pr];
     const bool fb = (flags & 2u) != 0;
@@ -1686,6 +1705,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             inf = inf2;
         }
     }
+    probe("verify_ladder", tid == 0);
     jp29 V;  // pair B's v R0 on pair A's lanes (quad_perm [2,3,2,3])
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
@@ -1694,6 +1714,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     }
 
     __syncthreads();  // #2: the helper's (v u1) G is in gsum
+    probe("verify_barrier2", tid == 0);
     {
         jp29 g;
 #pragma unroll
@@ -1741,6 +1762,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         accept = false;
         exc = false;
     }
+    probe("verify_final", tid == 0);
     if (active && (tid & 3) == 0) {
         if (exc && valid) {
             if constexpr (FRAMED) {  // the fixup kernel's inputs
