@@ -1430,14 +1430,26 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     __shared__ u32 hsc[17 * T];                 // the helper's scalars: [k_A 0..7, k_B 0..7, flags][tuple]
     __shared__ u32 gsum[28 * T];                // the helper's (v u1) G: [x, y, z limbs, inf][tuple]
     inv::stage_divstep_table(dtab);  // ends with a barrier
-#ifdef SBFT_HALF_PROBE  // development: phase times of workgroup 0 (tools/half_probe.py), 100 MHz ticks
+#ifdef SBFT_HALF_PROBE  // development: phase times of workgroup 0 (tools/half_probe.py), 100 MHz ticks,
+                        // kept in registers and printed once at the end (a printf is a blocking host call)
     const uint64_t probe_t0 = __builtin_amdgcn_s_memrealtime();
-    auto probe = [&](const char* what, bool me) {
-        const uint64_t t = __builtin_amdgcn_s_memrealtime();
-        if (me && blockIdx.x == 0) printf("half-probe %s %llu\n", what, (unsigned long long)(t - probe_t0));
+    uint32_t probe_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int probe_n = 0;
+    auto probe = [&](const char*, bool) {
+        const uint32_t t = (uint32_t)(__builtin_amdgcn_s_memrealtime() - probe_t0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (i == probe_n) probe_t[i] = t;
+        ++probe_n;
+    };
+    auto probe_dump = [&](const char* who, bool me) {
+        if (me && blockIdx.x == 0)
+            printf("half-probe %s %u %u %u %u %u %u %u %u\n", who, probe_t[0], probe_t[1], probe_t[2], probe_t[3],
+                   probe_t[4], probe_t[5], probe_t[6], probe_t[7]);
     };
 #else
     auto probe = [](const char*, bool) {};
+    auto probe_dump = [](const char*, bool) {};
 #endif
 
     auto load_tuple = [&](uint32_t idx, fe& r, fe& s, fe& qx, fe& qy) {
@@ -1570,6 +1582,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         }
         probe("helper_comb", lane == 0);
         __syncthreads();  // #2: hand-over to the verify wavefronts
+        probe_dump("helper hash,sinv,hgcd,published,barrier1,comb", lane == 0);
         return;
     }
 
@@ -1763,6 +1776,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         exc = false;
     }
     probe("verify_final", tid == 0);
+    probe_dump("verify inputs,sqrt,tables,barrier1,ladder,barrier2,final", tid == 0);
     if (active && (tid & 3) == 0) {
         if (exc && valid) {
             if constexpr (FRAMED) {  // the fixup kernel's inputs
