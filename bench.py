@@ -755,23 +755,29 @@ def main():
                     lat["commit_quorum_n100_concurrent_singles"]["cpu_openssl"] = qc
                     lat["commit_quorum_n100_concurrent_singles"]["speedup_p50_vs_cpu"] = round(
                         qc["p50_ms"] / lat["commit_quorum_n100_concurrent_singles"]["coalesced"]["p50_ms"], 1)
-                if qc and "commit_quorum_n100_hook" in lat:
-                    h = lat["commit_quorum_n100_hook"]
-                    h["cpu_openssl"] = qc
-                    h["speedup_p50_vs_cpu"] = round(qc["p50_ms"] / h["p50_ms"], 2)
-                    h["speedup_p99_vs_cpu"] = round(qc["p99_ms"] / h["p99_ms"], 2)
-                    # the stock library's own shape: one goroutine per vote, and Go sizes
-                    # GOMAXPROCS by the affinity mask, not the cgroup quota -- so on a box whose
-                    # mask is wider than its quota the 66 verifies run on 66 CPUs at once
+                if "commit_quorum_n100_hook" in lat:
+                    # the hook's own scenario on the CPU (tools/latency_harness quorum-vote-cpu):
+                    # the same 67 votes released per decision, each verified as it arrives, 66
+                    # valid close it, every 10th decision with a bad vote -- on the job's cores,
+                    # and with one thread per vote as the stock library's goroutines would run:
+                    # Go sizes GOMAXPROCS by the affinity mask, not the cgroup quota, so on a box
+                    # whose mask is wider than its quota the 67 verifies run on 67 CPUs at once
                     # (bursting past the quota, which a 16-core machine could not do)
-                    if cores < 66 and host_cores().get("affinity", 0) >= 66:
-                        q66 = _harness("quorum-cpu", 66, 200, 66)
-                        if q66:
-                            q66["note"] = ("66 threads on a %d-CPU affinity mask, %s-core quota"
+                    h = lat["commit_quorum_n100_hook"]
+                    calls = h.get("decisions", 200)
+                    qv = _harness("quorum-vote-cpu", 67, 66, calls, cores)
+                    if qv:
+                        h["cpu_openssl"] = qv
+                        h["speedup_p50_vs_cpu"] = round(qv["p50_ms"] / h["p50_ms"], 2)
+                        h["speedup_p99_vs_cpu"] = round(qv["p99_ms"] / h["p99_ms"], 2)
+                    if cores < 67 and host_cores().get("affinity", 0) >= 67:
+                        q67 = _harness("quorum-vote-cpu", 67, 66, calls, 67)
+                        if q67:
+                            q67["note"] = ("67 threads on a %d-CPU affinity mask, %s-core quota"
                                            % (host_cores()["affinity"], host_cores().get("cgroup_quota_cores")))
-                            h["cpu_openssl_thread_per_vote"] = q66
-                            h["speedup_p50_vs_cpu_thread_per_vote"] = round(q66["p50_ms"] / h["p50_ms"], 2)
-                            h["speedup_p99_vs_cpu_thread_per_vote"] = round(q66["p99_ms"] / h["p99_ms"], 2)
+                            h["cpu_openssl_thread_per_vote"] = q67
+                            h["speedup_p50_vs_cpu_thread_per_vote"] = round(q67["p50_ms"] / h["p50_ms"], 2)
+                            h["speedup_p99_vs_cpu_thread_per_vote"] = round(q67["p99_ms"] / h["p99_ms"], 2)
             rec["latency"] = lat
         print(json.dumps(rec), flush=True)
     if world > 1:

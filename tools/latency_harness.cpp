@@ -25,6 +25,10 @@
 //       the same fan-out with the verify on the CPU: CALLERS votes verified by THREADS
 //       workers (one thread per vote when THREADS >= CALLERS), SHA-256(Msg) + ECDSA_do_verify
 //       each, keys pre-materialised.
+//   quorum-vote-cpu VOTERS NEED DECISIONS THREADS
+//       quorum-hook's scenario on the CPU: VOTERS votes released per decision, each verified as
+//       it arrives (one thread per vote, or a pool of THREADS), NEED valid ones close it; every
+//       10th decision has a bad vote, as in quorum-hook.
 //   proposal-cpu REQUESTS DECISIONS THREADS
 //   proposal-gpu REQUESTS DECISIONS
 //   parse-cpu    REQUESTS ITERS
@@ -307,13 +311,15 @@ struct BatchWorker {
     std::vector<int> who;
     std::vector<int32_t> res;
     int rc = 0;
+    const std::atomic<int>* armed = nullptr;  // the channel's decision is collecting: stay awake
     void start() {
         th = std::thread([this] {
             for (;;) {
                 int s;
                 const auto t0 = Clock::now();
                 while ((s = st.load(std::memory_order_acquire)) != 1 && s != 3) {
-                    if (Clock::now() - t0 < std::chrono::microseconds(50)) {  // a batch follows an
+                    if ((armed && armed->load(std::memory_order_relaxed)) ||
+                        Clock::now() - t0 < std::chrono::microseconds(50)) {  // a batch follows an
                         __builtin_ia32_pause();                               // arrival closely
                         continue;
                     }
@@ -339,6 +345,11 @@ struct BatchWorker {
 
 struct HookChannel {
     int voters, need, inflight;
+    // SBFT_HOOK_ARM=1: the batch workers spin from the release of a decision's votes until its
+    // quorum (one core each while collecting) instead of sleeping until a batch is posted; the
+    // futex wake of a sleeping worker otherwise lies on every decision's critical path
+    std::atomic<int> armed{0};
+    bool arm = false;
     sbft_verifier* v;
     const std::vector<sbft_proposal>* props;
     const std::vector<std::vector<std::vector<uint8_t>>>*msgs, *vals, *bads;
@@ -369,9 +380,12 @@ struct HookChannel {
                     order[k].store(i + 1, std::memory_order_release);
                 }
             });
+        const char* e = std::getenv("SBFT_HOOK_ARM");
+        arm = e && std::atoi(e) != 0;
         for (int k = 0; k < std::max(1, inflight); ++k) {
             w.emplace_back(new BatchWorker());
             w.back()->v = v;
+            w.back()->armed = &armed;
             w.back()->start();
         }
     }
@@ -390,6 +404,10 @@ struct HookChannel {
         const auto t0 = Clock::now();
         gen.store(g, std::memory_order_release);
         futex(&gen, FUTEX_WAKE_PRIVATE, 2);
+        if (arm) {
+            armed.store(1, std::memory_order_relaxed);
+            for (auto& x : w) futex(&x->st, FUTEX_WAKE_PRIVATE, 1);
+        }
         int valid = 0, consumed = 0, in_flight = 0, in_votes = 0;
         std::vector<int> pending;
         auto harvest = [&](BatchWorker& x) {
@@ -445,6 +463,7 @@ struct HookChannel {
             }
         }
         const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        armed.store(0, std::memory_order_relaxed);
         if (valid != need) wrong++;
         // drain: batches still in flight and the remaining arrivals (outside the latency)
         for (auto& x : w)
@@ -617,6 +636,71 @@ static int quorum_cpu(int callers, int decisions, int threads) {
                 "\"p99_ms\": %.4f, \"rejected\": %d}\n",
                 callers, decisions, nt, pct(t, 50) / 1e3, pct(t, 99) / 1e3, bad.load());
     return 0;
+}
+
+// quorum-vote-cpu VOTERS NEED DECISIONS THREADS: the stock processCommits with an OpenSSL plugin,
+// under the same arrivals as quorum-hook: VOTERS votes released together per decision (a
+// wake-up tree), every vote verified as it arrives (view.go:537-541: a goroutine per vote; with
+// THREADS < VOTERS a pool of THREADS, thread j taking votes j, j + THREADS, ...), and the View
+// continuing once NEED are valid. Every 10th decision carries one bad vote (voter 7), as in
+// quorum-hook, so those decisions wait for the spare vote. Latency = release -> NEED valid.
+static int quorum_vote_cpu(int voters, int need, int decisions, int threads) {
+    auto votes = cpu_tuples(voters, 128, 128);
+    const int nt = std::max(1, std::min(threads, voters));
+    const int total = decisions + 5;
+    std::unique_ptr<std::atomic<int>[]> valid(new std::atomic<int>[total]), done(new std::atomic<int>[total]);
+    for (int k = 0; k < total; ++k) {
+        valid[k].store(0);
+        done[k].store(0);
+    }
+    std::atomic<int> gen{-1};
+    std::atomic<bool> stop{false};
+    std::vector<std::thread> th;
+    for (int j = 0; j < nt; ++j)
+        th.emplace_back([&, j] {
+            int seen = -1;
+            for (;;) {
+                int g;
+                bool slept = false;
+                while ((g = gen.load(std::memory_order_acquire)) == seen && !stop.load()) {
+                    futex(&gen, FUTEX_WAIT_PRIVATE, seen);
+                    slept = true;
+                }
+                if (slept) futex(&gen, FUTEX_WAKE_PRIVATE, 2);  // the release is a wake-up tree
+                if (stop.load()) return;
+                for (int k = seen + 1; k <= g; ++k)
+                    for (int i = j; i < voters; i += nt) {
+                        const bool bad = k % 10 == 4 && i == 7;  // decisions 9, 19, ... after warm-up
+                        if (cpu_verify(votes[i]) && !bad) valid[k].fetch_add(1, std::memory_order_acq_rel);
+                        done[k].fetch_add(1, std::memory_order_acq_rel);
+                    }
+                seen = g;
+            }
+        });
+    std::vector<double> t;
+    int wrong = 0;
+    for (int g = 0; g < total; ++g) {
+        const auto t0 = Clock::now();
+        gen.store(g, std::memory_order_release);
+        futex(&gen, FUTEX_WAKE_PRIVATE, 2);
+        while (valid[g].load(std::memory_order_acquire) < need) {
+            if (done[g].load(std::memory_order_acquire) == voters) break;  // all in, quorum short
+            __builtin_ia32_pause();
+        }
+        const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+        if (g >= 5) t.push_back(us);
+        // drain the spare vote (outside the latency), as quorum-hook does
+        while (done[g].load(std::memory_order_acquire) < voters) __builtin_ia32_pause();
+        if (valid[g].load() < need) wrong++;
+    }
+    stop.store(true);
+    gen.fetch_add(1);
+    futex(&gen, FUTEX_WAKE_PRIVATE, INT_MAX);
+    for (auto& x : th) x.join();
+    std::printf("{\"mode\": \"quorum-vote-cpu\", \"voters\": %d, \"need\": %d, \"decisions\": %d, \"threads\": %d, "
+                "\"p50_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f, \"wrong_verdicts\": %d}\n",
+                voters, need, decisions, nt, pct(t, 50) / 1e3, pct(t, 99) / 1e3, pct(t, 100) / 1e3, wrong);
+    return wrong ? 2 : 0;
 }
 
 // quorum-pipe CHANNELS DECISIONS gpu|cpu: pipelined decisions at n = 100 (config 4). CHANNELS
@@ -987,7 +1071,7 @@ static int parse_cpu(int requests, int iters) {
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-hook|quorum-pipe|sign|quorum-cpu|proposal-cpu|proposal-gpu|parse-cpu ...\n", argv[0]);
+        std::fprintf(stderr, "usage: %s quorum-gpu|quorum-batch|quorum-hook|quorum-pipe|sign|quorum-cpu|quorum-vote-cpu|proposal-cpu|proposal-gpu|parse-cpu ...\n", argv[0]);
         return 1;
     }
     const std::string mode = argv[1];
@@ -998,6 +1082,7 @@ int main(int argc, char** argv) {
     if (mode == "sign") return sign_both(arg(2, 200));
     if (mode == "quorum-pipe") return quorum_pipe(arg(2, 2), arg(3, 200), !(argc > 4 && !std::strcmp(argv[4], "cpu")));
     if (mode == "quorum-cpu") return quorum_cpu(arg(2, 66), arg(3, 200), arg(4, 66));
+    if (mode == "quorum-vote-cpu") return quorum_vote_cpu(arg(2, 67), arg(3, 66), arg(4, 200), arg(5, 67));
     if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
     if (mode == "proposal-gpu") return proposal_gpu(arg(2, 3000), arg(3, 20));
     if (mode == "parse-cpu") return parse_cpu(arg(2, 6000), arg(3, 50));
