@@ -36,6 +36,9 @@
 #else
 #define SBFT_UNROLL1
 #endif
+#ifndef SBFT_INV_PIPE
+#define SBFT_INV_PIPE 1  // inv_mod: the next batch's divsteps overlap this batch's updates
+#endif
 
 namespace sbft {
 namespace inv {
@@ -229,6 +232,29 @@ SBFT_HD void inv_mod(uint32_t out[8], const uint32_t x[8], const uint32_t* tab, 
     else
         e.v[0] = 1;
     int32_t delta = 1;
+#if SBFT_INV_PIPE
+    // Software-pipelined: batch i+1's divsteps need only the low limb of T_i (f, g) / 2^30,
+    // which limbs 0 and 1 give; so they are computed first, and the next batch's dependent
+    // chain of table lookups runs while the full (f, g) and (d, e) updates of batch i fill its
+    // wait cycles (the one-lane form is latency-bound: one wavefront per SIMD on the latency
+    // kernels). The last batch's look-ahead is computed and dropped.
+    int32_t u, v, q, r;
+    delta = divsteps30(delta, (uint32_t)f.v[0], (uint32_t)g.v[0], tab, u, v, q, r);
+SBFT_UNROLL1
+    for (int batch = 0; batch < 26 && !is_zero30(g); ++batch) {
+        const int64_t lf = (mac(mac(0, u, f.v[0]), v, g.v[0]) >> 30) + (int64_t)u * f.v[1] + (int64_t)v * g.v[1];
+        const int64_t lg = (mac(mac(0, q, f.v[0]), r, g.v[0]) >> 30) + (int64_t)q * f.v[1] + (int64_t)r * g.v[1];
+        int32_t u2, v2, q2, r2;
+        const int32_t delta2 = divsteps30(delta, (uint32_t)lf & SBFT_M30, (uint32_t)lg & SBFT_M30, tab, u2, v2, q2, r2);
+        update_de(d, e, u, v, q, r, P);
+        update_fg(f, g, u, v, q, r);
+        delta = delta2;
+        u = u2;
+        v = v2;
+        q = q2;
+        r = r2;
+    }
+#else
 SBFT_UNROLL1
     for (int batch = 0; batch < 26 && !is_zero30(g); ++batch) {
         int32_t u, v, q, r;
@@ -236,6 +262,7 @@ SBFT_UNROLL1
         update_de(d, e, u, v, q, r, P);
         update_fg(f, g, u, v, q, r);
     }
+#endif
     // f = +-1: x^-1 = f * d
     if (f.v[8] < 0) {
         for (int i = 0; i < 9; ++i) d.v[i] = -d.v[i];
@@ -292,12 +319,29 @@ __device__ __forceinline__ void inv_mod_wave(uint32_t out[8], const uint32_t x[8
     int32_t f_i = m_i, g_i = on ? lane_limb(xs.v, lane) : 0, d_i = 0, e_i = on ? lane_limb(cs.v, lane) : 0;
     const uint32_t minv = P ? SBFT_PINV30 : SBFT_NINV30;
     int32_t delta = 1;
+#if SBFT_INV_PIPE
+    // pipelined as inv_mod: the next batch's divsteps start from the low limb of T (f, g) / 2^30
+    // (limbs 0 and 1 of f and g), ahead of this batch's lane-parallel updates
+    int32_t u, v, q, r;
+    delta = divsteps30(delta, (uint32_t)__builtin_amdgcn_readlane(f_i, 0), (uint32_t)__builtin_amdgcn_readlane(g_i, 0),
+                       tab, u, v, q, r);
+    SBFT_UNROLL1
+    for (int batch = 0; batch < 26; ++batch) {
+        if (__builtin_amdgcn_ballot_w64(g_i != 0) == 0) break;  // g == 0
+        const int32_t f0 = __builtin_amdgcn_readlane(f_i, 0), g0 = __builtin_amdgcn_readlane(g_i, 0);
+        const int32_t f1 = __builtin_amdgcn_readlane(f_i, 1), g1 = __builtin_amdgcn_readlane(g_i, 1);
+        const int64_t lf = (((int64_t)u * f0 + (int64_t)v * g0) >> 30) + (int64_t)u * f1 + (int64_t)v * g1;
+        const int64_t lg = (((int64_t)q * f0 + (int64_t)r * g0) >> 30) + (int64_t)q * f1 + (int64_t)r * g1;
+        int32_t u2, v2, q2, r2;
+        const int32_t delta2 = divsteps30(delta, (uint32_t)lf, (uint32_t)lg, tab, u2, v2, q2, r2);
+#else
     SBFT_UNROLL1
     for (int batch = 0; batch < 26; ++batch) {
         if (__builtin_amdgcn_ballot_w64(g_i != 0) == 0) break;  // g == 0
         const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(f_i, 0), g0 = (uint32_t)__builtin_amdgcn_readlane(g_i, 0);
         int32_t u, v, q, r;
         delta = divsteps30(delta, f0, g0, tab, u, v, q, r);
+#endif
         const int32_t d0 = __builtin_amdgcn_readlane(d_i, 0), e0 = __builtin_amdgcn_readlane(e_i, 0);
         const int64_t cd0 = (int64_t)u * d0 + (int64_t)v * e0, ce0 = (int64_t)q * d0 + (int64_t)r * e0;
         const int32_t md = (int32_t)((0u - (uint32_t)cd0 * minv) & SBFT_M30);
@@ -311,6 +355,13 @@ __device__ __forceinline__ void inv_mod_wave(uint32_t out[8], const uint32_t x[8
         d_i = div30_lanes(cd, top);
         e_i = div30_lanes(ce, top);
         if (!on) f_i = g_i = d_i = e_i = 0;
+#if SBFT_INV_PIPE
+        delta = delta2;
+        u = u2;
+        v = v2;
+        q = q2;
+        r = r2;
+#endif
     }
     s30 f, d;
 #pragma unroll

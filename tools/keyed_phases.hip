@@ -18,6 +18,8 @@ __device__ unsigned long long g_mark_wall[16];
         }                                                   \
     } while (0)
 #include "../smartbft_amd/csrc/p256_keyed.hip"
+// the engine's test-only fault injection lives in gpuverify.cpp, which this tool does not link
+extern "C" int sbft_fault_hit(int) { return 0; }
 
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); return 1; } } while (0)
 
