@@ -1291,6 +1291,101 @@ SBFT_DEV void p29_add_aff_pl(pl29& P, const f29& x2, const f29& y2) {
 #define SBFT_PAIR_LANE_LOCAL 1
 #endif
 
+// ---------------------------------------------------------------- lane-local, W = c Z^2 carried
+// The half kernel's two ladders (p256_verify_half_kernel) run the same instruction stream on two
+// curves: pair A on the curve itself, pair B on E_c: y^2 = x^3 - 3c^2 x + b c^3 for c = r^3 - 3r
+// + b, which (x, y) -> (c x, c y0 y) maps the curve onto when c = y0^2; R0 = (r, y0) lands on
+// (c r, c^2), so pair B needs no square root. The doubling's a Z^4 term is then -3 (c Z^2)^2, so
+// both pairs carry W = c Z^2 (c = 1 on pair A) and the step that squared Z computes (X - W)(X +
+// W) directly (a general product instead of a square); W moves along as W3 = g W (doubling) and
+// W HH (addition). The table entries are stored divided by c, so the addition's U2 = x2 Z1^2 is
+// x2'' W and S2 = y2'' Z1 W. tests/test_f29_bounds.py (dbl_w, add_aff_w) checks every column,
+// limb and contract, W = c Z^2 and X / W = x(k R0) on the curve.
+// Halved representative as p29_dbl_h (X3 = h^2 - 2b, Y3 = h (b - X3) - g^2, Z3 = Y Z, h = 3a'/2):
+//   1: a' = (X - W)(X + W) | g = Y^2      2: b = X g | W3 = W g
+//   3: X3 = h^2 - 2b | L = g^2            4: Y3 = h (b - X3) - L | Z3 = Y Z
+// In: X in N', Y in N' or N+-, Z, W in N. Out: X3, Y3 in N', Z3, W3 in N.
+struct plw29 {
+    f29 xb, zy, zo, w;  // X (both lanes), Z | Y, Z (odd lane), W (both lanes)
+};
+SBFT_DEV void p29_dbl_plw(plw29& P) {
+    f29 a, b, o1, s1, o2, h, o3, s3, o4;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        a.v[i] = sel_pair(P.xb.v[i] - P.w.v[i], P.zy.v[i]);   // X - W: |.| < 2^29.2 | Y
+        b.v[i] = sel_pair(P.xb.v[i] + P.w.v[i], P.zy.v[i]);   // X + W < 2^30.1 | Y
+    }
+    f29_mul_ilp(o1, a, b);                                    // a' | g
+    s1 = f29_swap_pair(o1);                                   // g | a'
+    f29_mul_ilp(o2, f29_sel_pair(P.xb, P.w), f29_sel_pair(s1, o1));  // b = X g | W3 = W g
+    f29_triple_half(h, o1);                                   // h = 3a'/2 (even lane; limbs < 2^29 + 3)
+    {
+        const f29 sq = f29_sel_pair(h, o1);
+        const f29* const v[1] = {&o2};
+        const u32 c[1] = {sel_pair((u32)-2, 0u)};
+        f29_mulsq_add_ilp<true, 1>(o3, sq, sq, v, c, ~0u);   // X3 = h^2 - 2b | L = g^2: N'
+    }
+    s3 = f29_swap_pair(o3);                                   // L | X3
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        a.v[i] = sel_pair(h.v[i], P.zy.v[i]);                 // h | Y
+        b.v[i] = sel_pair(o2.v[i] - o3.v[i], P.zo.v[i]);      // b - X3: (-2^29.2, 2^29 + 2^25) | Z
+    }
+    {
+        const f29* const v[1] = {&s3};
+        const u32 c[1] = {sel_pair((u32)-1, 0u)};
+        f29_mulsq_add_ilp<false, 1>(o4, a, b, v, c, sel_pair(~0u, 0u));  // Y3 = h (b - X3) - L: N' | Z3 = Y Z: N
+    }
+    P.xb = f29_sel_pair(o3, s3);                              // X3 in both lanes
+    P.zy = f29_swap_pair(o4);                                 // Z3 | Y3
+    P.zo = o4;                                                // Z3 (odd lane)
+    P.w = f29_bcast_pair(o2, true);                           // W3 in both lanes
+}
+// The mixed addition with W (p29_add_aff_pl's steps 2-6, step 1 gone, W3 = W HH last):
+//   1: U2 = x2'' W | T = Z1 W   2: HH = H^2 | S2 = y2'' T   3: V = X1 HH | HHH
+//   4: Z3 = Z1 H | X3 = r^2 - HHH - 2V   5: Y1 HHH | r (V - X3)   6: W3 = W HH (both lanes)
+// (x2'', y2'') = the entry divided by c, in both lanes (N, y2'' N+- when negated). Out: X3 in
+// N', Y3 in N+-, Z3, W3 in N.
+SBFT_DEV void p29_add_aff_plw(plw29& P, const f29& x2, const f29& y2) {
+    f29 o1, s1, h, o2, s2, hh, o3, s3, r, o4, szy, a, b, o5, s5, s4, o6;
+    f29_mul_ilp(o1, f29_sel_pair(x2, P.zo), P.w);             // U2 | T
+    s1 = f29_swap_pair(o1);                                   // T | U2
+#pragma unroll
+    for (int i = 0; i < 9; ++i) h.v[i] = sel_pair(o1.v[i], s1.v[i]) - P.xb.v[i];  // H: (-2^29.2, 2^29 + 2^25)
+    f29_mul_ilp(o2, f29_sel_pair(h, y2), f29_sel_pair(h, o1)); // HH | S2
+    s2 = f29_swap_pair(o2);                                   // S2 | HH
+    hh = f29_sel_pair(o2, s2);                                // HH in both lanes
+    f29_mul_ilp(o6, P.w, hh);                                 // W3 = W HH (independent of steps 3-5)
+    f29_mul_ilp(o3, f29_sel_pair(P.xb, h), hh);               // V | HHH
+    s3 = f29_swap_pair(o3);                                   // HHH | V
+    f29_sub(r, o2, P.zy);                                     // r = S2 - Y1 (odd lane): |.| < 2^29.2
+    {
+        const f29* const v[2] = {&o3, &s3};
+        const u32 c[2] = {sel_pair(0u, (u32)-1), sel_pair(0u, (u32)-2)};
+        f29_mulsq_add_ilp<false, 2>(o4, f29_sel_pair(P.zy, r), f29_sel_pair(h, r), v, c,
+                                    sel_pair(0u, ~0u));       // Z3 = Z1 H: N | X3 = r^2 - HHH - 2V: N'
+    }
+    szy = f29_swap_pair(P.zy);                                // Y1 (even lane)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        a.v[i] = sel_pair(szy.v[i], r.v[i]);
+        b.v[i] = sel_pair(s3.v[i], s3.v[i] - o4.v[i]);        // HHH | V - X3: (-2^29.2, 2^29 + 2^25)
+    }
+    f29_mul_ilp(o5, a, b);                                    // Y1 HHH | r (V - X3)
+    s5 = f29_swap_pair(o5);
+    s4 = f29_swap_pair(o4);                                   // X3 | Z3
+    P.xb = f29_bcast_pair(o4, true);                          // X3 in both lanes
+#pragma unroll
+    for (int i = 0; i < 9; ++i) P.zy.v[i] = sel_pair(o4.v[i], o5.v[i] - s5.v[i]);  // Z3 | Y3 (N+-)
+    P.zo = s4;                                                // Z3 (odd lane)
+    P.w = o6;
+}
+SBFT_DEV void plw29_to(jp29& p, const plw29& q) {
+    p.x = q.xb;
+    p.y = f29_bcast_pair(q.zy, true);
+    p.z = f29_bcast_pair(q.zy, false);
+}
+
 // ---------------------------------------------------------------- co-Z table building
 // Odd multiples [1, 3, ..., 2^w - 1]Q with Meloni's co-Z additions (2007): every point of the
 // chain shares the Z of the running 2Q, so an addition costs 4M + 2S and only the Z ratios

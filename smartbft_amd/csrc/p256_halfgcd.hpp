@@ -25,6 +25,10 @@
 
 #include "p256_inv.hpp"  // SBFT_HD, SBFT_UNROLL1
 
+#ifndef SBFT_HGCD_LEHMER
+#define SBFT_HGCD_LEHMER 1  // lehmer() batches (0: one step() per quotient, the round-4 form)
+#endif
+
 namespace sbft {
 namespace hgcd {
 
@@ -137,6 +141,116 @@ SBFT_HD void step(state& s) {
     s.neg = !s.neg;
 }
 
+// ---- Lehmer steps: many quotients from the leading 53 bits, one multi-word update ----
+// Knuth's Algorithm L (TAOCP vol. 2, 4.5.2) on x = floor(a / 2^s), y = floor(b / 2^s), s = len(a)
+// - 53, all exact in double precision. (A B; C D) is the cofactor matrix of the steps taken, so
+// the true remainders are (A a + B b, C a + D b) and, scaled by 2^-s, lie within [x + min(A, B),
+// x + max(A, B)] and [y + min(C, D), y + max(C, D)] (the entries of a row have opposite signs).
+// A quotient is taken only when both corners give it -- floor((x + A) / (y + C)) ==
+// floor((x + B) / (y + D)) -- so it is the true quotient; only while the true b is surely still
+// >= 2^128 (y + min(C, D) >= 2^(128 - s)), so the reduction stops where step() would; and only
+// while the new entries stay below 2^30 (signed 32-bit multipliers for the update). Every
+// division is exact to within one: x, y < 2^53 and the remainder x - q y is formed exactly by an
+// FMA. Returns false when no quotient could be taken (the caller then runs one step()).
+SBFT_HD double hgcd_lead53(const uint32_t x[8], int ka, int sh) {
+    // bits [32 ka + 32 - ... ] of x: the words ka, ka - 1, ka - 2 (ka >= 4), shifted right by sh
+    uint32_t w2 = 0, w1 = 0, w0 = 0;
+SBFT_UNROLL
+    for (int k = 2; k < 8; ++k) {
+        if (k == ka) w2 = x[k];
+        if (k == ka - 1) w1 = x[k];
+        if (k == ka - 2) w0 = x[k];
+    }
+    // (w2 w1 w0) >> sh, sh in [12, 43]: the result has at most 53 bits
+    const uint64_t hi = ((uint64_t)w2 << 32) | w1;
+    uint64_t v;
+    if (sh >= 32) v = hi >> (sh - 32);
+    else v = (hi << (32 - sh)) | (w0 >> sh);
+    return (double)v;
+}
+
+SBFT_HD bool lehmer(state& s) {
+    int ka = 7;
+SBFT_UNROLL
+    for (int k = 4; k < 8; ++k)
+        if (s.a[k] != 0) ka = k;  // a >= b >= 2^128: the top word is at 4..7
+    uint32_t top = 0;
+SBFT_UNROLL
+    for (int k = 4; k < 8; ++k)
+        if (k == ka) top = s.a[k];
+    const int len = 32 * ka + 32 - __builtin_clz(top);  // bit length of a, >= 129
+    const int sft = len - 53;                            // >= 76
+    const int sh = sft - 32 * (ka - 2);                  // in [12, 43]
+    double x = hgcd_lead53(s.a, ka, sh), y = hgcd_lead53(s.b, ka, sh);
+    const double thr = ldexp(1.0, 128 - sft);  // 2^128 / 2^s
+    double A = 1.0, B = 0.0, C = 0.0, D = 1.0;
+    int k = 0;
+    const double cap = 1073741824.0;  // 2^30
+SBFT_UNROLL1
+    for (; k < 64; ++k) {
+        if (!(y + fmin(C, D) >= thr)) break;  // the true b may already be < 2^128
+        const double y1 = y + C, y2 = y + D, x1 = x + A, x2 = x + B;
+        if (!(y1 > 0.0) || !(y2 > 0.0)) break;
+        double q = floor(x1 / y1);
+        if (fma(-q, y1, x1) < 0.0) q -= 1.0;  // the rounded quotient can only be one too large
+        const double r2 = fma(-q, y2, x2);
+        if (r2 < 0.0 || r2 >= y2) break;  // the other corner disagrees
+        const double nc = fma(-q, C, A), nd = fma(-q, D, B);
+        if (!(fabs(nc) < cap) || !(fabs(nd) < cap)) break;
+        const double ny = fma(-q, y, x);
+        A = C;
+        B = D;
+        C = nc;
+        D = nd;
+        x = y;
+        y = ny;
+    }
+    if (k == 0) return false;
+    const int32_t iA = (int32_t)A, iB = (int32_t)B, iC = (int32_t)C, iD = (int32_t)D;
+    uint32_t na[8], nb[8];
+    int64_t ca = 0, cb = 0;
+SBFT_UNROLL
+    for (int j = 0; j < 8; ++j) {  // (A a + B b, C a + D b): both exact remainders, >= 0
+        ca += (int64_t)iA * (int64_t)s.a[j] + (int64_t)iB * (int64_t)s.b[j];
+        cb += (int64_t)iC * (int64_t)s.a[j] + (int64_t)iD * (int64_t)s.b[j];
+        na[j] = (uint32_t)ca;
+        nb[j] = (uint32_t)cb;
+        ca >>= 32;
+        cb >>= 32;
+    }
+    // cofactor magnitudes: the signs alternate along the sequence and across each matrix row,
+    // so |A t_a + B t_b| = |A| |t_a| + |B| |t_b|
+    const uint32_t mA = (uint32_t)(iA < 0 ? -iA : iA), mB = (uint32_t)(iB < 0 ? -iB : iB);
+    const uint32_t mC = (uint32_t)(iC < 0 ? -iC : iC), mD = (uint32_t)(iD < 0 ? -iD : iD);
+    uint32_t nta[5], ntb[5];
+    uint64_t ua = 0, ub = 0;  // products < 2^62 each: a limb's sum stays below 2^64
+SBFT_UNROLL
+    for (int j = 0; j < 5; ++j) {
+        ua += (uint64_t)mA * s.ta[j] + (uint64_t)mB * s.tb[j];
+        ub += (uint64_t)mC * s.ta[j] + (uint64_t)mD * s.tb[j];
+        nta[j] = (uint32_t)ua;
+        ntb[j] = (uint32_t)ub;
+        ua >>= 32;
+        ub >>= 32;
+    }
+    if (ca != 0 || cb != 0 || ua != 0 || ub != 0 || ntb[4] > 1u) {  // cannot happen; the caller's
+        s.ok = false;                                                // relation check is the net
+        return true;
+    }
+SBFT_UNROLL
+    for (int j = 0; j < 8; ++j) {
+        s.a[j] = na[j];
+        s.b[j] = nb[j];
+    }
+SBFT_UNROLL
+    for (int j = 0; j < 5; ++j) {
+        s.ta[j] = nta[j];
+        s.tb[j] = ntb[j];
+    }
+    if (k & 1) s.neg = !s.neg;
+    return true;
+}
+
 // Outputs of a finished state: w = r_i (< 2^128), |v| = |t_i| (<= 2^128), v < 0.
 SBFT_HD void result(const state& s, uint32_t w[8], uint32_t v[8], bool& vneg) {
     for (int k = 0; k < 8; ++k) {
@@ -150,7 +264,8 @@ SBFT_HD void result(const state& s, uint32_t w[8], uint32_t v[8], bool& vneg) {
 SBFT_HD bool half_gcd(const uint32_t u[8], uint32_t w[8], uint32_t v[8], bool& vneg) {
     state s;
     init(s, u);
-    for (int it = 0; it < 400 && more(s); ++it) step(s);
+    for (int it = 0; it < 400 && more(s); ++it)
+        if (!SBFT_HGCD_LEHMER || !lehmer(s)) step(s);
     if (more(s)) s.ok = false;
     result(s, w, v, vneg);
     return s.ok;

@@ -33,8 +33,10 @@
 #endif
 #if defined(__HIPCC__)
 #define SBFT_UNROLL1 _Pragma("unroll 1")
+#define SBFT_UNROLL _Pragma("unroll")
 #else
 #define SBFT_UNROLL1
+#define SBFT_UNROLL
 #endif
 #ifndef SBFT_INV_PIPE
 #define SBFT_INV_PIPE 1  // inv_mod: the next batch's divsteps overlap this batch's updates

@@ -697,6 +697,95 @@ SBFT_DEV void build_q_table_pair_m(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29
     }
 }
 
+// build_q_table_pair_m for the W-carrying ladders of the half kernel (p29_dbl_plw): the odd
+// multiples of (qxm, qym) on E_c (y^2 = x^3 - 3c^2 x + b c^3; c = 1: the curve itself), stored
+// divided by c. ac = c^2 enters DBLU's M = 3 (x^2 - c^2); the inversion is of z c, and 1 / z and
+// 1 / c come out of one paired step. Each entry is then X (lam^2 / c) | (Y lam)(lam^2 / c) in three
+// paired steps, as before. In: qxm, qym, ac, cc in N or N'. Out: entries in N.
+template <class InvP>
+SBFT_DEV void build_q_table_pair_w(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29& qxm, const f29& qym, const f29& ac,
+                                   const f29& cc, bool odd, InvP inv_p) {
+    static_assert(kQTab == 8, "the Z-ratio product tree below is written for 7 ratios");
+    auto pmul = [odd](f29& e, f29& d, const f29& a0, const f29& b0, const f29& a1, const f29& b1) {
+        f29 o;
+        f29_mul_ilp(o, f29_pick(odd, a0, a1), f29_pick(odd, b0, b1));
+        f29_unpair(o, e, d);
+    };
+    const f29 r2 = f29_const(C29_R2);
+    f29 dx, dy, cx, cy, z;
+    {  // DBLU as build_q_table_pair_m, M = 3 (B - c^2)
+        f29 b, e, l, t, m, m2;
+        pmul(b, e, qxm, qxm, qym, qym);
+        pmul(l, t, e, e, qxm, e);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t.v[i] <<= 2;  // 4xE < 2^31
+        f29_normalize(cx, t);                       // S (N')
+#pragma unroll
+        for (int i = 0; i < 9; ++i) m.v[i] = 3 * (b.v[i] - ac.v[i]);  // |.| < 3 2^29.2 < 2^30.8
+        f29_normalize(m, m);                        // M (N')
+        f29_mul_ilp(m2, m, m);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t.v[i] = m2.v[i] - (cx.v[i] << 1);
+        f29_normalize(dx, t);                       // X2 (N')
+#pragma unroll
+        for (int i = 0; i < 9; ++i) l.v[i] <<= 2;  // 4L < 2^31
+        f29_normalize(l, l);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) l.v[i] <<= 1;  // 8L, |.| < 2^30.2
+        f29_normalize(cy, l);                       // 8L (N')
+        f29_sub(t, cx, dx);                         // S - X2, |.| < 2^29.3
+        f29_mul_ilp(m2, m, t);
+        f29_sub(t, m2, cy);
+        f29_normalize(dy, t);                       // Y2 (N')
+        f29_add(z, qym, qym);                       // Z = 2y
+    }
+    f29 hs[kQTab - 1];
+#pragma unroll 1
+    for (int k = 1; k < kQTab; ++k) {  // ZADDU (curve-independent), as build_q_table_pair_m
+        f29 h, r, c, dd, w1, w2, t, u, a1, c2;
+        f29_sub(h, dx, cx);
+        f29_sub(r, dy, cy);
+        pmul(c, dd, h, h, r, r);
+        pmul(w1, w2, dx, c, cx, c);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t.v[i] = dd.v[i] - w1.v[i] - w2.v[i];
+        f29_normalize(cx, t);
+        f29_sub(u, w1, w2);
+        f29_sub(t, w1, cx);
+        pmul(a1, c2, dy, u, r, t);
+        f29_sub(t, c2, a1);
+        f29_normalize(cy, t);
+        dx = w1;
+        dy = a1;
+        tx[k] = cx;
+        ty[k] = cy;
+        hs[k - 1] = h;
+    }
+    {  // Z(T_7) = z h_1 ... h_7 as a tree, then z c
+        f29 p0, p1, p2, p3;
+        pmul(p0, p1, z, hs[0], hs[1], hs[2]);
+        pmul(p2, p3, hs[3], hs[4], hs[5], hs[6]);
+        pmul(p0, p1, p0, p1, p2, p3);
+        f29_mul_ilp(z, p0, p1);
+    }
+    f29 zc, ic, lam, kap;
+    f29_mul_ilp(zc, z, cc);
+    {
+        const fe zi = inv_p(f29_canon_plain(zc));
+        f29_mul_ilp(ic, f29_from_u256(zi), r2);  // 1 / (z c)
+    }
+    pmul(lam, kap, ic, cc, ic, z);               // 1 / z | 1 / c
+#pragma unroll 1
+    for (int k = kQTab - 1; k >= 1; --k) {  // lam^2 | Y lam, lam^2 / c | lam h_k, X lam^2 / c | Y lam^3 / c
+        f29 l2, yl, l2k, nxt;
+        pmul(l2, yl, lam, lam, ty[k], lam);
+        pmul(l2k, nxt, l2, kap, lam, hs[k - 1]);
+        pmul(tx[k], ty[k], tx[k], l2k, yl, l2k);
+        lam = nxt;  // 1 / Z(T_{k-1})
+    }
+    pmul(tx[0], ty[0], qxm, kap, qym, kap);  // the base itself, divided by c
+}
+
 // 2-3. w = s^-1 of tuple t from the launch-wide Montgomery trick (p256_sinv_* kernels: 1,024
 // tuples per scan group), then u1 = e w, u2 = r w, recoded for the signed-odd ladders: an even
 // u becomes n - u with the base negated ((n-u)(-P) = uP); u == 0 becomes n, whose ladder
@@ -1484,37 +1573,16 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         const uint32_t slot = mine ? lane : 0u;
         const uint32_t tc = blockIdx.x * T + slot;
         const uint32_t ic = tc < n ? tc : n - 1;
-        fe e_raw, r, s, qx, qy;
+        fe r, s, qx, qy;
         load_tuple(ic, r, s, qx, qy);
-        if constexpr (FRAMED) {
-            uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-            if (mine && tc < n) {
-                const uint8_t* msg = fr.blob + fr.off[ic];
-                const uint32_t L = fr.len[ic], nb = sha256_nblocks(L);
-                uint32_t w[16];
-                for (uint32_t b = 0; b < nb; ++b) {
-                    sha256_block_at(msg, L, b, w);
-                    compress(h, w);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                e_raw.v[7 - k] = h[k];
-                if (mine) edig[k * T + lane] = h[k];
-            }
-        } else {
-            e_raw = load_be32(digest + 32ull * ic);
-        }
-        probe("helper_hash", lane == 0);
         const bool valid = verify_inputs_valid(r, s, qx, qy);
         fe one = fe_zero();
         one.v[0] = 1;
-        fe si, wm, e, u1, u2;
+        // barrier 1 waits for (v, w) only: s^-1, u2 and the reduction come first; the hash, u1 and
+        // the comb sum are needed at barrier 2
+        fe si, wm, u2;
         inv::inv_mod(si.v, (valid ? s : one).v, dtab, false);  // plain s^-1 mod n
         fn_mul(wm, si, fe_const(C_R2N));                          // s^-1 R
-        fn_canon(e, e_raw);
-        fn_mul(u1, e, wm);
-        fn_canon(u1, u1);
         fn_mul(u2, r, wm);
         fn_canon(u2, u2);
         if (!valid) u2 = one;
@@ -1525,14 +1593,14 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         for (int it = 0; it < 400; ++it) {
             const bool go = hgcd::more(hs);
             if (!__any(go)) break;
-            if (go) hgcd::step(hs);
+            if (go && !(SBFT_HGCD_LEHMER && hgcd::lehmer(hs))) hgcd::step(hs);
         }
         fe w, va;
         bool vneg;
         hgcd::result(hs, w.v, va.v, vneg);
-        fe vr, c;
+        fe vr;
         fn_mul(vr, va, fe_const(C_R2N));  // |v| R
-        bool good = hs.ok && !hgcd::more(hs) && !fe_is_zero_raw(w);
+        bool good = hs.ok && !hgcd::more(hs) && !fe_is_zero_raw(w) && va.v[4] <= 1u;
         {  // v u2 == +-w (mod n): the result is used only when it provably holds
             fe t;
             fn_mul(t, vr, u2);
@@ -1540,15 +1608,11 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             good = good && fe_eq(t, vneg ? mod_n_neg(w) : w);
         }
         probe("helper_hgcd", lane == 0);
-        fn_mul(c, vr, u1);  // |v| u1
-        fn_canon(c, c);
-        if (vneg && !fe_is_zero_raw(c)) c = mod_n_neg(c);
         const bool fb = valid && (!good || fe_lt(r, P256_PMN));  // the classic way: v = 1, w = u2
         fe ka = w, kb = va;
         if (fb || !valid) {
             ka = u2;
             kb = one;
-            c = u1;
             vneg = false;
         }
         if (mine) {
@@ -1562,6 +1626,35 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         probe("helper_published", lane == 0);
         __syncthreads();  // #1: the scalars are in hsc (the verify wavefronts' tables in qtab)
         probe("helper_barrier1", lane == 0);
+        fe e_raw;
+        if constexpr (FRAMED) {
+            uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+            if (mine && tc < n) {
+                const uint8_t* msg = fr.blob + fr.off[ic];
+                const uint32_t L = fr.len[ic], nb = sha256_nblocks(L);
+                uint32_t wd[16];
+                for (uint32_t b = 0; b < nb; ++b) {
+                    sha256_block_at(msg, L, b, wd);
+                    compress(h, wd);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                e_raw.v[7 - k] = h[k];
+                if (mine) edig[k * T + lane] = h[k];
+            }
+        } else {
+            e_raw = load_be32(digest + 32ull * ic);
+        }
+        probe("helper_hash", lane == 0);
+        fe e, u1, c;
+        fn_canon(e, e_raw);
+        fn_mul(u1, e, wm);
+        fn_canon(u1, u1);
+        fn_mul(c, vr, u1);  // |v| u1
+        fn_canon(c, c);
+        if (vneg && !fe_is_zero_raw(c)) c = mod_n_neg(c);
+        if (fb || !valid) c = u1;
         // c G on the comb, in comb_add_u1g's odd recoding (even c -> n - c, base negated; c = 0
         // becomes n, whose comb sum cancels to infinity)
         const bool neg1 = (c.v[0] & 1u) == 0;
@@ -1571,6 +1664,25 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         bool ginf = true;  // the first addition returns its addend (add_aff_fix)
         comb_add_u1g(g, c, neg1, gcomb, [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
                      [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
+        probe("helper_comb", lane == 0);
+        // x = r is on the curve iff r^3 - 3r + b is a square (the verify wavefronts' pair B ran on
+        // E_c without knowing): y = (.)^((p+1)/4), y^2 == r^3 - 3r + b
+        bool has_r0;
+        {
+            f29 rm, t2, t3, rhs, y0, yy, d;
+            const f29 b = f29_const(C29_B);
+            f29_mul_ilp(rm, f29_from_u256(r), f29_const(C29_R2));
+            f29_sqr_ilp(t2, rm);
+            f29_mul_ilp(t3, t2, rm);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) rhs.v[i] = t3.v[i] - 3u * rm.v[i] + b.v[i];  // |limb| < 2^31
+            f29_normalize(rhs, rhs);                                                  // N'
+            f29_sqrt_chain(y0, rhs);
+            f29_sqr_ilp(yy, y0);
+            f29_sub(d, yy, rhs);  // |limb| < 2^30, |.| < 2^259
+            has_r0 = f29_zero_mod_p_any(d);
+        }
+        probe("helper_square", lane == 0);
         if (mine) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
@@ -1578,11 +1690,10 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                 gsum[(9 + k) * T + lane] = g.y.v[k];
                 gsum[(18 + k) * T + lane] = g.z.v[k];
             }
-            gsum[27 * T + lane] = ginf ? 1u : 0u;
+            gsum[27 * T + lane] = (ginf ? 1u : 0u) | (has_r0 ? 2u : 0u);
         }
-        probe("helper_comb", lane == 0);
         __syncthreads();  // #2: hand-over to the verify wavefronts
-        probe_dump("helper hash,sinv,hgcd,published,barrier1,comb", lane == 0);
+        probe_dump("helper sinv,hgcd,published,barrier1,hash,comb,square", lane == 0);
         return;
     }
 
@@ -1598,9 +1709,10 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     load_tuple(idx, r, s, qx, qy);
     const bool valid = verify_inputs_valid(r, s, qx, qy);
 
-    // R0 = (r, y0), y0 = (r^3 - 3r + b)^((p+1)/4) (every lane: pair B uses it)
-    const f29 r2c = f29_const(C29_R2);
-    f29 rm, rhs, y0;
+    // Pair A's base is Q on the curve; pair B's is P' = (c r, c^2) on E_c, c = r^3 - 3r + b (the
+    // image of R0 = (r, sqrt(c)) when c is a square; the helper decides that by barrier 2)
+    const f29 r2c = f29_const(C29_R2), one29 = f29_const(C29_ONE);
+    f29 rm, rhs;
     f29_mul_ilp(rm, f29_from_u256(r), r2c);  // |r R| < 2^256.1 (product output)
     {
         f29 t2, t3;
@@ -1609,29 +1721,24 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         f29_mul_ilp(t3, t2, rm);
 #pragma unroll
         for (int i = 0; i < 9; ++i) rhs.v[i] = t3.v[i] - 3u * rm.v[i] + b.v[i];  // |limb| < 2^31, |.| < 2^259
-        f29_normalize(rhs, rhs);                                                  // N'
+        f29_normalize(rhs, rhs);                                                  // c (N')
     }
     probe("verify_inputs", tid == 0);
-    f29_sqrt_chain(y0, rhs);
-    probe("verify_sqrt", tid == 0);
-    bool has_r0;  // x = r is on the curve
+    const bool onc = role == 1 && valid;  // this pair runs on E_c (else on the curve, c = 1)
+    f29 px, py, cc, ac;
     {
-        f29 yy, d;
-        f29_sqr_ilp(yy, y0);
-        f29_sub(d, yy, rhs);  // |limb| < 2^30, |.| < 2^259
-        has_r0 = f29_zero_mod_p_any(d);
-    }
-    {
-        f29 qxm, qym, o;
-        f29_mul_ilp(o, f29_pick(odd, f29_from_u256(qx), f29_from_u256(qy)), r2c);
-        f29_unpair(o, qxm, qym);
-        f29 px = role ? rm : qxm, py = role ? y0 : qym;
-        if (!(valid && (role == 0 || has_r0))) {  // stand-in base 2G (verdict masked or rejected)
+        f29 o;  // A: qx R2 | qy R2, B: c r | c c, one paired step
+        const f29 qa = f29_pick(odd, f29_from_u256(qx), f29_from_u256(qy));
+        f29_mul_ilp(o, role ? rhs : qa, role ? f29_pick(odd, rm, rhs) : r2c);
+        f29_unpair(o, px, py);
+        if (!valid) {  // stand-in base 2G on the curve (verdict masked)
             px = f29_const(C29_G2X);
             py = f29_const(C29_G2Y);
         }
+        cc = onc ? rhs : one29;  // c
+        ac = onc ? py : one29;   // c^2 = y(P')
         f29 tx[kQTab], ty[kQTab];
-        build_q_table_pair_m(tx, ty, px, py, odd, [&](const fe& zp) {
+        build_q_table_pair_w(tx, ty, px, py, ac, cc, odd, [&](const fe& zp) {
             fe zi;
             inv::inv_mod(zi.v, zp.v, dtab, true);
             return zi;
@@ -1678,56 +1785,84 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         tab_entry((d < 0 ? -d : d) >> 1, x, y);
         if ((d < 0) != negb) f29_neg(y, y);
     };
+    auto base_neg = [&](f29& x, f29& y) {
+        tab_entry(0, x, y);
+        if (!negb) f29_neg(y, y);
+    };
     auto dblp = [odd](jp29& p) { p29_dbl_pair(p, p, odd); };
-    jp29 acc;
-    tab_entry(0, acc.x, acc.y);  // the top term 16^L (k = 16^L + sum d_i 16^i)
-    acc.z = f29_const(C29_ONE);
-    if (negb) f29_neg(acc.y, acc.y);
-    bool inf = false;  // only a classic (fb) ladder can meet infinity, at its last addition
+    plw29 q;  // the top term 16^L (k = 16^L + sum d_i 16^i): the base itself, Z = 1, W = c
     {
-        pl29 q = pl29_from(acc, odd);
+        f29 y0 = py;
+        if (negb) f29_neg(y0, y0);
+        q.xb = px;
+        q.zy = f29_sel_pair(one29, y0);
+        q.zo = one29;
+        q.w = cc;
+    }
 #pragma unroll 1
-        for (int i = L - 1; i >= 1; --i) {
+    for (int i = L - 1; i >= 1; --i) {
 #pragma unroll
-            for (int d = 0; d < kQWin; ++d) p29_dbl_pl(q, odd);
-            f29 x2, y2;
-            qentry(i, x2, y2);
-            p29_add_aff_pl(q, x2, y2);
-        }
+        for (int d = 0; d < kQWin; ++d) p29_dbl_plw(q);
+        f29 x2, y2;
+        qentry(i, x2, y2);
+        p29_add_aff_plw(q, x2, y2);
+    }
 #pragma unroll
-        for (int d = 0; d < kQWin; ++d) p29_dbl_pl(q, odd);
-        pl29_to(acc, q);
+    for (int d = 0; d < kQWin; ++d) p29_dbl_plw(q);
+    // The last addition (digit 0) and, for an even k, the subtraction of the base: free of
+    // exceptional cases on the half-size ladders (both pairs, W kept).
+    plw29 qw = q;
+    {
         f29 x2, y2;
         qentry(0, x2, y2);
-        p29_add_aff_pair(acc, x2, y2, odd);
-        add_aff_fix(acc, inf, dblp, [&](f29& x, f29& y) { qentry(0, x, y); });
+        p29_add_aff_plw(qw, x2, y2);
     }
     if (__any(keven)) {  // k + 1 ran: subtract the base once
-        auto base_neg = [&](f29& x, f29& y) {
-            tab_entry(0, x, y);
-            if (!negb) f29_neg(y, y);
-        };
-        jp29 a2 = acc;
-        bool inf2 = inf;
+        plw29 q2 = qw;
         f29 x2, y2;
         base_neg(x2, y2);
-        p29_add_aff_pair(a2, x2, y2, odd);
-        add_aff_fix(a2, inf2, dblp, base_neg);
-        if (keven) {
-            acc = a2;
-            inf = inf2;
+        p29_add_aff_plw(q2, x2, y2);
+        if (keven) qw = q2;
+    }
+    jp29 acc;
+    plw29_to(acc, qw);
+    bool inf = false;  // only a classic (fb) ladder can meet infinity, at its last addition
+    if (__builtin_expect(__any(fb), 0)) {  // classic ladders (pair A, c = 1): the exact repairs
+        jp29 a;
+        plw29_to(a, q);
+        bool infa = false;
+        f29 x2, y2;
+        qentry(0, x2, y2);
+        p29_add_aff_pair(a, x2, y2, odd);
+        add_aff_fix(a, infa, dblp, [&](f29& x, f29& y) { qentry(0, x, y); });
+        if (__any(keven)) {
+            jp29 a2 = a;
+            bool inf2 = infa;
+            base_neg(x2, y2);
+            p29_add_aff_pair(a2, x2, y2, odd);
+            add_aff_fix(a2, inf2, dblp, base_neg);
+            if (keven) {
+                a = a2;
+                infa = inf2;
+            }
+        }
+        if (fb) {
+            acc = a;
+            inf = infa;
         }
     }
     probe("verify_ladder", tid == 0);
-    jp29 V;  // pair B's v R0 on pair A's lanes (quad_perm [2,3,2,3])
+    f29 VX, VW;  // pair B's X and W = c Z^2 of v R0, on pair A's lanes (quad_perm [2,3,2,3])
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-        V.x.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)acc.x.v[i], 0xEE, 0xF, 0xF, false);
-        V.z.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)acc.z.v[i], 0xEE, 0xF, 0xF, false);
+        VX.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)acc.x.v[i], 0xEE, 0xF, 0xF, false);
+        VW.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)qw.w.v[i], 0xEE, 0xF, 0xF, false);
     }
 
-    __syncthreads();  // #2: the helper's (v u1) G is in gsum
+    __syncthreads();  // #2: the helper's (v u1) G and the square test are in gsum
     probe("verify_barrier2", tid == 0);
+    const u32 gflags = gsum[27 * T + pr];
+    const bool has_r0 = (gflags & 2u) != 0;  // x = r is on the curve
     {
         jp29 g;
 #pragma unroll
@@ -1736,7 +1871,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             g.y.v[i] = gsum[(9 + i) * T + pr];
             g.z.v[i] = gsum[(18 + i) * T + pr];
         }
-        const bool ginf = gsum[27 * T + pr] != 0;
+        const bool ginf = (gflags & 1u) != 0;
         const jp29 a0 = acc;
         p29_add_jac_lean(acc, g);
         // H == 0 (Z3 = 0): a doubling if X3 == 0 (c G == w Q), else infinity (c G == -w Q)
@@ -1751,17 +1886,16 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             inf = (hz && !twice) || (inf && ginf);
         }
     }
-    // T = acc (pair A), V: accept iff T != infinity and X_T Z_V^2 == X_V Z_T^2
+    // T = acc (pair A), V on E_c: x(V) = X_V / W_V. Accept iff T != infinity and X_T W_V == X_V Z_T^2
     bool accept, exc;
     {
-        f29 zt2, zv2, lhs, rhs2, d;
+        f29 zt2, lhs, rhs2, d;
         f29_sqr(zt2, acc.z);
-        f29_sqr(zv2, V.z);
-        f29_mul(lhs, acc.x, zv2);
-        f29_mul(rhs2, V.x, zt2);
+        f29_mul(lhs, acc.x, VW);
+        f29_mul(rhs2, VX, zt2);
         f29_sub(d, lhs, rhs2);  // |limb| < 2^29.2, |.| < 2^257
         accept = has_r0 && f29_zero_mod_p_any(d);
-        exc = has_r0 && (f29_zero_mod_p(acc.z) || f29_zero_mod_p(V.z));  // never expected: fixup net
+        exc = has_r0 && (f29_zero_mod_p(acc.z) || f29_zero_mod_p(VW));  // never expected: fixup net
     }
     if (__builtin_expect(__any(fb), 0)) {
         bool exc_f;
@@ -1776,7 +1910,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         exc = false;
     }
     probe("verify_final", tid == 0);
-    probe_dump("verify inputs,sqrt,tables,barrier1,ladder,barrier2,final", tid == 0);
+    probe_dump("verify inputs,tables,barrier1,ladder,barrier2,final", tid == 0);
     if (active && (tid & 3) == 0) {
         if (exc && valid) {
             if constexpr (FRAMED) {  // the fixup kernel's inputs

@@ -288,6 +288,54 @@ def add_aff_f(X, Y, Z, x2, y2):
     return X3, Y3, Z3
 
 
+def dbl_w(X, Y, Z, W):
+    """p29_dbl_plw (the half kernel's lane-local doubling with W = c Z^2 carried along, on E_c:
+    y^2 = x^3 - 3 c^2 x + b c^3; c = 1 is the curve itself), halved representative:
+      a' = (X - W)(X + W) | g = Y^2;  b = X g | W3 = g W;  X3 = h^2 - 2b | L = g^2 (h = 3a'/2);
+      Y3 = h (b - X3) - L | Z3 = Y Z.  Every product is a general one (one lane's is a square)."""
+    a1 = mont(sub(X, W), add(X, W))
+    g = mont(Y, Y)
+    b = mont(X, g)
+    W3 = mont(W, g)
+    h = triple_half(a1)
+    assert all(0 <= h[i] < (1 << 29) + 3 for i in range(8)) and abs(val(h)) < 2 ** 258.1
+    X3 = mont(h, h, sq=True, addends=[(b, -2)], fold=True)
+    L = mont(g, g, sq=True, addends=[(b, 0)], fold=True)  # the odd lane: the same call, c = 0
+    t = sub(b, X3)
+    Y3 = mont(h, t, addends=[(L, -1)], fold=True)
+    Z3 = mont(Y, Z, addends=[(L, 0)])                      # odd lane: c = 0, no fold
+    for v in (a1, g, b, W3, Z3):
+        check_N(v)
+    for v in (X3, L, Y3):
+        check_Np(v)
+    return X3, Y3, Z3, W3
+
+
+def add_aff_w(X, Y, Z, W, x2, y2):
+    """p29_add_aff_plw: the mixed addition with W = c Z1^2 for the table entries (x/c, y/c):
+      U2 = x2 W | T = Z1 W;  HH = H^2 | S2 = y2 T;  V = X1 HH | HHH;  Z3 = Z1 H | X3 = r^2 - HHH - 2V;
+      Y1 HHH | r (V - X3);  W3 = W HH."""
+    u2 = mont(x2, W)
+    T = mont(Z, W)
+    h = sub(u2, X)
+    hh = mont(h, h)
+    s2 = mont(y2, T)
+    V = mont(X, hh)
+    hhh = mont(h, hh)
+    rr = sub(s2, Y)
+    Z3 = mont(Z, h, addends=[(hhh, 0), (V, 0)])
+    X3 = mont(rr, rr, addends=[(hhh, -1), (V, -2)], fold=True)
+    t = sub(V, X3)
+    a = mont(Y, hhh)
+    b = mont(rr, t)
+    Y3 = sub(b, a)
+    W3 = mont(W, hh)
+    for v in (u2, T, hh, s2, V, hhh, Z3, a, b, W3):
+        check_N(v)
+    check_Np(X3)
+    return X3, Y3, Z3, W3
+
+
 def jac_to_affine(X, Y, Z):
     x, y, z = plain(X), plain(Y), plain(Z)
     zi = pow(z, -1, P)
@@ -338,3 +386,55 @@ def test_extreme_operands():
     dbl_h(X3, Y3, Z3)
     dbl_h(Np_max, [(-MASK) & 0xFFFFFFFF] * 8 + [(1 << 24) - 1], N_max)
     add_aff_f(X3, Y3, Z3, N_max, [(-MASK) & 0xFFFFFFFF] * 8 + [0])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_w_ladder_on_the_isomorphic_curve(seed):
+    """The half kernel's v R0 side without the square root (p29_dbl_plw / p29_add_aff_plw): R0 =
+    (r, y0) on the curve, c = r^3 - 3r + b = y0^2, and the ladder runs on E_c: y^2 = x^3 - 3c^2 x +
+    b c^3 from P' = (c r, c^2), the image of R0 under (x, y) -> (c x, c y0 y), with W = c Z^2 and
+    the table entries (x/c, y/c) = (x_E, y0 y_E). Checked: no overflow, every contract, W = c Z^2
+    all along, and X / W = x(k R0) on the curve (the comparison the kernel makes) -- no y0 needed.
+    c = 1 (the base on the curve itself, pair A) runs the same code."""
+    rng = random.Random(seed)
+    G = pyref.G
+    for c_is_one in (False, True):
+        R0 = pyref.mul(rng.randrange(1, pyref.N), G)
+        r, y0 = R0
+        c = 1 if c_is_one else (r ** 3 - 3 * r + pyref.B) % P
+        yscale = 1 if c_is_one else y0
+        if c_is_one:
+            X, Y = mont_of(r), mont_of(y0)
+        else:
+            X, Y = mont_of(c * r % P), mont_of(c * c % P)
+        Z, W = mont_of(1), mont_of(c)
+        ref = R0
+        for step in range(150):
+            X = relimb(X, rng, -(1 << 26) + 1, (1 << 29) + (1 << 26), 0, 1 << 24)   # N'
+            W = relimb(W, rng, 0, 1 << 29)                                           # N
+            if step % 5 == 4:
+                q = pyref.mul(rng.randrange(1, pyref.N), R0)
+                x2, y2 = mont_of(q[0]), mont_of(yscale * q[1] % P)
+                if rng.random() < 0.5:  # a negated table entry: N+- limbs
+                    y2 = [(-i32(w)) & 0xFFFFFFFF for w in y2]
+                    q = (q[0], (-q[1]) % P)
+                X, Y, Z, W = add_aff_w(X, Y, Z, W, x2, y2)
+                ref = pyref.add(ref, q)
+                Y = relimb(Y, rng, -(1 << 29) + 1, 1 << 29)  # N+-
+            else:
+                Y = relimb(Y, rng, -(1 << 26) + 1, (1 << 29) + (1 << 26), 0, 1 << 24)   # N'
+                X, Y, Z, W = dbl_w(X, Y, Z, W)
+                ref = pyref.add(ref, ref)
+            z = plain(Z)
+            assert plain(W) == c * z * z % P, step
+            assert plain(X) * pow(plain(W), -1, P) % P == ref[0], step
+
+
+def test_w_extreme_operands():
+    top = (1 << 29) + (1 << 26) - 1
+    Np_max = [top] * 8 + [(1 << 24) - 1]
+    N_max = [MASK] * 8 + [(1 << 24) - 1]
+    X3, Y3, Z3, W3 = dbl_w(Np_max, Np_max, N_max, N_max)
+    add_aff_w(X3, Y3, Z3, W3, N_max, [(-MASK) & 0xFFFFFFFF] * 8 + [0])
+    dbl_w(Np_max, [(-MASK) & 0xFFFFFFFF] * 8 + [(1 << 24) - 1], N_max, N_max)
+    add_aff_w(Np_max, [(-MASK) & 0xFFFFFFFF] * 8 + [0], N_max, N_max, N_max, N_max)
