@@ -150,8 +150,8 @@ SBFT_HD void step(state& s) {
 // floor((x + B) / (y + D)) -- so it is the true quotient; only while the true b is surely still
 // >= 2^128 (y + min(C, D) >= 2^(128 - s)), so the reduction stops where step() would; and only
 // while the new entries stay below 2^30 (signed 32-bit multipliers for the update). Every
-// division is exact to within one: x, y < 2^53 and the remainder x - q y is formed exactly by an
-// FMA. Returns false when no quotient could be taken (the caller then runs one step()).
+// quotient estimate is within one of the truth (x, y < 2^53, rcp53) and the remainder x - q y,
+// formed exactly by an FMA, corrects it. Returns false when no quotient could be taken (the caller then runs one step()).
 SBFT_HD double hgcd_lead53(const uint32_t x[8], int ka, int sh) {
     // bits [32 ka + 32 - ... ] of x: the words ka, ka - 1, ka - 2 (ka >= 4), shifted right by sh
     uint32_t w2 = 0, w1 = 0, w0 = 0;
@@ -167,6 +167,21 @@ SBFT_UNROLL
     if (sh >= 32) v = hi >> (sh - 32);
     else v = (hi << (32 - sh)) | (w0 >> sh);
     return (double)v;
+}
+
+// 1 / y to ~2^-46 relative: v_rcp_f64 and one Newton step on the device (the IEEE division is
+// a ten-instruction dependent chain); the host build starts from a float reciprocal instead, so
+// that tests/test_native.py exercises the same correction with a rough first estimate. With q
+// below 2^31 (the cofactor cap) floor(x1 / y1) is then off by at most one either way, and the
+// remainder fixes it.
+SBFT_HD double rcp53(double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(y);
+#else
+    double r = (double)(float)(1.0 / y);
+#endif
+    r = fma(fma(-y, r, 1.0), r, r);
+    return fma(fma(-y, r, 1.0), r, r);
 }
 
 SBFT_HD bool lehmer(state& s) {
@@ -191,8 +206,10 @@ SBFT_UNROLL1
         if (!(y + fmin(C, D) >= thr)) break;  // the true b may already be < 2^128
         const double y1 = y + C, y2 = y + D, x1 = x + A, x2 = x + B;
         if (!(y1 > 0.0) || !(y2 > 0.0)) break;
-        double q = floor(x1 / y1);
-        if (fma(-q, y1, x1) < 0.0) q -= 1.0;  // the rounded quotient can only be one too large
+        double q = floor(x1 * rcp53(y1));
+        const double rm = fma(-q, y1, x1);  // exact: |x1 - q y1| < 2^53
+        if (rm < 0.0) q -= 1.0;
+        else if (rm >= y1) q += 1.0;
         const double r2 = fma(-q, y2, x2);
         if (r2 < 0.0 || r2 >= y2) break;  // the other corner disagrees
         const double nc = fma(-q, C, A), nd = fma(-q, D, B);

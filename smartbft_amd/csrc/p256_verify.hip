@@ -702,9 +702,9 @@ SBFT_DEV void build_q_table_pair_m(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29
 // divided by c. ac = c^2 enters DBLU's M = 3 (x^2 - c^2); the inversion is of z c, and 1 / z and
 // 1 / c come out of one paired step. Each entry is then X (lam^2 / c) | (Y lam)(lam^2 / c) in three
 // paired steps, as before. In: qxm, qym, ac, cc in N or N'. Out: entries in N.
-template <class InvP>
+template <class InvP, class Mark>
 SBFT_DEV void build_q_table_pair_w(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29& qxm, const f29& qym, const f29& ac,
-                                   const f29& cc, bool odd, InvP inv_p) {
+                                   const f29& cc, bool odd, InvP inv_p, Mark mark) {
     static_assert(kQTab == 8, "the Z-ratio product tree below is written for 7 ratios");
     auto pmul = [odd](f29& e, f29& d, const f29& a0, const f29& b0, const f29& a1, const f29& b1) {
         f29 o;
@@ -770,10 +770,12 @@ SBFT_DEV void build_q_table_pair_w(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29
     }
     f29 zc, ic, lam, kap;
     f29_mul_ilp(zc, z, cc);
+    mark(0);  // co-Z chain done
     {
         const fe zi = inv_p(f29_canon_plain(zc));
         f29_mul_ilp(ic, f29_from_u256(zi), r2);  // 1 / (z c)
     }
+    mark(1);  // inverted
     pmul(lam, kap, ic, cc, ic, z);               // 1 / z | 1 / c
 #pragma unroll 1
     for (int k = kQTab - 1; k >= 1; --k) {  // lam^2 | Y lam, lam^2 / c | lam h_k, X lam^2 / c | Y lam^3 / c
@@ -1738,11 +1740,14 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         cc = onc ? rhs : one29;  // c
         ac = onc ? py : one29;   // c^2 = y(P')
         f29 tx[kQTab], ty[kQTab];
-        build_q_table_pair_w(tx, ty, px, py, ac, cc, odd, [&](const fe& zp) {
-            fe zi;
-            inv::inv_mod(zi.v, zp.v, dtab, true);
-            return zi;
-        });
+        build_q_table_pair_w(
+            tx, ty, px, py, ac, cc, odd,
+            [&](const fe& zp) {
+                fe zi;
+                inv::inv_mod(zi.v, zp.v, dtab, true);
+                return zi;
+            },
+            [&](int m) { probe(m ? "verify_inverse" : "verify_chain", tid == 0); });
 #pragma unroll
         for (int m = 0; m < kQTab; ++m)
 #pragma unroll
@@ -1910,7 +1915,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         exc = false;
     }
     probe("verify_final", tid == 0);
-    probe_dump("verify inputs,tables,barrier1,ladder,barrier2,final", tid == 0);
+    probe_dump("verify inputs,chain,inverse,tables,barrier1,ladder,barrier2,final", tid == 0);
     if (active && (tid & 3) == 0) {
         if (exc && valid) {
             if constexpr (FRAMED) {  // the fixup kernel's inputs

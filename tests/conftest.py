@@ -14,6 +14,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C ABI)")
 
 
+def pytest_collection_modifyitems(config, items):
+    # torch ships its own HIP runtime; once the engine's (/opt/rocm) has initialised the device in
+    # this process, torch.cuda.is_available() came back False on the MI355X box (a run that began
+    # with tests/test_gpu_half.py). So when GPU tests are selected, torch initialises first.
+    if any(item.get_closest_marker("gpu") for item in items):
+        import torch
+        torch.cuda.is_available()
+
+
 def load_p256_vectors():
     """Golden P-256 vectors: (fields (n,160) uint8, expected (n,), category (n,), names)."""
     import json
