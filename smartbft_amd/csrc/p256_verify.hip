@@ -702,9 +702,9 @@ SBFT_DEV void build_q_table_pair_m(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29
 // divided by c. ac = c^2 enters DBLU's M = 3 (x^2 - c^2); the inversion is of z c, and 1 / z and
 // 1 / c come out of one paired step. Each entry is then X (lam^2 / c) | (Y lam)(lam^2 / c) in three
 // paired steps, as before. In: qxm, qym, ac, cc in N or N'. Out: entries in N.
-template <class InvP, class Mark>
-SBFT_DEV void build_q_table_pair_w(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29& qxm, const f29& qym, const f29& ac,
-                                   const f29& cc, bool odd, InvP inv_p, Mark mark) {
+template <class InvP, class Mark, class St, class Ld>
+SBFT_DEV void build_q_table_pair_w(const f29& qxm, const f29& qym, const f29& ac, const f29& cc, bool odd, InvP inv_p,
+                                   Mark mark, St st, Ld ld) {
     static_assert(kQTab == 8, "the Z-ratio product tree below is written for 7 ratios");
     auto pmul = [odd](f29& e, f29& d, const f29& a0, const f29& b0, const f29& a1, const f29& b1) {
         f29 o;
@@ -739,8 +739,11 @@ SBFT_DEV void build_q_table_pair_w(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29
         f29_normalize(dy, t);                       // Y2 (N')
         f29_add(z, qym, qym);                       // Z = 2y
     }
+    // The co-Z entries go to their table slots (st: LDS) as they come; only the Z ratios stay in
+    // registers across the inversion (with all 16 coordinates live there, the safegcd ran at half
+    // speed). The loops are unrolled, so nothing is indexed at run time (no scratch).
     f29 hs[kQTab - 1];
-#pragma unroll 1
+#pragma unroll
     for (int k = 1; k < kQTab; ++k) {  // ZADDU (curve-independent), as build_q_table_pair_m
         f29 h, r, c, dd, w1, w2, t, u, a1, c2;
         f29_sub(h, dx, cx);
@@ -757,8 +760,7 @@ SBFT_DEV void build_q_table_pair_w(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29
         f29_normalize(cy, t);
         dx = w1;
         dy = a1;
-        tx[k] = cx;
-        ty[k] = cy;
+        st(k, cx, cy);
         hs[k - 1] = h;
     }
     {  // Z(T_7) = z h_1 ... h_7 as a tree, then z c
@@ -777,15 +779,19 @@ SBFT_DEV void build_q_table_pair_w(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29
     }
     mark(1);  // inverted
     pmul(lam, kap, ic, cc, ic, z);               // 1 / z | 1 / c
-#pragma unroll 1
+#pragma unroll
     for (int k = kQTab - 1; k >= 1; --k) {  // lam^2 | Y lam, lam^2 / c | lam h_k, X lam^2 / c | Y lam^3 / c
-        f29 l2, yl, l2k, nxt;
-        pmul(l2, yl, lam, lam, ty[k], lam);
+        f29 l2, yl, l2k, nxt, X, Y;
+        ld(k, X, Y);
+        pmul(l2, yl, lam, lam, Y, lam);
         pmul(l2k, nxt, l2, kap, lam, hs[k - 1]);
-        pmul(tx[k], ty[k], tx[k], l2k, yl, l2k);
+        pmul(X, Y, X, l2k, yl, l2k);
+        st(k, X, Y);
         lam = nxt;  // 1 / Z(T_{k-1})
     }
-    pmul(tx[0], ty[0], qxm, kap, qym, kap);  // the base itself, divided by c
+    f29 x0, y0;
+    pmul(x0, y0, qxm, kap, qym, kap);  // the base itself, divided by c
+    st(0, x0, y0);
 }
 
 // 2-3. w = s^-1 of tuple t from the launch-wide Montgomery trick (p256_sinv_* kernels: 1,024
@@ -1623,7 +1629,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                 hsc[k * T + lane] = ka.v[k];
                 hsc[(8 + k) * T + lane] = kb.v[k];
             }
-            hsc[16 * T + lane] = (vneg ? 1u : 0u) | (fb ? 2u : 0u);
+            hsc[16 * T + lane] = (vneg ? 1u : 0u) | (fb ? 2u : 0u) | (valid ? 4u : 0u);
         }
         probe("helper_published", lane == 0);
         __syncthreads();  // #1: the scalars are in hsc (the verify wavefronts' tables in qtab)
@@ -1709,7 +1715,9 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     const uint32_t idx = active ? t : (n - 1);
     fe r, s, qx, qy;
     load_tuple(idx, r, s, qx, qy);
-    const bool valid = verify_inputs_valid(r, s, qx, qy);
+    // No input checks here: the helper makes them (valid arrives with the scalars at barrier 1).
+    // An invalid tuple's pairs run on whatever its r and Q are -- pure arithmetic with wave-uniform
+    // trip counts, whose result only the masked verdict would read.
 
     // Pair A's base is Q on the curve; pair B's is P' = (c r, c^2) on E_c, c = r^3 - 3r + b (the
     // image of R0 = (r, sqrt(c)) when c is a square; the helper decides that by barrier 2)
@@ -1726,41 +1734,45 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         f29_normalize(rhs, rhs);                                                  // c (N')
     }
     probe("verify_inputs", tid == 0);
-    const bool onc = role == 1 && valid;  // this pair runs on E_c (else on the curve, c = 1)
+    const bool onc = role == 1;  // this pair runs on E_c (pair A on the curve, c = 1)
     f29 px, py, cc, ac;
     {
         f29 o;  // A: qx R2 | qy R2, B: c r | c c, one paired step
         const f29 qa = f29_pick(odd, f29_from_u256(qx), f29_from_u256(qy));
         f29_mul_ilp(o, role ? rhs : qa, role ? f29_pick(odd, rm, rhs) : r2c);
         f29_unpair(o, px, py);
-        if (!valid) {  // stand-in base 2G on the curve (verdict masked)
-            px = f29_const(C29_G2X);
-            py = f29_const(C29_G2Y);
-        }
-        cc = onc ? rhs : one29;  // c
+        cc = onc ? rhs : one29;  // c (never 0: the curve has no point of order 2)
         ac = onc ? py : one29;   // c^2 = y(P')
-        f29 tx[kQTab], ty[kQTab];
+        // both lanes of the pair store the same words in this pair's column of qtab
+        auto st = [&](int m, const f29& x, const f29& y) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                qtab[(m * 18 + k) * 2 * T + col] = x.v[k];
+                qtab[(m * 18 + 9 + k) * 2 * T + col] = y.v[k];
+            }
+        };
+        auto ld = [&](int m, f29& x, f29& y) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                x.v[k] = qtab[(m * 18 + k) * 2 * T + col];
+                y.v[k] = qtab[(m * 18 + 9 + k) * 2 * T + col];
+            }
+        };
         build_q_table_pair_w(
-            tx, ty, px, py, ac, cc, odd,
+            px, py, ac, cc, odd,
             [&](const fe& zp) {
                 fe zi;
                 inv::inv_mod(zi.v, zp.v, dtab, true);
                 return zi;
             },
-            [&](int m) { probe(m ? "verify_inverse" : "verify_chain", tid == 0); });
-#pragma unroll
-        for (int m = 0; m < kQTab; ++m)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {  // both lanes of the pair store the same words
-                qtab[(m * 18 + k) * 2 * T + col] = tx[m].v[k];
-                qtab[(m * 18 + 9 + k) * 2 * T + col] = ty[m].v[k];
-            }
+            [&](int m) { probe(m ? "verify_inverse" : "verify_chain", tid == 0); }, st, ld);
     }
     probe("verify_tables", tid == 0);
     __syncthreads();  // #1: tables in qtab, the helper's scalars in hsc
     probe("verify_barrier1", tid == 0);
 
     const u32 flags = hsc[16 * T + pr];
+    const bool valid = (flags & 4u) != 0;
     const bool fb = (flags & 2u) != 0;
     const bool negb = role == 1 && (flags & 1u) != 0;  // v < 0: v R0 = |v| (-R0)
     fe k;
