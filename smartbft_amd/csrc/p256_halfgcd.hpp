@@ -169,19 +169,20 @@ SBFT_UNROLL
     return (double)v;
 }
 
-// 1 / y to ~2^-46 relative: v_rcp_f64 and one Newton step on the device (the IEEE division is
-// a ten-instruction dependent chain); the host build starts from a float reciprocal instead, so
-// that tests/test_native.py exercises the same correction with a rough first estimate. With q
-// below 2^31 (the cofactor cap) floor(x1 / y1) is then off by at most one either way, and the
-// remainder fixes it.
+// 1 / y: v_rcp_f64 and one Newton step on the device (the IEEE division is a ten-instruction
+// dependent chain); the host build starts from a float reciprocal (2 steps), so that
+// tests/test_native.py exercises the same correction with a rough first estimate. With q below
+// 2^31 (the cofactor cap) floor(x1 / y1) is then off by at most one either way and the remainder
+// fixes it; a worse estimate fails the remainder test and only ends the round.
 SBFT_HD double rcp53(double y) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    double r = __builtin_amdgcn_rcp(y);
+    const double r = __builtin_amdgcn_rcp(y);
+    return fma(fma(-y, r, 1.0), r, r);
 #else
     double r = (double)(float)(1.0 / y);
-#endif
     r = fma(fma(-y, r, 1.0), r, r);
     return fma(fma(-y, r, 1.0), r, r);
+#endif
 }
 
 SBFT_HD bool lehmer(state& s) {
@@ -203,17 +204,19 @@ SBFT_UNROLL
     const double cap = 1073741824.0;  // 2^30
 SBFT_UNROLL1
     for (; k < 64; ++k) {
-        if (!(y + fmin(C, D) >= thr)) break;  // the true b may already be < 2^128
+        // every condition from independent values, one exit test: the per-step dependent chain
+        // is y1 -> rcp -> q -> remainder -> (x, y) (a branch per test cost more than the test)
         const double y1 = y + C, y2 = y + D, x1 = x + A, x2 = x + B;
-        if (!(y1 > 0.0) || !(y2 > 0.0)) break;
         double q = floor(x1 * rcp53(y1));
         const double rm = fma(-q, y1, x1);  // exact: |x1 - q y1| < 2^53
-        if (rm < 0.0) q -= 1.0;
-        else if (rm >= y1) q += 1.0;
-        const double r2 = fma(-q, y2, x2);
-        if (r2 < 0.0 || r2 >= y2) break;  // the other corner disagrees
+        q = rm < 0.0 ? q - 1.0 : (rm >= y1 ? q + 1.0 : q);
+        const double rq = fma(-q, y1, x1), r2 = fma(-q, y2, x2);
         const double nc = fma(-q, C, A), nd = fma(-q, D, B);
-        if (!(fabs(nc) < cap) || !(fabs(nd) < cap)) break;
+        const bool ok = (y + fmin(C, D) >= thr) & (y1 > 0.0) & (y2 > 0.0) & (rq >= 0.0) & (rq < y1) &
+                        (r2 >= 0.0) & (r2 < y2) & (fabs(nc) < cap) & (fabs(nd) < cap);
+        // refused: the true b may be below 2^128, the corners disagree (or the estimate was off by
+        // more than one), or an entry would reach 2^30
+        if (!ok) break;
         const double ny = fma(-q, y, x);
         A = C;
         B = D;
