@@ -185,7 +185,12 @@ SBFT_HD double rcp53(double y) {
 #endif
 }
 
-SBFT_HD bool lehmer(state& s) {
+// The quotient batch of a Lehmer round: the cofactor matrix (A B; C D) of the k quotients taken.
+struct lmat {
+    double A, B, C, D;
+    int k;
+};
+SBFT_HD lmat lehmer_quotients(const state& s) {
     int ka = 7;
 SBFT_UNROLL
     for (int k = 4; k < 8; ++k)
@@ -225,8 +230,63 @@ SBFT_UNROLL1
         x = y;
         y = ny;
     }
+    return lmat{A, B, C, D, k};
+}
+
+// The same quotient batch with exactly K candidate steps and no branch: a step's conditions go
+// through one chain of minima into one comparison (every value is an integer below 2^53, so
+// a >= b is a - b + 1/2 > 0), and a refused step freezes the lane for the rest of the batch.
+// One wavefront runs K steps per round whatever its lanes do (the variable loop ran its slowest
+// lane's count plus the exit tests: VALU compares into SGPR masks, scalar ANDs, exec updates).
+template <int K>
+SBFT_HD lmat lehmer_quotients_k(const state& s) {
+    int ka = 7;
+SBFT_UNROLL
+    for (int k = 4; k < 8; ++k)
+        if (s.a[k] != 0) ka = k;
+    uint32_t top = 0;
+SBFT_UNROLL
+    for (int k = 4; k < 8; ++k)
+        if (k == ka) top = s.a[k];
+    const int len = 32 * ka + 32 - __builtin_clz(top);
+    const int sft = len - 53;
+    const int sh = sft - 32 * (ka - 2);
+    double x = hgcd_lead53(s.a, ka, sh), y = hgcd_lead53(s.b, ka, sh);
+    const double thr = ceil(ldexp(1.0, 128 - sft)) - 0.5;  // y + min(C, D) >= 2^(128-s), integers
+    const double cap = 1073741824.0;                       // 2^30
+    double A = 1.0, B = 0.0, C = 0.0, D = 1.0, kk = 0.0;
+    bool live = true;
+SBFT_UNROLL
+    for (int j = 0; j < K; ++j) {
+        const double y1 = y + C, y2 = y + D, x1 = x + A, x2 = x + B;
+        double q = floor(x1 * rcp53(y1));
+        const double rm = fma(-q, y1, x1);
+        q = rm < 0.0 ? q - 1.0 : (rm >= y1 ? q + 1.0 : q);
+        const double rq = fma(-q, y1, x1), r2 = fma(-q, y2, x2);
+        const double nc = fma(-q, C, A), nd = fma(-q, D, B);
+        const double m1 = fmin(fmin(y + fmin(C, D) - thr, fmin(y1, y2)), fmin(rq + 0.5, y1 - rq));
+        const double m2 = fmin(fmin(r2 + 0.5, y2 - r2), cap - fmax(fabs(nc), fabs(nd)));
+        live = live && fmin(m1, m2) > 0.0;
+        const double ny = fma(-q, y, x);
+        A = live ? C : A;
+        B = live ? D : B;
+        C = live ? nc : C;
+        D = live ? nd : D;
+        x = live ? y : x;
+        y = live ? ny : y;
+        kk += live ? 1.0 : 0.0;
+    }
+    return lmat{A, B, C, D, (int)kk};
+}
+
+#ifndef SBFT_HGCD_K
+#define SBFT_HGCD_K 16  // candidate steps per Lehmer round (0: the variable-length loop)
+#endif
+SBFT_HD bool lehmer(state& s) {
+    const lmat m = SBFT_HGCD_K ? lehmer_quotients_k<SBFT_HGCD_K ? SBFT_HGCD_K : 1>(s) : lehmer_quotients(s);
+    const int k = m.k;
     if (k == 0) return false;
-    const int32_t iA = (int32_t)A, iB = (int32_t)B, iC = (int32_t)C, iD = (int32_t)D;
+    const int32_t iA = (int32_t)m.A, iB = (int32_t)m.B, iC = (int32_t)m.C, iD = (int32_t)m.D;
     uint32_t na[8], nb[8];
     int64_t ca = 0, cb = 0;
 SBFT_UNROLL
