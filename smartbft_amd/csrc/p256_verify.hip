@@ -702,9 +702,9 @@ SBFT_DEV void build_q_table_pair_m(f29 (&tx)[kQTab], f29 (&ty)[kQTab], const f29
 // divided by c. ac = c^2 enters DBLU's M = 3 (x^2 - c^2); the inversion is of z c, and 1 / z and
 // 1 / c come out of one paired step. Each entry is then X (lam^2 / c) | (Y lam)(lam^2 / c) in three
 // paired steps, as before. In: qxm, qym, ac, cc in N or N'. Out: entries in N.
-template <class InvP, class Mark, class St, class Ld>
+template <class InvP, class Mark, class St, class Ld, class HSt, class HLd>
 SBFT_DEV void build_q_table_pair_w(const f29& qxm, const f29& qym, const f29& ac, const f29& cc, bool odd, InvP inv_p,
-                                   Mark mark, St st, Ld ld) {
+                                   Mark mark, St st, Ld ld, HSt hst, HLd hld) {
     static_assert(kQTab == 8, "the Z-ratio product tree below is written for 7 ratios");
     auto pmul = [odd](f29& e, f29& d, const f29& a0, const f29& b0, const f29& a1, const f29& b1) {
         f29 o;
@@ -739,11 +739,12 @@ SBFT_DEV void build_q_table_pair_w(const f29& qxm, const f29& qym, const f29& ac
         f29_normalize(dy, t);                       // Y2 (N')
         f29_add(z, qym, qym);                       // Z = 2y
     }
-    // The co-Z entries go to their table slots (st: LDS) as they come; only the Z ratios stay in
-    // registers across the inversion (with all 16 coordinates live there, the safegcd ran at half
-    // speed). The loops are unrolled, so nothing is indexed at run time (no scratch).
-    f29 hs[kQTab - 1];
-#pragma unroll
+    // The co-Z entries go to their table slots (st: LDS) as they come and the Z ratios to LDS of
+    // their own (hst), so nothing is live across the inversion (with all 16 coordinates in
+    // registers the safegcd ran at half speed) and the loops stay rolled: unrolled, the table
+    // build was ~40 KB of straight-line code that every workgroup streams through the instruction
+    // cache once; rolled, a ZADDU or a conversion step is fetched once and run seven times.
+#pragma unroll 1
     for (int k = 1; k < kQTab; ++k) {  // ZADDU (curve-independent), as build_q_table_pair_m
         f29 h, r, c, dd, w1, w2, t, u, a1, c2;
         f29_sub(h, dx, cx);
@@ -761,12 +762,19 @@ SBFT_DEV void build_q_table_pair_w(const f29& qxm, const f29& qym, const f29& ac
         dx = w1;
         dy = a1;
         st(k, cx, cy);
-        hs[k - 1] = h;
+        hst(k - 1, h);
     }
     {  // Z(T_7) = z h_1 ... h_7 as a tree, then z c
-        f29 p0, p1, p2, p3;
-        pmul(p0, p1, z, hs[0], hs[1], hs[2]);
-        pmul(p2, p3, hs[3], hs[4], hs[5], hs[6]);
+        f29 p0, p1, p2, p3, h0, h1, h2, h3, h4, h5, h6;
+        hld(0, h0);
+        hld(1, h1);
+        hld(2, h2);
+        hld(3, h3);
+        hld(4, h4);
+        hld(5, h5);
+        hld(6, h6);
+        pmul(p0, p1, z, h0, h1, h2);
+        pmul(p2, p3, h3, h4, h5, h6);
         pmul(p0, p1, p0, p1, p2, p3);
         f29_mul_ilp(z, p0, p1);
     }
@@ -779,12 +787,13 @@ SBFT_DEV void build_q_table_pair_w(const f29& qxm, const f29& qym, const f29& ac
     }
     mark(1);  // inverted
     pmul(lam, kap, ic, cc, ic, z);               // 1 / z | 1 / c
-#pragma unroll
+#pragma unroll 1
     for (int k = kQTab - 1; k >= 1; --k) {  // lam^2 | Y lam, lam^2 / c | lam h_k, X lam^2 / c | Y lam^3 / c
-        f29 l2, yl, l2k, nxt, X, Y;
+        f29 l2, yl, l2k, nxt, X, Y, hk;
         ld(k, X, Y);
+        hld(k - 1, hk);
         pmul(l2, yl, lam, lam, Y, lam);
-        pmul(l2k, nxt, l2, kap, lam, hs[k - 1]);
+        pmul(l2k, nxt, l2, kap, lam, hk);
         pmul(X, Y, X, l2k, yl, l2k);
         st(k, X, Y);
         lam = nxt;  // 1 / Z(T_{k-1})
@@ -1523,6 +1532,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     constexpr int T = kHalfTuples;
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     __shared__ u32 qtab[kQTab * 18 * 2 * T];    // [entry][x limbs, y limbs][pair A | pair B][tuple]
+    __shared__ u32 hrat[(kQTab - 1) * 9 * 2 * T]; // the table build's Z ratios, [ratio][limb][column]
     __shared__ u32 edig[FRAMED ? 8 * T : 1];    // FRAMED: the helper's digests [word][tuple]
     __shared__ u32 hsc[17 * T];                 // the helper's scalars: [k_A 0..7, k_B 0..7, flags][tuple]
     __shared__ u32 gsum[28 * T];                // the helper's (v u1) G: [x, y, z limbs, inf][tuple]
@@ -1765,7 +1775,15 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                 inv::inv_mod(zi.v, zp.v, dtab, true);
                 return zi;
             },
-            [&](int m) { probe(m ? "verify_inverse" : "verify_chain", tid == 0); }, st, ld);
+            [&](int m) { probe(m ? "verify_inverse" : "verify_chain", tid == 0); }, st, ld,
+            [&](int m, const f29& h) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) hrat[(m * 9 + k) * 2 * T + col] = h.v[k];
+            },
+            [&](int m, f29& h) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) h.v[k] = hrat[(m * 9 + k) * 2 * T + col];
+            });
     }
     probe("verify_tables", tid == 0);
     __syncthreads();  // #1: tables in qtab, the helper's scalars in hsc
