@@ -70,12 +70,14 @@ def _euclid_half(u):
     return b, tb, qmax
 
 
-def test_half_gcd_matches_euclid(tmp_path):
+@pytest.mark.parametrize("rounds", [16, 0])
+def test_half_gcd_matches_euclid(tmp_path, rounds):
     """p256_halfgcd.hpp (the half-size scalars of p256_verify_half_kernel) against exact Euclid:
     the same (w, v) whenever every quotient is below 2^31, a give-up otherwise, and always
     v u = w (mod n), 0 < w < 2^128, |v| < 2^128 on success."""
     exe = str(tmp_path / "hgcd_test")
-    subprocess.run(["g++", "-O2", "-Wall", "-Werror", "-o", exe,
+    # rounds: SBFT_HGCD_K, Lehmer rounds of exactly that many candidate steps (0: the variable loop)
+    subprocess.run(["g++", "-O2", "-Wall", "-Werror", f"-DSBFT_HGCD_K={rounds}", "-o", exe,
                     os.path.join(ROOT, "tests", "native", "hgcd_test.cpp")], check=True)
     rng = random.Random(11)
     us = [1, 2, 3, N - 1, N - 2, N // 2, N // 3, (N + 1) // 2, (1 << 128) - 1, 1 << 128, (1 << 128) + 1,
