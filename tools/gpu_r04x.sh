@@ -1,0 +1,34 @@
+#!/bin/bash
+# The table inversion split over the lane pair (inv::inv_mod_pair, SBFT_INV_PAIR=1): half-kernel
+# tests, phase probes with and without it, config-3 A/B against the one-lane inversion (lib_nopair).
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+V=$PWD/tools/variants
+step() {  # name, seconds, command...
+    local name=$1 secs=$2; shift 2
+    echo "== $name" | tee -a gpurun_out/r04x.log
+    timeout -k 10 "$secs" "$@" > "gpurun_out/r04x_$name.log" 2>&1
+    local rc=$?
+    grep -v "^W2026\|^E2026\|amdgpu.ids" "gpurun_out/r04x_$name.log" | tail -4 | tee -a gpurun_out/r04x.log
+    echo "rc=$rc" | tee -a gpurun_out/r04x.log
+    return $rc
+}
+step half 500 python -u -m pytest tests/test_gpu_half.py tests/test_gpu_exceptional.py tests/test_gpu_verify.py tests/test_gpu_configs.py tests/test_gpu_split.py -x -q --timeout 120 --timeout-method thread || exit $?
+SBFT_GV_LIB=$V/lib_probe.so step probe 120 python tools/half_probe.py || exit $?
+SBFT_GV_LIB=$V/lib_probenp.so step probenp 120 python tools/half_probe.py || exit $?
+out=gpurun_out/r04x_ab.txt
+: > $out
+for rep in 1 2 3; do
+  for v in cur nopair; do
+    case $v in cur) unset SBFT_GV_LIB;; *) export SBFT_GV_LIB=$V/lib_$v.so;; esac
+    timeout -k 10 180 python tools/latency_probe.py --calls 200 > gpurun_out/r04x_${v}_$rep.log 2>&1 || { tail -3 gpurun_out/r04x_${v}_$rep.log; exit 1; }
+    python - gpurun_out/r04x_${v}_$rep.log $v $rep >> $out <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+L = d["verify_proposal_10k"]
+print(sys.argv[2], "rep", sys.argv[3], "vp10k p50/p99", L["p50_ms"], L["p99_ms"])
+PY
+  done
+done
+unset SBFT_GV_LIB
+cat $out
