@@ -64,9 +64,13 @@ type Verifier struct {
 	onFail func(op string, err error)
 }
 
-// engineFailure reports whether rc is an infrastructure code (SBFT_GV_E*, -1 .. -6), as opposed
-// to a verdict (0, or SBFT_V_EVERIFY / EFORMAT / EKEY / ESPACE, -10 .. -13).
-func engineFailure(rc C.int) bool { return rc < 0 && rc > C.SBFT_V_EVERIFY }
+// engineFailure reports whether rc says the engine itself failed (SBFT_GV_ENODEV, ENOMEM,
+// ELAUNCH, EDEVICE, ESELFTEST: -2 .. -6), as opposed to a verdict (0, or SBFT_V_EVERIFY /
+// EFORMAT / EKEY / ESPACE, -10 .. -13) or SBFT_GV_EINVAL (-1). EINVAL is an argument the caller
+// built from its input, so it is returned as a VerifyError, never fail-stop: input a Byzantine
+// client or replica controls must not be able to stop this replica. (The C entry points read an
+// empty request, which cgo passes as NULL, 0, as SBFT_V_EFORMAT.)
+func engineFailure(rc C.int) bool { return rc <= C.SBFT_GV_ENODEV && rc >= C.SBFT_GV_ESELFTEST }
 
 // failStop hands an engine failure to the fail-stop hook; it does not return.
 func (v *Verifier) failStop(op string, rc C.int) {
@@ -319,8 +323,14 @@ func (v *Verifier) VerifyConsenterSigs(sigs []types.Signature, pr types.Proposal
 	status := make([]C.int32_t, len(sigs))
 	if rc := C.sbft_verifier_verify_consenter_sigs(v.v, p.signatures(sigs), C.size_t(len(sigs)), p.proposal(pr),
 		&status[0]); rc != 0 {
-		// every rc here is the engine's (per-signature verdicts come back in status)
-		v.failStop("VerifyConsenterSigs", rc)
+		// per-signature verdicts come back in status; a non-zero rc is the engine's, or EINVAL
+		if engineFailure(rc) {
+			v.failStop("VerifyConsenterSigs", rc)
+		}
+		for i := range errs {
+			errs[i] = &VerifyError{Code: int(rc), Index: -1, Msg: "gpuverify: " + C.GoString(C.sbft_gv_strerror(rc))}
+		}
+		return auxes, errs
 	}
 	for i, st := range status {
 		switch st {
@@ -391,7 +401,10 @@ func (v *Verifier) PruneSet(reqs [][]byte) ([]int, error) {
 	idx := make([]C.size_t, len(reqs))
 	var n C.size_t
 	if rc := C.sbft_pool_prune(v.v, &ptrs[0], &lens[0], C.size_t(len(reqs)), &idx[0], &n); rc != 0 {
-		v.failStop("PruneSet", rc) // pruning would otherwise drop valid requests as revoked
+		if engineFailure(rc) {
+			v.failStop("PruneSet", rc) // pruning would otherwise drop valid requests as revoked
+		}
+		return nil, &VerifyError{Code: int(rc), Index: -1, Msg: "gpuverify: " + C.GoString(C.sbft_gv_strerror(rc))}
 	}
 	out := make([]int, int(n))
 	for i := range out {

@@ -53,9 +53,10 @@ typedef struct sbft_gv_opts {
     uint32_t device_mask;   /* bit d selects HIP device d; 0 = all visible devices */
     uint32_t min_split;     /* batches smaller than this stay on one device (0 = default 65536) */
     int32_t pair_max;       /* per-device batches of at most this many tuples run the latency kernel
-                               (two lanes per tuple); 0 = default SBFT_GV_PAIR_MAX_DEFAULT, < 0 = never */
-    int32_t quad_max;       /* ignored (round 3's four-lane form of the pair kernel, measured no
-                               faster, is gone; half_max selects the four-lane kernel now) */
+                               (two lanes per tuple); 0 = default SBFT_GV_PAIR_MAX_DEFAULT, < 0 = never
+                               (and then no latency kernel at all unless half_max is set explicitly:
+                               pair_max < 0 with half_max 0 forces the one-lane throughput kernel) */
+    int32_t reserved0;      /* must be 0 */
     uint32_t slots_per_device; /* engine slots per selected device (0 = 1). Each slot owns a stream,
                                   staging, G's comb table and the registered-key tables, and takes
                                   one share of a split batch, exactly as a separate GPU would: with
@@ -63,12 +64,20 @@ typedef struct sbft_gv_opts {
                                   placement, per-device host workers) runs on a single GPU. For
                                   testing the split; a deployment leaves it 0. The environment
                                   variable SBFT_GV_SLOTS_PER_DEVICE overrides it. */
-    int32_t half_max;       /* per-device batches of at most this many tuples (and above quad_max)
-                               run the half-size-scalar latency kernel: four lanes per tuple, w Q and
+    int32_t half_max;       /* per-device batches of at most this many tuples run the
+                               half-size-scalar latency kernel (checked before pair_max): four lanes per tuple, w Q and
                                v R0 as two 128-bit ladders (p256_verify_half_kernel); 0 = default
                                SBFT_GV_HALF_MAX_DEFAULT, < 0 = never. The environment variable
                                SBFT_GV_HALF_MAX overrides it. */
-    uint64_t reserved[2];
+    uint64_t client_table_bytes; /* per-device budget for client-key comb tables
+                                    (sbft_gv_register_client_keys; 512 KiB per key and slot):
+                                    0 = default, 1/8 of the device's memory (36 GB of the
+                                    MI355X's 288 GB, ~70,000 clients); the environment variable
+                                    SBFT_GV_CLIENT_TABLE_BYTES overrides it. Keys past the
+                                    budget stay unregistered (their requests take the generic
+                                    launch, same verdicts), so client registration can never
+                                    use the memory the verify paths stage in. */
+    uint64_t reserved[1];
 } sbft_gv_opts;
 
 #define SBFT_GV_PAIR_MAX_DEFAULT 32768u
@@ -103,6 +112,17 @@ const char* sbft_gv_strerror(int code);
  * VerifyProposal (view.go:555) / VerifyConsenterSig (view.go:631, :834). */
 int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* r, const uint8_t* s,
                         const uint8_t* qx, const uint8_t* qy, size_t n, uint8_t* ok_out);
+/* sbft_gv_verify_p256 on a named kernel instead of the one the batch size selects (tests and
+ * diagnostics; same verdicts whichever kernel runs): SBFT_GV_KERNEL_THROUGHPUT (one lane per
+ * tuple), _PAIR (two lanes), _HALF (half-size scalars, four lanes), or _EXACT: every tuple
+ * through the exact case-split kernel alone -- the net the others hand flagged tuples to
+ * (Booth digits, explicit infinity and doubling branches; slow, one lane per tuple). */
+#define SBFT_GV_KERNEL_EXACT 0
+#define SBFT_GV_KERNEL_THROUGHPUT 1
+#define SBFT_GV_KERNEL_PAIR 2
+#define SBFT_GV_KERNEL_HALF 3
+int sbft_gv_verify_p256_kernel(sbft_gv_ctx* ctx, int kernel, const uint8_t* digest, const uint8_t* r,
+                               const uint8_t* s, const uint8_t* qx, const uint8_t* qy, size_t n, uint8_t* ok_out);
 
 /* Page-locked host memory, visible to every device of the process (hipHostMalloc, portable).
  * When all five input arrays of sbft_gv_verify_p256 live in such memory and a device's share
@@ -203,6 +223,16 @@ int sbft_gv_register_key(sbft_gv_ctx* ctx, const uint8_t qx[32], const uint8_t q
  * key's id, or 0 if it is not a point on the curve. Keys registered before keep their id.
  * Returns a negative SBFT_GV_E* only on an engine failure (nothing is registered then). */
 int sbft_gv_register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy, size_t n, uint32_t* key_ids);
+/* Client-key registry form of sbft_gv_register_keys, under a memory budget: new keys are
+ * registered in order while their tables fit both sbft_gv_opts.client_table_bytes and the
+ * headroom every device keeps free for staging (SBFT_GV_HBM_RESERVE bytes, or 1/32 of the
+ * device's memory if larger); the rest get key_ids[i] = 0 (unregistered: the generic verify
+ * paths take their requests, with the same verdicts). *registered (may be NULL) receives the
+ * number of keys of this call that hold an id. A budget that is spent is not an error: this
+ * returns a negative SBFT_GV_E* only on an engine failure (nothing is registered then). */
+#define SBFT_GV_HBM_RESERVE (8ull << 30)
+int sbft_gv_register_client_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy, size_t n,
+                                 uint32_t* key_ids, size_t* registered);
 
 /* Verify n tuples (digest, r, s) against registered keys key_id[k]. Same verdict semantics
  * as sbft_gv_verify_p256 (an unknown key id verifies false). Small batches run one
@@ -234,7 +264,8 @@ int sbft_gv_selftest_field(sbft_gv_ctx* ctx, int op, const uint8_t* a, const uin
  * stream synchronisations report SBFT_GV_EDEVICE once the work has drained. Every entry point
  * must then return the negative SBFT_GV_E* code (never a verdict) and the context stays usable:
  * the next call after disarming succeeds. Contexts created while a fault is armed fail their
- * self-test, so arm after sbft_gv_init. The environment variable
+ * self-test, so arm after sbft_gv_init. Arming prints a warning on stderr. In a library built
+ * with -DSBFT_FAULT_INJECTION (test builds only) the environment variable
  * SBFT_GV_FAULT=nomem|launch|sync[:count] arms one at the end of sbft_gv_init. Returns 0, or
  * SBFT_GV_EINVAL for an unknown kind. */
 #define SBFT_GV_FAULT_OFF 0

@@ -73,8 +73,13 @@ int sbft_verifier_add_consenter(sbft_verifier* v, uint64_t id, const uint8_t pub
  * precomputed comb tables (the keyed launch: no doublings, four lanes per signature); any
  * other proposal by the generic launch. Verdicts are the same either way.
  * pubkeys65: n x 65 bytes SEC1 uncompressed; keys that are not valid points are ignored.
- * Registration builds 512 KiB of tables per key per device (10,000 clients = 5 GB). */
+ * Registration builds 512 KiB of tables per key per device (10,000 clients = 5 GB), up to the
+ * engine's client-table budget (sbft_gv_register_client_keys): keys past it are left
+ * unregistered, not an error. */
 int sbft_verifier_add_clients(sbft_verifier* v, const uint8_t* pubkeys65, size_t n);
+/* Client keys registered so far (sbft_verifier_add_clients stops at the engine's client-table
+ * budget, sbft_gv_opts.client_table_bytes; the others stay on the generic path). */
+size_t sbft_verifier_client_count(const sbft_verifier* v);
 /* api.Verifier.VerificationSequence (dependencies.go:65-66). */
 uint64_t sbft_verifier_verification_sequence(const sbft_verifier* v);
 void sbft_verifier_set_verification_sequence(sbft_verifier* v, uint64_t seq);

@@ -524,6 +524,10 @@ struct sbft_gv_ctx {
     };
     std::unordered_map<std::array<uint8_t, 64>, uint32_t, KeyHash> key_index;
     std::atomic<uint32_t> nkeys{1};
+    // client-key budget (sbft_gv_register_client_keys): bytes of client comb tables allowed per
+    // device (0 = 1/8 of the device's memory) and the client keys that hold tables (under keys_mu)
+    uint64_t client_cap = 0;
+    size_t client_keys = 0;
     Helper helper;    // host work overlapped with a caller's copies (sbft_gv_framed_overlapped)
     Workers workers;  // host threads driving shares 1.. of a split batch (for_each_device)
 };
@@ -574,7 +578,10 @@ static int power_on_selftest(Slot* sl) {
     uint8_t* base = sl->dbuf;
     uint32_t* work = (uint32_t*)(base + 5 * f + fo);
     POSTCHK(hipMemcpyAsync(base, h.data(), 5 * f, hipMemcpyHostToDevice, sl->stream), "tuple copy");
-    for (int lanes : {1, 2, 3}) {
+    // every verify kernel on the same workspace, back to back, the exact fixup net last (0): it
+    // serves the others' flagged tuples, and in rounds 4-5 it had faulted unseen because nothing
+    // reached it
+    for (int lanes : {1, 2, 3, 0}) {
         cur = lanes;
         POSTCHK(hipMemsetAsync(base + 5 * f, 0xEE, n, sl->stream), "verdict memset");
         if (sbft_launch_p256_verify(base, base + f, base + 2 * f, base + 3 * f, base + 4 * f, base + 5 * f, (uint32_t)n,
@@ -621,6 +628,9 @@ int sbft_gv_inject_fault(int kind, int count) {
     g_fault_kind.store(SBFT_GV_FAULT_OFF);
     g_fault_left.store(kind == SBFT_GV_FAULT_OFF ? 0 : count);
     g_fault_kind.store(kind);
+    if (kind != SBFT_GV_FAULT_OFF)  // loud: an armed fault makes engine calls fail (fail-stop in Go)
+        fprintf(stderr, "sbft_gpuverify: TEST FAULT INJECTION ARMED (kind %d, count %d): engine calls will fail\n",
+                kind, count);
     return SBFT_GV_OK;
 }
 
@@ -647,11 +657,15 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     if (!ctx) return SBFT_GV_ENOMEM;
     if (opts && opts->min_split) ctx->min_split = opts->min_split;
     if (opts && opts->pair_max) ctx->pair_max = opts->pair_max < 0 ? 0u : (uint32_t)opts->pair_max;
+    // pair_max < 0 means "no latency kernel": the half kernel too, unless half_max asks for it
+    if (opts && opts->pair_max < 0 && !opts->half_max) ctx->half_max = 0;
     if (opts && opts->half_max) ctx->half_max = opts->half_max < 0 ? 0u : (uint32_t)opts->half_max;
     if (const char* e = getenv("SBFT_GV_HALF_MAX")) {
         const long v = strtol(e, nullptr, 10);
         ctx->half_max = v < 0 ? 0u : (uint32_t)v;
     }
+    if (opts) ctx->client_cap = opts->client_table_bytes;
+    if (const char* e = getenv("SBFT_GV_CLIENT_TABLE_BYTES")) ctx->client_cap = strtoull(e, nullptr, 10);
     if (const char* e = getenv("SBFT_KEYED_ZC_MAX")) ctx->keyed_zc_max = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("SBFT_KEYED_LANES_MIN")) ctx->keyed_lanes_min = (size_t)strtoull(e, nullptr, 10);
     // slots per device (sbft_gv_opts.slots_per_device, SBFT_GV_SLOTS_PER_DEVICE): > 1 runs the
@@ -707,6 +721,7 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
             }
     }
     // SBFT_GV_FAULT=nomem|launch|sync[:count] (tests): armed once the self-test has passed
+#ifdef SBFT_FAULT_INJECTION  // test builds only: a stray variable must not stop a deployment
     if (const char* e = getenv("SBFT_GV_FAULT")) {
         const int kind = !std::strncmp(e, "nomem", 5) ? SBFT_GV_FAULT_NOMEM
                          : !std::strncmp(e, "launch", 6) ? SBFT_GV_FAULT_LAUNCH
@@ -714,6 +729,7 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
         const char* c = std::strchr(e, ':');
         (void)sbft_gv_inject_fault(kind, c ? std::atoi(c + 1) : -1);
     }
+#endif
     *out = ctx;
     return SBFT_GV_OK;
 }
@@ -1362,6 +1378,18 @@ int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* 
         if (pipe && c.lanes == 1 && c.count >= 2 * kPipeSub)
             return enqueue_verify_piped(c, digest, r, s, qx, qy, ok_out);
         return enqueue_verify(c, digest, r, s, qx, qy, ok_out);
+    });
+}
+
+int sbft_gv_verify_p256_kernel(sbft_gv_ctx* ctx, int kernel, const uint8_t* digest, const uint8_t* r,
+                               const uint8_t* s, const uint8_t* qx, const uint8_t* qy, size_t n, uint8_t* ok_out) {
+    if (!ctx || kernel < SBFT_GV_KERNEL_EXACT || kernel > SBFT_GV_KERNEL_HALF) return SBFT_GV_EINVAL;
+    if (n == 0) return SBFT_GV_OK;
+    if (!digest || !r || !s || !qx || !qy || !ok_out || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
+        Chunk k = c;
+        k.lanes = kernel;
+        return enqueue_verify(k, digest, r, s, qx, qy, ok_out);
     });
 }
 
@@ -2121,15 +2149,36 @@ int sign_wave(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_
     return SBFT_GV_OK;
 }
 
-}  // namespace
+// New client keys whose tables still fit (caller holds keys_mu): the client budget per device
+// (ctx->client_cap, default 1/8 of the device's memory) and, on every device, the memory above
+// the staging reserve. A device with k slots pays k tables per key.
+size_t client_key_room(sbft_gv_ctx* ctx) {
+    const size_t tb = sbft_comb_table_bytes();
+    std::map<int, size_t> spd;
+    for (Slot* sl : ctx->slots) ++spd[sl->device];
+    size_t room = SIZE_MAX;
+    for (const auto& [dev, k] : spd) {
+        size_t free_b = 0, total = 0;
+        if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total) != hipSuccess) return 0;
+        const uint64_t cap = ctx->client_cap ? ctx->client_cap : total / 8;
+        const uint64_t used = (uint64_t)ctx->client_keys * tb * k;
+        const size_t by_cap = used >= cap ? 0 : (size_t)((cap - used) / (tb * k));
+        const uint64_t reserve = std::max<uint64_t>(SBFT_GV_HBM_RESERVE, total / 32);
+        const size_t by_free = free_b <= reserve ? 0 : (size_t)((free_b - reserve) / (tb * k));
+        room = std::min(room, std::min(by_cap, by_free));
+    }
+    return room;
+}
 
-extern "C" {
-
-int sbft_gv_register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy, size_t n, uint32_t* key_ids) {
+// sbft_gv_register_keys with at most max_new keys added (the rest: id 0, not added)
+int register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy, size_t n, uint32_t* key_ids,
+                  bool client, size_t* registered) {
     if (!ctx || (n && (!qx || !qy || !key_ids)) || n > 0xffffffu) return SBFT_GV_EINVAL;
     std::lock_guard<std::mutex> g(ctx->keys_mu);
     const size_t before = ctx->keys.size();
+    const size_t max_new = client ? client_key_room(ctx) : SIZE_MAX;
     std::vector<size_t> pending;  // positions i whose key is new in this call
+    std::vector<uint8_t> held(n, 1);  // 0: past the budget (id 0)
     for (size_t i = 0; i < n; ++i) {
         std::array<uint8_t, 64> k;
         std::memcpy(k.data(), qx + 32 * i, 32);
@@ -2137,6 +2186,11 @@ int sbft_gv_register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy
         auto it = ctx->key_index.find(k);
         if (it != ctx->key_index.end()) {
             key_ids[i] = it->second;  // resolved below for keys added by this call
+            continue;
+        }
+        if (pending.size() >= max_new) {
+            key_ids[i] = 0;
+            held[i] = 0;
             continue;
         }
         const uint32_t id = (uint32_t)ctx->keys.size();
@@ -2184,9 +2238,27 @@ int sbft_gv_register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy
     }
     for (size_t id = before; id < upto; ++id) ctx->key_valid[id] = st[id - before];
     ctx->nkeys = (uint32_t)upto;
-    for (size_t i = 0; i < n; ++i)
-        if (!ctx->key_valid[key_ids[i]]) key_ids[i] = 0;
+    if (client) ctx->client_keys += upto - before;
+    size_t got = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (held[i] && !ctx->key_valid[key_ids[i]]) key_ids[i] = 0;
+        got += key_ids[i] != 0;
+    }
+    if (registered) *registered = got;
     return SBFT_GV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sbft_gv_register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy, size_t n, uint32_t* key_ids) {
+    return register_keys(ctx, qx, qy, n, key_ids, false, nullptr);
+}
+
+int sbft_gv_register_client_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy, size_t n,
+                                 uint32_t* key_ids, size_t* registered) {
+    return register_keys(ctx, qx, qy, n, key_ids, true, registered);
 }
 
 int sbft_gv_register_key(sbft_gv_ctx* ctx, const uint8_t qx[32], const uint8_t qy[32], uint32_t* key_id) {

@@ -56,7 +56,13 @@ SBFT_DEV void block_scan_mul_n(fe& x, u32 (*buf)[W], int tid, bool suffix) {
 // The fully case-split verify (Booth radix-16 digits including zero, explicit infinity and
 // doubling branches in every addition). It runs only for tuples the lean kernel flagged:
 // adversarial inputs whose Shamir ladder hits P + P, P + (-P) or infinity.
-__device__ __noinline__ bool verify_general(const fe& e_raw, const fe& r, const fe& s, const fe& qx,
+// Inlined into its one caller, the fixup kernel. As a __noinline__ function (rounds 1-4) it was
+// over 128 KiB of code, so its branches needed long-branch expansion, and from round 4's build on
+// the compiler used s[30:31] -- the function's return address -- as the long branches' scratch
+// pair: the return jumped into the function's own body and the fixup kernel faulted on its first
+// flagged tuple (tools/scan_retaddr.py, run on every CPU test pass, refuses a build
+// with such a function). A kernel has no return address to lose.
+SBFT_DEV bool verify_general(const fe& e_raw, const fe& r, const fe& s, const fe& qx,
                                             const fe& qy, const u32* gtab) {
     // 1. range checks
     bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
@@ -221,6 +227,14 @@ __global__ __launch_bounds__(256) void p256_verify_fixup_kernel(const uint8_t* _
                                       load_be32(qyy + 32ull * idx), gtab);
         ok[idx] = v ? 1 : 0;
     }
+}
+
+// lanes = 0 (sbft_launch_p256_verify): every tuple through the fixup kernel -- the count and
+// the list 0 .. n-1 written on the device, so the whole launch stays on the stream
+__global__ __launch_bounds__(256) void p256_fixup_all_kernel(uint32_t* __restrict__ work, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) work[0] = n;
+    if (i < n) work[1 + i] = i;
 }
 
 // ------------------------------------------------------------ batched s^-1
@@ -2197,6 +2211,16 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
+    }
+    if (lanes == 0) {  // the exact net alone: every tuple is "flagged"
+        hipLaunchKernelGGL(sbft::p256_fixup_all_kernel, dim3(blocks), dim3(threads), 0, stream, d_work, n);
+        SBFT_STEP("fixup list");
+        if (ev0 && hipEventRecord(ev0, stream) != hipSuccess) return -1;
+        hipLaunchKernelGGL(sbft::p256_verify_fixup_kernel, dim3(blocks < 8u * (unsigned)cus ? blocks : 8u * (unsigned)cus),
+                           dim3(threads), 0, stream, d_digest, d_r, d_s, d_qx, d_qy, d_ok, (const uint32_t*)d_work);
+        if (ev1 && hipEventRecord(ev1, stream) != hipSuccess) return -1;
+        SBFT_STEP("fixup");
+        return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (!work_zeroed && hipMemsetAsync(d_work, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
     SBFT_STEP("memset");

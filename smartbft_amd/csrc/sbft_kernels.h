@@ -32,8 +32,9 @@ size_t sbft_verify_work_bytes(size_t n);
 // once by sbft_launch_gcomb_build; unused when that size is 0).
 // ev0/ev1 (may be NULL): events recorded on the stream right before / after the main
 // verify kernel (kernel timing, sbft_gv_kernel_time). lanes: 1 = the one-lane throughput
-// kernel, 2 / 4 = the small-batch latency kernel with that many lanes per tuple
-// (p256_verify_small_kernel).
+// kernel, 2 = the pair latency kernel (p256_verify_small_kernel<2>), 3 = the half-size-scalar
+// kernel (p256_verify_half_kernel), 0 = every tuple through the exact case-split fixup kernel
+// alone (the net the others hand flagged tuples to; the self-test and tests exercise it this way).
 int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                             const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok, uint32_t n,
                             uint32_t* d_work, const void* d_gcomb, hipStream_t stream,

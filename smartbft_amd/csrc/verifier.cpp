@@ -807,7 +807,7 @@ struct sbft_verifier {
     };
     std::unordered_map<uint64_t, KeyEnt> keys;
     // client-key registry (sbft_verifier_add_clients): request key -> engine key id
-    std::shared_mutex clients_mu;
+    mutable std::shared_mutex clients_mu;
     KeyMap clients;
     // Proposal.Digest memo (view.go:435,443,524 recompute it per proposal): exact-content key
     std::mutex memo_mu;
@@ -1226,12 +1226,19 @@ int sbft_verifier_add_clients(sbft_verifier* v, const uint8_t* pubkeys65, size_t
         which.push_back(i);
         ++m;
     }
-    const int rc = sbft_gv_register_keys(v->ctx, qx.data(), qy.data(), m, ids.data());
+    // under the engine's client-table budget: keys past it get id 0 and stay on the generic path
+    const int rc = sbft_gv_register_client_keys(v->ctx, qx.data(), qy.data(), m, ids.data(), nullptr);
     if (rc) return rc;
     std::unique_lock<std::shared_mutex> g(v->clients_mu);
     for (size_t j = 0; j < m; ++j)
         if (ids[j]) v->clients.put(pubkeys65 + 65 * which[j] + 1, ids[j]);
     return 0;
+}
+
+size_t sbft_verifier_client_count(const sbft_verifier* v) {
+    if (!v) return 0;
+    std::shared_lock<std::shared_mutex> g(v->clients_mu);
+    return v->clients.count;
 }
 
 uint64_t sbft_verifier_verification_sequence(const sbft_verifier* v) { return v ? v->vseq.load() : 0; }
@@ -1384,9 +1391,12 @@ int sbft_verifier_verify_proposal(sbft_verifier* v, const sbft_proposal* p, char
 
 int sbft_verifier_verify_request(sbft_verifier* v, const uint8_t* req, size_t len, char* info, size_t info_cap,
                                  char* err, size_t err_cap) {
-    if (!v || !req) return SBFT_GV_EINVAL;
+    if (!v || (!req && len)) return SBFT_GV_EINVAL;
     Req q;
-    if (!parse_request(req, len, 0, q) || q.pub[0] != 0x04) {
+    // an empty request (a Go nil or zero-length slice arrives as NULL, 0) is a malformed request
+    // from the network, never an engine error: Controller.HandleRequest passes whatever a client
+    // or a forwarding replica sent (controller.go:233-246)
+    if (!req || !parse_request(req, len, 0, q) || q.pub[0] != 0x04) {
         put_err(err, err_cap, "malformed request");
         return SBFT_V_EFORMAT;
     }
@@ -1805,7 +1815,11 @@ void sbft_request_batcher_stats(const sbft_request_batcher* b, uint64_t* launche
 
 int sbft_request_batcher_verify(sbft_request_batcher* b, const uint8_t* req, size_t len, char* info, size_t info_cap,
                                 char* err, size_t err_cap) {
-    if (!b || !req) return SBFT_GV_EINVAL;
+    if (!b || (!req && len)) return SBFT_GV_EINVAL;
+    if (!req) {  // empty request: malformed (as sbft_verifier_verify_request), no batch taken
+        put_err(err, err_cap, "malformed request");
+        return SBFT_V_EFORMAT;
+    }
     using Batch = sbft_request_batcher::Batch;
     sbft_request_batcher::Entry me;
     me.req = req;

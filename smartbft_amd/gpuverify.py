@@ -24,10 +24,14 @@ EXPORTS = [
     "sbft_gv_kernel_timing", "sbft_gv_kernel_time", "sbft_gv_register_keys",
     "sbft_gv_sha256_verify_p256_framed", "sbft_gv_host_alloc", "sbft_gv_host_free",
     "sbft_gv_plan_split", "sbft_gv_sha256_verify_p256_stream", "sbft_gv_inject_fault",
+    "sbft_gv_register_client_keys", "sbft_gv_verify_p256_kernel",
 ]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _vp = ctypes.c_void_p
+
+# sbft_gv_verify_p256_kernel's kernel names (include/sbft_gpuverify.h)
+KERNEL_EXACT, KERNEL_THROUGHPUT, KERNEL_PAIR, KERNEL_HALF = 0, 1, 2, 3
 
 
 class GpuVerifyError(RuntimeError):
@@ -36,9 +40,9 @@ class GpuVerifyError(RuntimeError):
 
 class Opts(ctypes.Structure):
     _fields_ = [("device_mask", ctypes.c_uint32), ("min_split", ctypes.c_uint32),
-                ("pair_max", ctypes.c_int32), ("quad_max", ctypes.c_int32),
+                ("pair_max", ctypes.c_int32), ("reserved0", ctypes.c_int32),
                 ("slots_per_device", ctypes.c_uint32), ("half_max", ctypes.c_int32),
-                ("reserved", ctypes.c_uint64 * 2)]
+                ("client_table_bytes", ctypes.c_uint64), ("reserved", ctypes.c_uint64 * 1)]
 
 
 _LIB = None
@@ -60,6 +64,7 @@ def load_library():
     L.sbft_gv_strerror.argtypes = [ctypes.c_int]
     L.sbft_gv_strerror.restype = ctypes.c_char_p
     L.sbft_gv_verify_p256.argtypes = [_vp] + [_u8p] * 5 + [ctypes.c_size_t, _u8p]
+    L.sbft_gv_verify_p256_kernel.argtypes = [_vp, ctypes.c_int] + [_u8p] * 5 + [ctypes.c_size_t, _u8p]
     L.sbft_gv_sha256.argtypes = [_vp, _u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64),
                                  ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, _u8p]
     L.sbft_gv_sha256_verify_p256.argtypes = [_vp, _u8p, ctypes.c_size_t,
@@ -88,6 +93,8 @@ def load_library():
     _u32p = ctypes.POINTER(ctypes.c_uint32)
     L.sbft_gv_register_key.argtypes = [_vp, _u8p, _u8p, _u32p]
     L.sbft_gv_register_keys.argtypes = [_vp, _u8p, _u8p, ctypes.c_size_t, _u32p]
+    L.sbft_gv_register_client_keys.argtypes = [_vp, _u8p, _u8p, ctypes.c_size_t, _u32p,
+                                               ctypes.POINTER(ctypes.c_size_t)]
     L.sbft_gv_verify_p256_keyed.argtypes = [_vp] + [_u8p] * 3 + [_u32p, ctypes.c_size_t, _u8p]
     L.sbft_gv_sha256_verify_p256_keyed.argtypes = [_vp, _u8p, ctypes.c_size_t,
                                                    ctypes.POINTER(ctypes.c_uint64), _u32p, _u8p, _u8p,
@@ -218,17 +225,18 @@ class GpuVerifier:
     """One sbft_gv_ctx. Host-array calls are synchronous; *_dev calls take torch tensors
     (device-resident) and enqueue on the given (or current) stream."""
 
-    def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0, quad_max: int = 0,
-                 slots_per_device: int = 0, half_max: int = 0):
+    def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0,
+                 slots_per_device: int = 0, half_max: int = 0, client_table_bytes: int = 0):
         """pair_max / half_max: per-device batches of at most this many tuples run the pair
         latency kernel (two lanes per tuple) / the half-size-scalar kernel (four lanes: two 128-bit
-        ladders), half_max taking precedence (0 = library default, negative = never). quad_max is
-        accepted and ignored (round 3's four-lane pair form is gone).
+        ladders), half_max taking precedence (0 = library default, negative = never; pair_max < 0
+        with half_max 0 forces the one-lane throughput kernel).
         slots_per_device > 1: that many engine slots per GPU, each taking a share of a split
-        batch as a separate device would (runs the multi-device split on one GPU)."""
+        batch as a separate device would (runs the multi-device split on one GPU).
+        client_table_bytes: per-device budget of client-key comb tables (0 = 1/8 of the device)."""
         self.L = load_library()
         ctx = _vp()
-        opts = Opts(device_mask, min_split, pair_max, quad_max, slots_per_device, half_max)
+        opts = Opts(device_mask, min_split, pair_max, 0, slots_per_device, half_max, client_table_bytes)
         rc = self.L.sbft_gv_init(ctypes.byref(opts), ctypes.byref(ctx))
         if rc:
             raise GpuVerifyError(f"sbft_gv_init: {self.L.sbft_gv_strerror(rc).decode()} ({rc})")
@@ -261,6 +269,16 @@ class GpuVerifier:
                     "sbft_gv_verify_p256")
         return ok
 
+    def verify_kernel(self, kernel: int, digest, r, s, qx, qy) -> np.ndarray:
+        """sbft_gv_verify_p256_kernel: the same verify on a named kernel (KERNEL_EXACT,
+        KERNEL_THROUGHPUT, KERNEL_PAIR, KERNEL_HALF)."""
+        n = len(digest)
+        arrs = [_soa(a, n) for a in (digest, r, s, qx, qy)]
+        ok = np.zeros(n, dtype=np.uint8)
+        self._check(self.L.sbft_gv_verify_p256_kernel(self.ctx, kernel, *[_p(a) for a in arrs], n, _p(ok)),
+                    "sbft_gv_verify_p256_kernel")
+        return ok
+
     def register_key(self, qx: bytes, qy: bytes) -> int:
         """Precompute the comb tables of a (consenter) key; returns its key id (>= 1). Raises
         GpuVerifyError for a key that is not a valid P-256 point."""
@@ -270,17 +288,24 @@ class GpuVerifier:
         self._check(self.L.sbft_gv_register_key(self.ctx, kx, ky, ctypes.byref(kid)), "sbft_gv_register_key")
         return kid.value
 
-    def register_keys(self, qx, qy) -> np.ndarray:
-        """Batch registration (one table-build launch per device): key ids, 0 for invalid keys."""
+    def register_keys(self, qx, qy, client: bool = False) -> np.ndarray:
+        """Batch registration (one table-build launch per device): key ids, 0 for invalid keys.
+        client=True: sbft_gv_register_client_keys, under the client-table budget (keys past it
+        also get id 0)."""
         n = len(qx)
         if n and isinstance(qx[0], (bytes, bytearray)):
             qx = np.frombuffer(b"".join(qx), dtype=np.uint8).reshape(n, 32)
             qy = np.frombuffer(b"".join(qy), dtype=np.uint8).reshape(n, 32)
         ax, ay = _soa(qx, n), _soa(qy, n)
         ids = np.zeros(n, dtype=np.uint32)
-        self._check(self.L.sbft_gv_register_keys(self.ctx, _p(ax), _p(ay), n,
-                                                 ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))),
-                    "sbft_gv_register_keys")
+        pids = ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        if client:
+            got = ctypes.c_size_t()
+            self._check(self.L.sbft_gv_register_client_keys(self.ctx, _p(ax), _p(ay), n, pids, ctypes.byref(got)),
+                        "sbft_gv_register_client_keys")
+            assert got.value == int(np.count_nonzero(ids))
+        else:
+            self._check(self.L.sbft_gv_register_keys(self.ctx, _p(ax), _p(ay), n, pids), "sbft_gv_register_keys")
         return ids
 
     def verify_keyed(self, digest, r, s, key_ids) -> np.ndarray:
@@ -401,11 +426,18 @@ class GpuVerifier:
         import torch
         s = stream if stream is not None else torch.cuda.current_stream(device)
         with torch.cuda.stream(s):
-            off = d_off.view(torch.int64) if d_off.dtype == torch.uint64 else d_off.to(torch.int64)
-            ln = d_len.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
-            bad = (off < 0) | (off + ln > d_blob.numel())
-            if bool(bad.any()):
+            if bool(GpuVerifier._blob_bounds_bad(d_off, d_len, d_blob.numel()).any()):
                 raise ValueError("a message extends past the end of the blob (or its offset is >= 2^63)")
+
+    @staticmethod
+    def _blob_bounds_bad(d_off, d_len, blob_bytes: int):
+        """Per message: True unless [off, off + len) lies inside a blob of blob_bytes bytes (any
+        device; tests/test_abi.py runs it on CPU tensors). off + len is never formed: it wraps
+        for an offset near 2^63 (a uint64 offset >= 2^63 reads as negative int64)."""
+        import torch
+        off = d_off.view(torch.int64) if d_off.dtype == torch.uint64 else d_off.to(torch.int64)
+        ln = d_len.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        return (off < 0) | (ln > blob_bytes) | (off > blob_bytes - ln)
 
     def verify_dev(self, d_digest, d_r, d_s, d_qx, d_qy, d_ok, stream=None):
         n = d_ok.numel()

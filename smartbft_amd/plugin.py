@@ -119,6 +119,8 @@ def _lib():
     L.sbft_verifier_free.restype = None
     L.sbft_verifier_add_consenter.argtypes = [_vp, ctypes.c_uint64, _u8p]
     L.sbft_verifier_add_clients.argtypes = [_vp, _u8p, ctypes.c_size_t]
+    L.sbft_verifier_client_count.argtypes = [_vp]
+    L.sbft_verifier_client_count.restype = ctypes.c_size_t
     L.sbft_verifier_verification_sequence.restype = ctypes.c_uint64
     L.sbft_verifier_verification_sequence.argtypes = [_vp]
     L.sbft_verifier_set_verification_sequence.argtypes = [_vp, ctypes.c_uint64]
@@ -251,6 +253,10 @@ class Verifier:
         rc = self.L.sbft_verifier_add_clients(self.h, _buf(blob, keep), len(pubkeys65))
         if rc:
             raise VerifyError(rc, "client key registration failed")
+
+    def client_count(self) -> int:
+        """Client keys registered so far (registration stops at the engine's table budget)."""
+        return self.L.sbft_verifier_client_count(self.h)
 
     def VerificationSequence(self) -> int:
         return self.L.sbft_verifier_verification_sequence(self.h)

@@ -149,3 +149,36 @@ def test_half_kernel_constants():
     hg = open(os.path.join(ROOT, "smartbft_amd", "csrc", "p256_halfgcd.hpp")).read()
     m = re.search(r"#define SBFT_HGCD_N \{([^}]*)\}", hg)
     assert sum(int(w.strip().rstrip("u"), 16) << (32 * i) for i, w in enumerate(m.group(1).split(","))) == N
+
+
+def test_blob_bounds_predicate_does_not_wrap():
+    """_blob_bounds_bad (the device-resident hash entries' offset check) compares without forming
+    off + len, so offsets near 2^63 are refused instead of wrapping into range."""
+    import torch
+    from smartbft_amd.gpuverify import GpuVerifier
+    off = torch.tensor([0, 246, 247, (1 << 63) - 1, (1 << 63) - 5, -1, 0], dtype=torch.int64)
+    ln = torch.tensor([256, 10, 10, 10, 4, 1, 257], dtype=torch.int32)
+    got = GpuVerifier._blob_bounds_bad(off, ln, 256).tolist()
+    assert got == [False, False, True, True, True, True, True]
+    u = torch.tensor([0, 1 << 63, (1 << 64) - 1], dtype=torch.uint64)  # >= 2^63 reads negative
+    assert GpuVerifier._blob_bounds_bad(u, torch.tensor([1, 1, 1], dtype=torch.int32), 256).tolist() == \
+        [False, True, True]
+    big = torch.tensor([0], dtype=torch.int32) - 1  # length 2^32 - 1 as uint32
+    assert GpuVerifier._blob_bounds_bad(torch.tensor([0]), big, 256).tolist() == [True]
+
+
+def test_no_device_function_overwrites_its_return_address():
+    """The built library holds no non-kernel device function that writes s[30:31], its return
+    address (tools/scan_retaddr.py). ROCm 7.2's branch relaxation did this in the >128 KiB
+    verify_general (the fixup kernel's callee) from round 4 on, and the fixup kernel faulted on its
+    first flagged tuple."""
+    import shutil
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump") or not shutil.which("python3"):
+        pytest.skip("no ROCm llvm-objdump")
+    sys_path = os.path.join(ROOT, "tools")
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("scan_retaddr", os.path.join(sys_path, "scan_retaddr.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    from smartbft_amd import gpuverify
+    assert mod.offenders(gpuverify.LIB_PATH) == []

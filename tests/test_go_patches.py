@@ -81,9 +81,15 @@ def test_go_binding_fails_stop_on_engine_errors():
     error: every entry point that can see one hands it to failStop."""
     src = open(os.path.join(ROOT, "go", "gpuverify", "verifier.go")).read()
     bat = open(os.path.join(ROOT, "go", "gpuverify", "batcher.go")).read()
-    assert "func engineFailure(rc C.int) bool { return rc < 0 && rc > C.SBFT_V_EVERIFY }" in src
+    # engine codes only (ENODEV .. ESELFTEST); EINVAL and verdicts come back as VerifyError
+    assert "func engineFailure(rc C.int) bool { return rc <= C.SBFT_GV_ENODEV && rc >= C.SBFT_GV_ESELFTEST }" in src
     for op in ("VerifyProposal", "VerifyRequest", "VerifyConsenterSig", "VerifyConsenterSigs", "VerifySignature",
                "PruneSet"):
         assert f'v.failStop("{op}", rc)' in src, op
     assert 'rv.failStop("VerifyRequest", rc)' in bat
+    # every failStop is behind engineFailure: bad input (EINVAL, EFORMAT) never stops a replica
+    assert src.count("if engineFailure(rc) {") == 6, src.count("if engineFailure(rc) {")
+    assert bat.count("if engineFailure(rc) {") == 1
+    test = open(os.path.join(ROOT, "go", "gpuverify", "verifier_test.go")).read()
+    assert "func TestVerifyRequestEmptyIsMalformed" in test and "[][]byte{nil, {}}" in test
     assert "log.Fatalf" in src

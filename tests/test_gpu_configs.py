@@ -115,6 +115,49 @@ def test_config3_verify_proposal_10k_registered_clients(gpu, requests_10k):
     full.close()
 
 
+def test_config3_client_table_budget(requests_10k):
+    """The client-key registry under an HBM budget: with room for 3,000 clients'
+    tables, registering all 10,000 registers 3,000 and leaves the rest on the generic path -- no
+    error, now or at proposal time -- and a proposal mixing registered and unregistered clients
+    gets the oracle's verdicts. Consenter keys are not budgeted. With 2 slots per device each key
+    costs two tables, so the same budget holds half as many clients."""
+    from smartbft_amd import GpuVerifier, plugin
+    reqs = requests_10k
+    tb = 512 << 10
+    gv = GpuVerifier(device_mask=1, client_table_bytes=3000 * tb)
+    try:
+        v = plugin.Verifier(gv, 1)
+        v.add_clients([q[-129:-64] for q in reqs])
+        assert v.client_count() == 3000
+        v.add_clients([q[-129:-64] for q in reqs[::-1]])  # budget spent: nothing more, no error
+        assert v.client_count() == 3000
+        ids = gv.register_keys(np.stack([np.frombuffer(q[-128:-96], np.uint8) for q in reqs[:5]]),
+                               np.stack([np.frombuffer(q[-96:-64], np.uint8) for q in reqs[:5]]), client=True)
+        assert (ids != 0).all()  # keys already registered keep their ids
+        p = plugin.Proposal(plugin.encode_payload(reqs), b"header", b"metadata", 1)
+        want = [(f"client{31337 + i}", f"tx{31337 + i}") for i in range(10_000)]
+        assert [(i.ClientID, i.ID) for i in v.VerifyProposal(p)] == want
+        for where, kind in CASES:
+            _check_proposal(v, reqs, where, kind)
+        sg = plugin.Signer(gv, 7, (12345).to_bytes(32, "big"))
+        v.add_consenter(7, sg.public_key())  # past the client budget: consenters still register
+        assert v.VerifyConsenterSigs([sg.SignProposal(p, b"x")], p) == [0]
+        sg.close()
+        v.close()
+    finally:
+        gv.close()
+    gv2 = GpuVerifier(device_mask=1, slots_per_device=2, client_table_bytes=3000 * tb)
+    try:
+        v2 = plugin.Verifier(gv2, 1)
+        v2.add_clients([q[-129:-64] for q in reqs[:4000]])
+        assert v2.client_count() == 1500
+        p = plugin.Proposal(plugin.encode_payload(reqs[:4000]), b"header", b"metadata", 1)
+        assert len(v2.VerifyProposal(p)) == 4000
+        v2.close()
+    finally:
+        gv2.close()
+
+
 # ---------------------------------------------------------------- config 5
 def _config5_batch(n, seed, sign_with_gpu=None):
     """n messages, lengths uniform in [1 KiB, 64 KiB], each signed under its own key; ~1/5 with

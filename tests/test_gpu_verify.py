@@ -526,6 +526,8 @@ def test_device_hash_bounds_checked_on_launch_stream(gpu):
         gpu.sha256_dev(blob, off, ln, dig, stream=side)
     with pytest.raises(ValueError):
         gpu.sha256_dev(blob, torch.tensor([0, 1 << 63], dtype=torch.uint64, device=dev), ln, dig)
+    with pytest.raises(ValueError):  # off + len would wrap to a small negative int64
+        gpu.sha256_dev(blob, torch.tensor([0, (1 << 63) - 1], dtype=torch.int64, device=dev), ln, dig)
     ok_off = torch.tensor([1, 200], dtype=torch.int64, device=dev)
     gpu.sha256_dev(blob, ok_off, ln, dig)
     gpu.sha256_dev(blob, ok_off, ln, dig, check=False)
