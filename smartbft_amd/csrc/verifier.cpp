@@ -9,6 +9,7 @@
 #include "engine_internal.h"
 #include "modn_host.hpp"
 
+#include <pthread.h>
 #include <cpuid.h>
 #include <immintrin.h>
 
@@ -489,7 +490,10 @@ struct ParsePool {
             std::lock_guard<std::mutex> lk(mu);
             if (!started) {
                 for (int t = 1; t < kMax; ++t) {
-                    th[t - 1] = std::thread([this, t] { worker(t); });
+                    th[t - 1] = std::thread([this, t] {
+                        pthread_setname_np(pthread_self(), "sbft-parse");
+                        worker(t);
+                    });
                     th[t - 1].detach();  // process-lifetime helpers
                 }
                 started = true;

@@ -67,6 +67,25 @@ def test_verify_request(net):
         v.VerifyRequest(r[:10])
 
 
+def test_empty_request_is_malformed_not_an_engine_error(net):
+    """An empty request (Go's nil / []byte{}, passed as NULL, 0) is a malformed request from the
+    network: SBFT_V_EFORMAT, which the Go binding returns as a VerifyError. Before round 5 it was
+    SBFT_GV_EINVAL, which the binding's fail-stop would have turned into a replica exit."""
+    v, nodes, clients = net
+    for req in (b"", None):
+        with pytest.raises(plugin.VerifyError) as ei:
+            v.VerifyRequest(req or b"")
+        assert ei.value.code == plugin.EFORMAT
+    b = plugin.RequestBatcher(v, max_batch=4, max_wait_us=100)
+    with pytest.raises(plugin.VerifyError) as ei:
+        b.VerifyRequest(b"")
+    assert ei.value.code == plugin.EFORMAT
+    assert b.stats() == (0, 0)  # refused before joining a batch
+    r = clients[0].make_request("alice", "43", b"hi")
+    assert b.VerifyRequest(r).ID == "43"
+    b.close()
+
+
 def test_requests_signatures_verify_under_oracle(net):
     """The engine's RFC 6979 signatures are valid ECDSA under the independent oracle."""
     v, nodes, clients = net

@@ -45,8 +45,10 @@
 #include <linux/futex.h>
 #include <pthread.h>
 #include <sched.h>
+#include <dirent.h>
 #include <sys/resource.h>
 #include <sys/syscall.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <climits>
@@ -59,6 +61,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -87,6 +90,101 @@ static double pct(std::vector<double> v, double p) {
 static long futex(std::atomic<int>* a, int op, int val) {
     return syscall(SYS_futex, reinterpret_cast<int*>(a), op, val, nullptr, nullptr, 0);
 }
+// A blocking wait with a bounded spin, as a Go select parks its goroutine: spin up to spin_us for
+// ready(), then sleep on a futex that notify() (the producers: arriving votes, finished batches)
+// bumps. No lost wake-up: the waiter reads ev, announces itself, re-checks ready(), and only then
+// sleeps on ev's old value; a producer publishes its data, bumps ev, then wakes a sleeper.
+struct Waker {
+    std::atomic<int> ev{0}, sleeping{0};
+    long spin_us = 20;
+    void notify() {
+        ev.fetch_add(1, std::memory_order_seq_cst);
+        if (sleeping.load(std::memory_order_seq_cst)) futex(&ev, FUTEX_WAKE_PRIVATE, 1);
+    }
+    template <class Ready>
+    void wait(Ready ready) {
+        const auto t0 = Clock::now();
+        while (!ready()) {
+            if (Clock::now() - t0 < std::chrono::microseconds(spin_us)) {
+                __builtin_ia32_pause();
+                continue;
+            }
+            const int e = ev.load(std::memory_order_seq_cst);
+            sleeping.store(1, std::memory_order_seq_cst);
+            if (!ready()) futex(&ev, FUTEX_WAIT_PRIVATE, e);
+            sleeping.store(0, std::memory_order_relaxed);
+        }
+    }
+};
+static long env_long(const char* name, long dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atol(e) : dflt;
+}
+// this thread's CPU time, nanoseconds
+static int64_t thread_cpu_ns() {
+    timespec ts{};
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+// CPU time of this process's threads by name (/proc/self/task/*/stat utime + stime), ms: the
+// harness names its threads (voter, collector, batch worker), the engine its own (sbft-*), the
+// HIP runtime's keep theirs
+struct ThreadCpu {
+    std::map<long, std::pair<std::string, double>> by_tid;
+    static ThreadCpu now() {
+        ThreadCpu t;
+        const double tick_ms = 1000.0 / (double)sysconf(_SC_CLK_TCK);
+        DIR* d = opendir("/proc/self/task");
+        if (!d) return t;
+        while (dirent* e = readdir(d)) {
+            if (e->d_name[0] == '.') continue;
+            char path[300], buf[1024];
+            std::snprintf(path, sizeof path, "/proc/self/task/%s/stat", e->d_name);
+            FILE* f = std::fopen(path, "r");
+            if (!f) continue;
+            const size_t got = std::fread(buf, 1, sizeof buf - 1, f);
+            std::fclose(f);
+            buf[got] = 0;
+            char* l = std::strchr(buf, '(');
+            char* r = std::strrchr(buf, ')');
+            if (!l || !r) continue;
+            std::string comm(l + 1, r);
+            // fields after ')': state(3) ... utime(14) stime(15)
+            unsigned long ut = 0, st = 0;
+            int field = 3;
+            for (char* p = std::strtok(r + 2, " "); p; p = std::strtok(nullptr, " "), ++field) {
+                if (field == 14) ut = std::strtoul(p, nullptr, 10);
+                if (field == 15) {
+                    st = std::strtoul(p, nullptr, 10);
+                    break;
+                }
+            }
+            t.by_tid[std::atol(e->d_name)] = {comm, (ut + st) * tick_ms};
+        }
+        closedir(d);
+        return t;
+    }
+    // per-name CPU ms between `before` and this snapshot (threads started since count whole)
+    std::map<std::string, double> since(const ThreadCpu& before) const {
+        std::map<std::string, double> out;
+        for (const auto& [tid, v] : by_tid) {
+            auto it = before.by_tid.find(tid);
+            out[v.first] += v.second - (it != before.by_tid.end() ? it->second.second : 0.0);
+        }
+        return out;
+    }
+};
+static std::string cpu_json(const std::map<std::string, double>& m, double per) {
+    std::string s = "{";
+    for (const auto& [k, v] : m) {
+        if (v <= 0) continue;
+        char b[160];
+        std::snprintf(b, sizeof b, "%s\"%s\": %.3f", s.size() > 1 ? ", " : "", k.c_str(), v / per);
+        s += b;
+    }
+    return s + "}";
+}
+
 static std::vector<double> fan_out(size_t n, int rounds, const std::function<void(size_t, int)>& run) {
     std::atomic<int> gen{-1}, remaining{0}, done_gen{-1};
     std::atomic<bool> stop{false};
@@ -312,23 +410,30 @@ struct BatchWorker {
     std::vector<int32_t> res;
     int rc = 0;
     const std::atomic<int>* armed = nullptr;  // the channel's decision is collecting: stay awake
+    Waker* done = nullptr;                    // the collector's wait, notified when a batch is done
+    std::atomic<int64_t>* engine_ns = nullptr;  // CPU time spent inside the engine's calls
+    long spin_us = 10;  // after a batch, spin this long for the next one (SBFT_HOOK_WORKER_SPIN_US)
     void start() {
         th = std::thread([this] {
+            pthread_setname_np(pthread_self(), "h-bworker");
             for (;;) {
                 int s;
                 const auto t0 = Clock::now();
                 while ((s = st.load(std::memory_order_acquire)) != 1 && s != 3) {
                     if ((armed && armed->load(std::memory_order_relaxed)) ||
-                        Clock::now() - t0 < std::chrono::microseconds(50)) {  // a batch follows an
-                        __builtin_ia32_pause();                               // arrival closely
+                        Clock::now() - t0 < std::chrono::microseconds(spin_us)) {  // a batch follows
+                        __builtin_ia32_pause();                                    // an arrival closely
                         continue;
                     }
                     futex(&st, FUTEX_WAIT_PRIVATE, s);
                 }
                 if (s == 3) return;
                 res.assign(batch.size(), 0);
+                const int64_t c0 = thread_cpu_ns();
                 rc = sbft_verifier_verify_consenter_sigs(v, batch.data(), batch.size(), p, res.data());
+                if (engine_ns) engine_ns->fetch_add(thread_cpu_ns() - c0, std::memory_order_relaxed);
                 st.store(2, std::memory_order_release);
+                if (done) done->notify();
             }
         });
     }
@@ -359,12 +464,18 @@ struct HookChannel {
     std::vector<std::thread> th;
     std::vector<std::unique_ptr<BatchWorker>> w;
     int launches = 0, wrong = 0;
+    // the collector (the View goroutine) blocks while nothing arrives, as processCommits' select
+    // does (view.go:532-549); SBFT_HOOK_COLLECT_SPIN_US bounds its spin first (default 20 us)
+    Waker waker;
+    std::atomic<int64_t> engine_ns{0};
 
     void start() {
+        waker.spin_us = env_long("SBFT_HOOK_COLLECT_SPIN_US", 20);
         order.reset(new std::atomic<int>[voters]);
         for (int i = 0; i < voters; ++i) order[i].store(0);
         for (int i = 0; i < voters; ++i)
             th.emplace_back([this, i] {
+                pthread_setname_np(pthread_self(), "h-voter");
                 int seen = -1;
                 for (;;) {
                     int g;
@@ -378,6 +489,7 @@ struct HookChannel {
                     seen = g;
                     const int k = arrived.fetch_add(1, std::memory_order_acq_rel);
                     order[k].store(i + 1, std::memory_order_release);
+                    waker.notify();
                 }
             });
         const char* e = std::getenv("SBFT_HOOK_ARM");
@@ -386,8 +498,16 @@ struct HookChannel {
             w.emplace_back(new BatchWorker());
             w.back()->v = v;
             w.back()->armed = &armed;
+            w.back()->done = &waker;
+            w.back()->engine_ns = &engine_ns;
+            w.back()->spin_us = env_long("SBFT_HOOK_WORKER_SPIN_US", 10);
             w.back()->start();
         }
+    }
+    bool worker_done() const {
+        for (auto& x : w)
+            if (x->st.load(std::memory_order_acquire) == 2) return true;
+        return false;
     }
     void finish() {
         stop_.store(true);
@@ -459,7 +579,8 @@ struct HookChannel {
             }
             if (!progress) {
                 if (a == voters && in_flight == 0 && pending.empty()) break;  // all in, quorum short
-                __builtin_ia32_pause();
+                // nothing to do: sleep until a vote arrives or a batch finishes (select)
+                waker.wait([&] { return arrived.load(std::memory_order_acquire) > consumed || worker_done(); });
             }
         }
         const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
@@ -469,9 +590,9 @@ struct HookChannel {
         for (auto& x : w)
             while (x->st.load(std::memory_order_acquire) != 0) {
                 if (x->st.load(std::memory_order_acquire) == 2) harvest(*x);
-                else __builtin_ia32_pause();
+                else waker.wait([&] { return x->st.load(std::memory_order_acquire) != 1; });
             }
-        while (arrived.load(std::memory_order_acquire) < voters) __builtin_ia32_pause();
+        waker.wait([&] { return arrived.load(std::memory_order_acquire) >= voters; });
         for (int k = 0; k < voters; ++k)
             while (order[k].load(std::memory_order_acquire) == 0) __builtin_ia32_pause();
         return us;
@@ -722,6 +843,8 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
     std::atomic<int> wrong{0};
     double wall_s = 0, cpu0 = 0, cpu1 = 0;
     CgroupCpu cg0, cg1;
+    ThreadCpu tc0, tc1;
+    std::atomic<int64_t> engine_ns{0};
     int launches = 0;
     if (gpu) {
         sbft_gv_ctx* ctx = nullptr;
@@ -748,6 +871,7 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
             ch.start();
         }
         auto run = [&](int c, int from, int to) {
+            pthread_setname_np(pthread_self(), "h-collect");
             HookChannel& ch = *chs[c];
             VoteSet& s = *sets[c];
             std::vector<sbft_signature> prev(voters);
@@ -758,7 +882,9 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
                 for (int i = 0; i < voters; ++i)  // the previous block's commit signatures
                     prev[i] = sbft_signature{(uint64_t)(i + 2), s.vals[pb][i].data(), 64, s.msgs[pb][i].data(),
                                              s.msgs[pb][i].size()};
+                const int64_t c0 = thread_cpu_ns();
                 if (sbft_verifier_verify_consenter_sigs(vs[c], prev.data(), voters, &s.props[pb], st.data())) wrong++;
+                if (g >= 0) engine_ns.fetch_add(thread_cpu_ns() - c0, std::memory_order_relaxed);
                 for (int i = 0; i < voters; ++i) wrong += st[i] != 0;
                 ch.decide(g + 10, b, g % 10 == 9);
                 if (g >= 0) lat[c].push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
@@ -769,9 +895,13 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
             for (int c = 0; c < channels; ++c) th.emplace_back(run, c, -5, 0);
             for (auto& t : th) t.join();
         }
-        for (auto& ch : chs) ch->launches = 0;
+        for (auto& ch : chs) {
+            ch->launches = 0;
+            ch->engine_ns = 0;
+        }
         cg0 = cgroup_cpu();
         cpu0 = proc_cpu_us();
+        tc0 = ThreadCpu::now();
         const auto t0 = Clock::now();
         {
             std::vector<std::thread> th;
@@ -779,12 +909,14 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
             for (auto& t : th) t.join();
         }
         wall_s = std::chrono::duration<double>(Clock::now() - t0).count();
+        tc1 = ThreadCpu::now();
         cpu1 = proc_cpu_us();
         cg1 = cgroup_cpu();
         for (auto& ch : chs) {
             ch->finish();
             wrong += ch->wrong;
             launches += ch->launches;
+            engine_ns += ch->engine_ns.load();
         }
         sets.clear();
         for (auto* v : vs) sbft_verifier_free(v);
@@ -806,9 +938,16 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
         for (int c = 0; c < channels; ++c) gen.emplace_back(new std::atomic<int>(-1));
         std::atomic<bool> stop{false};
         std::vector<std::thread> vth;
+        // the View blocks on the valid-vote channel as the GPU side's collector does (Waker)
+        std::vector<std::unique_ptr<Waker>> wk;
+        for (int c = 0; c < channels; ++c) {
+            wk.emplace_back(new Waker());
+            wk.back()->spin_us = env_long("SBFT_HOOK_COLLECT_SPIN_US", 20);
+        }
         for (int c = 0; c < channels; ++c)
             for (int i = 0; i < voters; ++i)
                 vth.emplace_back([&, c, i] {
+                    pthread_setname_np(pthread_self(), "h-voter");
                     int seen = -1;
                     for (;;) {
                         int g;
@@ -817,18 +956,22 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
                         if (stop.load()) return;
                         for (int k = seen + 1; k <= g; ++k) {  // every decision released since
                             const bool bad = k % 10 == 4 && i == 7;
-                            if (cpu_verify(votes[c][i]) && !bad) valid[c][k].fetch_add(1, std::memory_order_acq_rel);
+                            if (cpu_verify(votes[c][i]) && !bad) {
+                                valid[c][k].fetch_add(1, std::memory_order_acq_rel);
+                                wk[c]->notify();
+                            }
                         }
                         seen = g;
                     }
                 });
         auto run = [&](int c, int from, int to) {
+            pthread_setname_np(pthread_self(), "h-collect");
             for (int g = from; g < to; ++g) {
                 const auto t0 = Clock::now();
                 for (int i = 0; i < voters; ++i) wrong += !cpu_verify(prev[c][i]);  // serial (view.go:630-644)
                 gen[c]->store(g, std::memory_order_release);
                 futex(gen[c].get(), FUTEX_WAKE_PRIVATE, INT_MAX);
-                while (valid[c][g].load(std::memory_order_acquire) < need) __builtin_ia32_pause();
+                wk[c]->wait([&] { return valid[c][g].load(std::memory_order_acquire) >= need; });
                 if (g >= 5) lat[c].push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
             }
         };
@@ -839,6 +982,7 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
         }
         cg0 = cgroup_cpu();
         cpu0 = proc_cpu_us();
+        tc0 = ThreadCpu::now();
         const auto t0 = Clock::now();
         {
             std::vector<std::thread> th;
@@ -846,6 +990,7 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
             for (auto& t : th) t.join();
         }
         wall_s = std::chrono::duration<double>(Clock::now() - t0).count();
+        tc1 = ThreadCpu::now();
         cpu1 = proc_cpu_us();
         cg1 = cgroup_cpu();
         stop.store(true);
@@ -863,10 +1008,11 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
     const double nd = (double)channels * decisions;
     std::printf("{\"mode\": \"quorum-pipe\", \"backend\": \"%s\", \"channels\": %d, \"decisions_per_channel\": %d, "
                 "\"decisions_per_s\": %.1f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"cpu_ms_per_decision\": %.3f, "
+                "\"engine_call_cpu_ms_per_decision\": %.3f, \"cpu_ms_per_decision_by_thread\": %s, "
                 "\"launches_per_decision\": %.2f, \"cgroup_throttled\": %lld, \"wrong_verdicts\": %d}\n",
                 gpu ? "gpu" : "cpu", channels, decisions, nd / wall_s, pct(all, 50) / 1e3, pct(all, 99) / 1e3,
-                (cpu1 - cpu0) / 1e3 / nd, gpu ? 1.0 + (double)launches / nd : 0.0,
-                cg1.nr_throttled - cg0.nr_throttled, wrong.load());
+                (cpu1 - cpu0) / 1e3 / nd, engine_ns.load() / 1e6 / nd, cpu_json(tc1.since(tc0), nd).c_str(),
+                gpu ? 1.0 + (double)launches / nd : 0.0, cg1.nr_throttled - cg0.nr_throttled, wrong.load());
     return wrong.load() ? 2 : 0;
 }
 

@@ -7,4 +7,4 @@ from smartbft_amd import GpuVerifier
 g = GpuVerifier(device_mask=1); print('init ok'); g.close()
 g = GpuVerifier(); print('init ok (all devices)'); g.close()" > gpurun_out/r04c_init.log 2>&1
 rc=$?; grep -v "^W2026\|amdgpu.ids" gpurun_out/r04c_init.log | tail -15; [ $rc -ne 0 ] && exit $rc
-bash tools/gpu_r04a.sh
+bash tools/rounds/gpu_r04a.sh
