@@ -365,7 +365,12 @@ def latency_configs(gv, calls: int):
                                                          "as votes arrive (processCommits batch hook, 2 in flight)")
     # pipelined decisions (config 4): 2 consensus instances deciding back to back on the node
     # (prev-commit batch of 67, then 66 arriving votes each); GPU (patched library) against
-    # OpenSSL (stock library: serial prev-commit loop, a thread per vote) on the same cores
+    # OpenSSL (stock library: serial prev-commit loop, a goroutine per vote) on the same cores.
+    # Votes are delivered (and, on the CPU side, verified) by host_cores / 2 threads per channel,
+    # as the Go runtime runs goroutines on GOMAXPROCS threads; the View blocks while it waits
+    # (round 5; round 4 ran a thread per vote and spinning waits: its CPU per decision was the
+    # harness's, profiles/r05c_config4_ab.txt). engine_call_cpu_ms_per_decision is the CPU time
+    # spent inside the engine's calls alone.
     pipe = {b: _harness("quorum-pipe", 2, max(100, calls), b) for b in ("gpu", "cpu")}
     if pipe["gpu"] and pipe["cpu"]:
         assert pipe["gpu"]["wrong_verdicts"] == 0 and pipe["cpu"]["wrong_verdicts"] == 0
@@ -373,7 +378,8 @@ def latency_configs(gv, calls: int):
             "gpu": pipe["gpu"], "cpu_openssl": pipe["cpu"],
             "decisions_per_s_vs_cpu": round(pipe["gpu"]["decisions_per_s"] / pipe["cpu"]["decisions_per_s"], 2),
             "path": "tools/latency_harness quorum-pipe: 2 channels x back-to-back decisions, each = "
-                    "verifyPrevCommitSignatures (67) + processCommits (66 of 67 arriving votes)"}
+                    "verifyPrevCommitSignatures (67) + processCommits (66 of 67 arriving votes); votes "
+                    "delivered by host_cores/2 threads per channel, blocking waits"}
     stock = _harness("quorum-gpu", 66, calls, 0, 0)
     coal = _harness("quorum-gpu", 66, calls, 66, 50)
     if stock and coal:

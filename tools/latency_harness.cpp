@@ -120,6 +120,20 @@ static long env_long(const char* name, long dflt) {
     const char* e = std::getenv(name);
     return e ? std::atol(e) : dflt;
 }
+// cores this job may use: the affinity mask, capped by the cgroup v2 CPU quota (as bench.py's
+// host_cores: the GPU box gives a 16-CPU quota inside a 256-CPU mask)
+static unsigned host_cores() {
+    cpu_set_t set;
+    unsigned n = sched_getaffinity(0, sizeof set, &set) == 0 ? (unsigned)CPU_COUNT(&set) : 1u;
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long period = 0;
+        if (std::fscanf(f, "%31s %ld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+            n = std::min(n, (unsigned)std::max(1L, (std::atol(q) + period - 1) / period));
+        std::fclose(f);
+    }
+    return std::max(1u, n);
+}
 // this thread's CPU time, nanoseconds
 static int64_t thread_cpu_ns() {
     timespec ts{};
@@ -450,6 +464,10 @@ struct BatchWorker {
 
 struct HookChannel {
     int voters, need, inflight;
+    // delivery threads: 0 = one per voter (quorum-hook: each vote arrives from its own thread);
+    // D > 0 = D threads, thread j delivering votes j, j + D, ... in turn (quorum-pipe: the node's
+    // Go runtime runs its network goroutines on GOMAXPROCS threads, not one OS thread per peer)
+    int deliverers = 0;
     // SBFT_HOOK_ARM=1: the batch workers spin from the release of a decision's votes until its
     // quorum (one core each while collecting) instead of sleeping until a batch is posted; the
     // futex wake of a sleeping worker otherwise lies on every decision's critical path
@@ -467,14 +485,19 @@ struct HookChannel {
     // the collector (the View goroutine) blocks while nothing arrives, as processCommits' select
     // does (view.go:532-549); SBFT_HOOK_COLLECT_SPIN_US bounds its spin first (default 20 us)
     Waker waker;
+    // arrivals that can change the collector's next step: it sleeps until arrived >= wake_at (the
+    // count at which the quorum becomes reachable) or a batch finishes, so only that voter wakes
+    // it (one futex wake per step instead of one per vote; the batches launched are the same)
+    std::atomic<int> wake_at{0};
     std::atomic<int64_t> engine_ns{0};
 
     void start() {
         waker.spin_us = env_long("SBFT_HOOK_COLLECT_SPIN_US", 20);
         order.reset(new std::atomic<int>[voters]);
         for (int i = 0; i < voters; ++i) order[i].store(0);
-        for (int i = 0; i < voters; ++i)
-            th.emplace_back([this, i] {
+        const int nd = deliverers > 0 ? std::min(deliverers, voters) : voters;
+        for (int j = 0; j < nd; ++j)
+            th.emplace_back([this, j, nd] {
                 pthread_setname_np(pthread_self(), "h-voter");
                 int seen = -1;
                 for (;;) {
@@ -487,9 +510,11 @@ struct HookChannel {
                     if (slept) futex(&gen, FUTEX_WAKE_PRIVATE, 2);  // the release is a wake-up tree
                     if (stop_.load()) return;
                     seen = g;
-                    const int k = arrived.fetch_add(1, std::memory_order_acq_rel);
-                    order[k].store(i + 1, std::memory_order_release);
-                    waker.notify();
+                    for (int i = j; i < voters; i += nd) {
+                        const int k = arrived.fetch_add(1, std::memory_order_seq_cst);
+                        order[k].store(i + 1, std::memory_order_release);
+                        if (k + 1 >= wake_at.load(std::memory_order_seq_cst)) waker.notify();
+                    }
                 }
             });
         const char* e = std::getenv("SBFT_HOOK_ARM");
@@ -579,8 +604,17 @@ struct HookChannel {
             }
             if (!progress) {
                 if (a == voters && in_flight == 0 && pending.empty()) break;  // all in, quorum short
-                // nothing to do: sleep until a vote arrives or a batch finishes (select)
-                waker.wait([&] { return arrived.load(std::memory_order_acquire) > consumed || worker_done(); });
+                // nothing to do: sleep until enough votes arrive to make the quorum reachable, or
+                // a batch finishes (the patch's select; view.go:532-549). With both batch slots
+                // busy only a finished batch can change anything.
+                const int short_by = need - valid - in_votes - (int)pending.size();
+                const int want = in_flight < inflight ? consumed + std::max(1, short_by) : INT_MAX;
+                wake_at.store(std::min(want, voters), std::memory_order_seq_cst);
+                waker.wait([&] {
+                    return arrived.load(std::memory_order_seq_cst) >= wake_at.load(std::memory_order_relaxed) ||
+                           worker_done();
+                });
+                wake_at.store(0, std::memory_order_relaxed);
             }
         }
         const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
@@ -592,7 +626,9 @@ struct HookChannel {
                 if (x->st.load(std::memory_order_acquire) == 2) harvest(*x);
                 else waker.wait([&] { return x->st.load(std::memory_order_acquire) != 1; });
             }
-        waker.wait([&] { return arrived.load(std::memory_order_acquire) >= voters; });
+        wake_at.store(voters, std::memory_order_seq_cst);
+        waker.wait([&] { return arrived.load(std::memory_order_seq_cst) >= voters; });
+        wake_at.store(0, std::memory_order_relaxed);
         for (int k = 0; k < voters; ++k)
             while (order[k].load(std::memory_order_acquire) == 0) __builtin_ia32_pause();
         return us;
@@ -839,6 +875,9 @@ static int quorum_vote_cpu(int voters, int need, int decisions, int threads) {
 static int quorum_pipe(int channels, int decisions, bool gpu) {
     const int voters = 67, need = 66;
     channels = std::max(1, channels);
+    // the node's goroutines run on GOMAXPROCS threads: the job's cores, shared by the channels
+    // (SBFT_PIPE_DELIVERERS per channel overrides; 0 = one OS thread per vote, the round-4 harness)
+    const int deliverers = (int)env_long("SBFT_PIPE_DELIVERERS", std::max(1, (int)host_cores() / channels));
     std::vector<std::vector<double>> lat(channels);
     std::atomic<int> wrong{0};
     double wall_s = 0, cpu0 = 0, cpu1 = 0;
@@ -863,6 +902,7 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
             ch.voters = voters;
             ch.need = need;
             ch.inflight = 2;
+            ch.deliverers = deliverers;
             ch.v = vs[c];
             ch.props = &sets[c]->props;
             ch.msgs = &sets[c]->msgs;
@@ -944,9 +984,10 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
             wk.emplace_back(new Waker());
             wk.back()->spin_us = env_long("SBFT_HOOK_COLLECT_SPIN_US", 20);
         }
+        const int nd = deliverers > 0 ? std::min(deliverers, voters) : voters;
         for (int c = 0; c < channels; ++c)
-            for (int i = 0; i < voters; ++i)
-                vth.emplace_back([&, c, i] {
+            for (int j = 0; j < nd; ++j)
+                vth.emplace_back([&, c, j, nd] {
                     pthread_setname_np(pthread_self(), "h-voter");
                     int seen = -1;
                     for (;;) {
@@ -954,13 +995,13 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
                         while ((g = gen[c]->load(std::memory_order_acquire)) == seen && !stop.load())
                             futex(gen[c].get(), FUTEX_WAIT_PRIVATE, seen);
                         if (stop.load()) return;
-                        for (int k = seen + 1; k <= g; ++k) {  // every decision released since
-                            const bool bad = k % 10 == 4 && i == 7;
-                            if (cpu_verify(votes[c][i]) && !bad) {
-                                valid[c][k].fetch_add(1, std::memory_order_acq_rel);
-                                wk[c]->notify();
+                        for (int k = seen + 1; k <= g; ++k)  // every decision released since
+                            for (int i = j; i < voters; i += nd) {  // a goroutine per vote, on nd threads
+                                const bool bad = k % 10 == 4 && i == 7;
+                                if (cpu_verify(votes[c][i]) && !bad &&
+                                    valid[c][k].fetch_add(1, std::memory_order_seq_cst) + 1 == need)
+                                    wk[c]->notify();  // the vote that completes the quorum wakes the View
                             }
-                        }
                         seen = g;
                     }
                 });
@@ -1009,9 +1050,11 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
     std::printf("{\"mode\": \"quorum-pipe\", \"backend\": \"%s\", \"channels\": %d, \"decisions_per_channel\": %d, "
                 "\"decisions_per_s\": %.1f, \"p50_ms\": %.4f, \"p99_ms\": %.4f, \"cpu_ms_per_decision\": %.3f, "
                 "\"engine_call_cpu_ms_per_decision\": %.3f, \"cpu_ms_per_decision_by_thread\": %s, "
+                "\"delivery_threads_per_channel\": %d, "
                 "\"launches_per_decision\": %.2f, \"cgroup_throttled\": %lld, \"wrong_verdicts\": %d}\n",
                 gpu ? "gpu" : "cpu", channels, decisions, nd / wall_s, pct(all, 50) / 1e3, pct(all, 99) / 1e3,
                 (cpu1 - cpu0) / 1e3 / nd, engine_ns.load() / 1e6 / nd, cpu_json(tc1.since(tc0), nd).c_str(),
+                deliverers > 0 ? std::min(deliverers, voters) : voters,
                 gpu ? 1.0 + (double)launches / nd : 0.0, cg1.nr_throttled - cg0.nr_throttled, wrong.load());
     return wrong.load() ? 2 : 0;
 }
