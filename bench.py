@@ -104,7 +104,7 @@ def host_cores() -> dict:
     return {"affinity": aff, "cgroup_quota_cores": quota, "cores_available": used, "cpu": model}
 
 
-def _openssl_rate(tuples: np.ndarray, threads: int, seconds: float):
+def _openssl_rate(tuples: np.ndarray, threads: int, seconds: float, runs: int = 5):
     exe = os.path.join(ROOT, "oracle", "openssl_bench")
     if not os.path.exists(exe):
         return None
@@ -112,12 +112,22 @@ def _openssl_rate(tuples: np.ndarray, threads: int, seconds: float):
         tf.write(tuples.tobytes())
         path = tf.name
     try:
-        out = subprocess.run([exe, path, str(threads), str(seconds)], capture_output=True, text=True, timeout=300)
+        out = subprocess.run([exe, path, str(threads), str(seconds), str(runs)], capture_output=True, text=True,
+                             timeout=300)
         if out.returncode != 0:
             return None
         return json.loads(out.stdout.strip().splitlines()[-1])
     finally:
         os.unlink(path)
+
+
+def _mapped(pattern: str) -> list:
+    """Files of this process's mappings whose path contains `pattern`."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1] for ln in f if pattern in ln and "/" in ln})
+    except OSError:
+        return []
 
 
 def _harness(*args, timeout=600):
@@ -156,15 +166,18 @@ def cpu_baseline(wl, sample: int, threads: int):
             "cpu": hc["cpu"], "cores_available": hc["cores_available"]}
     base = None
     tuples = np.concatenate(f, axis=1)
-    one = _openssl_rate(tuples, 1, 4)
-    allc = _openssl_rate(tuples, threads, 8)
+    # 1 warm-up + 5 timed runs of >= 2 s each, the median reported
+    one = _openssl_rate(tuples, 1, 2.0, 5)
+    allc = _openssl_rate(tuples, threads, 2.0, 5)
     if allc:
         base = {"value": allc["verifies_per_s"], "unit": "verifies/s", "cores": threads,
                 "kind": "port (fallback: OpenSSL 3.0.2 ECDSA_do_verify, ecp_nistz256 assembly; not Go, "
                         "which is absent here)",
-                "sample": f"first {sample} tuples of the bench workload, cycled for {allc['seconds']:.1f} s "
-                          f"on {threads} threads",
+                "sample": f"first {sample} tuples of the bench workload, cycled: 1 warm-up + "
+                          f"{allc.get('runs', 1)} timed runs of >= 2 s on {threads} threads, median "
+                          f"(runs: {allc.get('runs_per_s')})",
                 "single_core": one["verifies_per_s"] if one else None,
+                "single_core_runs": one.get("runs_per_s") if one else None,
                 "cpu": hc["cpu"], "cores_available": hc["cores_available"], "host": hc}
     return base, port, ok_cpu
 
@@ -712,6 +725,11 @@ def main():
                 "peak_T": VALU_ISSUE_PEAK_T, "frac": round(instr_per_verify * n / avg_kern_s / 1e12 / VALU_ISSUE_PEAK_T, 3)},
             "parity": {"full_size_mismatches": mismatches,
                        "expected_accepts": sum(int((~w.corrupted).sum()) for w in wls) * world},
+            # the HIP runtime this process's engine ran on: torch (imported first for device
+            # memory) brings its own libamdhip64 with the engine's SONAME, so here the engine
+            # binds to torch's copy; a deployment (cgo) loads /opt/rocm's. The parity suite on
+            # the shipped runtime is tests/test_gpu_runtime.py (a torch-free child process).
+            "hip_runtime": _mapped("libamdhip64"),
         }
         if rehearsal:
             # the K slots' launches run concurrently, so a launch's own duration says nothing

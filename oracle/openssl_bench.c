@@ -3,7 +3,9 @@
  * ECDSA_do_verify (P-256, ecp_nistz256 assembly), one pthread per core over an
  * atomic index; keys and signatures pre-built outside the timed region.
  * Labelled "fallback: OpenSSL, not Go" (BASELINE.md 2): Go is absent on the box.
- * Usage: openssl_bench <tuples.bin> <nthreads> <min_seconds>
+ * Usage: openssl_bench <tuples.bin> <nthreads> <min_seconds> [runs]
+ * SURVEY.md 8(d)'s method: one untimed warm-up run, then `runs` (default 1) timed runs of at
+ * least min_seconds each; verifies_per_s is the median run, runs_per_s every run.
  * Prints one JSON object: {"verifies_per_s":..., "threads":..., "n":..., "accepted":...}
  */
 #include <openssl/bn.h>
@@ -25,10 +27,13 @@ static atomic_size_t next_idx;
 static atomic_size_t accepted;
 static size_t total_target;
 
+static atomic_int stop_flag;  /* timed runs: the workers stop at the deadline */
+
 static void* worker(void* arg) {
     (void)arg;
     size_t acc = 0;
     for (;;) {
+        if (atomic_load_explicit(&stop_flag, memory_order_relaxed)) break;
         size_t i = atomic_fetch_add(&next_idx, 1);
         if (i >= total_target) break;
         size_t j = i % n;
@@ -77,15 +82,46 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < probe; ++i)
         if (keys[i]) ECDSA_do_verify(recs + 160 * i, 32, sigs[i], keys[i]);
     double per = (now() - t0) / (double)probe;
-    total_target = (size_t)(min_s / per * nt);
-    if (total_target < n) total_target = n;
+    (void)per;
+    const int runs = argc > 4 ? atoi(argv[4]) : 1;
     pthread_t* th = malloc(sizeof(pthread_t) * nt);
-    atomic_store(&next_idx, 0);
-    t0 = now();
-    for (int t = 0; t < nt; ++t) pthread_create(&th[t], NULL, worker, NULL);
-    for (int t = 0; t < nt; ++t) pthread_join(th[t], NULL);
-    double dt = now() - t0;
-    printf("{\"verifies_per_s\": %.1f, \"threads\": %d, \"n\": %zu, \"accepted\": %zu, \"seconds\": %.3f}\n",
-           total_target / dt, nt, total_target, (size_t)atomic_load(&accepted), dt);
+    double rates[64];
+    double secs = 0;
+    int done = 0;
+    size_t count = 0;
+    for (int r = -1; r < runs && r < 63; ++r) {  /* r = -1: the untimed warm-up run */
+        atomic_store(&next_idx, 0);
+        atomic_store(&accepted, 0);
+        atomic_store(&stop_flag, 0);
+        total_target = (size_t)-1;  /* every run lasts min_s: the workers stop at the deadline */
+        t0 = now();
+        for (int t = 0; t < nt; ++t) pthread_create(&th[t], NULL, worker, NULL);
+        const struct timespec nap = {(time_t)min_s, (long)((min_s - (double)(time_t)min_s) * 1e9)};
+        nanosleep(&nap, NULL);
+        atomic_store(&stop_flag, 1);
+        for (int t = 0; t < nt; ++t) pthread_join(th[t], NULL);
+        const double dt = now() - t0;
+        /* a worker takes an index only before the deadline and verifies every index it took */
+        const size_t taken = atomic_load(&next_idx);
+        count = taken;
+        if (r < 0) continue;
+        rates[done++] = (double)count / dt;
+        secs = dt;
+    }
+    total_target = count;
+    double sorted[64];
+    memcpy(sorted, rates, sizeof(double) * done);
+    for (int i = 1; i < done; ++i)
+        for (int j = i; j > 0 && sorted[j] < sorted[j - 1]; --j) {
+            const double x = sorted[j];
+            sorted[j] = sorted[j - 1];
+            sorted[j - 1] = x;
+        }
+    const double med = done % 2 ? sorted[done / 2] : 0.5 * (sorted[done / 2 - 1] + sorted[done / 2]);
+    printf("{\"verifies_per_s\": %.1f, \"threads\": %d, \"n\": %zu, \"accepted\": %zu, \"seconds\": %.3f, "
+           "\"runs\": %d, \"runs_per_s\": [",
+           med, nt, total_target, (size_t)atomic_load(&accepted), secs, done);
+    for (int i = 0; i < done; ++i) printf("%s%.1f", i ? ", " : "", rates[i]);
+    printf("]}\n");
     return 0;
 }

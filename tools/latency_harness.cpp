@@ -813,6 +813,8 @@ static int quorum_vote_cpu(int voters, int need, int decisions, int threads) {
     std::atomic<int> gen{-1};
     std::atomic<bool> stop{false};
     std::vector<std::thread> th;
+    Waker wk;  // the View blocks until the quorum (or the last vote) is in, as the GPU collector
+    wk.spin_us = env_long("SBFT_HOOK_COLLECT_SPIN_US", 20);
     for (int j = 0; j < nt; ++j)
         th.emplace_back([&, j] {
             int seen = -1;
@@ -828,8 +830,9 @@ static int quorum_vote_cpu(int voters, int need, int decisions, int threads) {
                 for (int k = seen + 1; k <= g; ++k)
                     for (int i = j; i < voters; i += nt) {
                         const bool bad = k % 10 == 4 && i == 7;  // decisions 9, 19, ... after warm-up
-                        if (cpu_verify(votes[i]) && !bad) valid[k].fetch_add(1, std::memory_order_acq_rel);
-                        done[k].fetch_add(1, std::memory_order_acq_rel);
+                        const bool last_valid = cpu_verify(votes[i]) && !bad &&
+                                                valid[k].fetch_add(1, std::memory_order_seq_cst) + 1 == need;
+                        if (done[k].fetch_add(1, std::memory_order_seq_cst) + 1 == voters || last_valid) wk.notify();
                     }
                 seen = g;
             }
@@ -840,14 +843,14 @@ static int quorum_vote_cpu(int voters, int need, int decisions, int threads) {
         const auto t0 = Clock::now();
         gen.store(g, std::memory_order_release);
         futex(&gen, FUTEX_WAKE_PRIVATE, 2);
-        while (valid[g].load(std::memory_order_acquire) < need) {
-            if (done[g].load(std::memory_order_acquire) == voters) break;  // all in, quorum short
-            __builtin_ia32_pause();
-        }
+        // all in with the quorum short ends it too
+        wk.wait([&] {
+            return valid[g].load(std::memory_order_seq_cst) >= need || done[g].load(std::memory_order_seq_cst) == voters;
+        });
         const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
         if (g >= 5) t.push_back(us);
         // drain the spare vote (outside the latency), as quorum-hook does
-        while (done[g].load(std::memory_order_acquire) < voters) __builtin_ia32_pause();
+        wk.wait([&] { return done[g].load(std::memory_order_seq_cst) == voters; });
         if (valid[g].load() < need) wrong++;
     }
     stop.store(true);
