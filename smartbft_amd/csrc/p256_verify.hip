@@ -1697,24 +1697,10 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         comb_add_u1g(g, c, neg1, gcomb, [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
                      [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
         probe("helper_comb", lane == 0);
-        // x = r is on the curve iff r^3 - 3r + b is a square (the verify wavefronts' pair B ran on
-        // E_c without knowing): y = (.)^((p+1)/4), y^2 == r^3 - 3r + b
-        bool has_r0;
-        {
-            f29 rm, t2, t3, rhs, y0, yy, d;
-            const f29 b = f29_const(C29_B);
-            f29_mul_ilp(rm, f29_from_u256(r), f29_const(C29_R2));
-            f29_sqr_ilp(t2, rm);
-            f29_mul_ilp(t3, t2, rm);
-#pragma unroll
-            for (int i = 0; i < 9; ++i) rhs.v[i] = t3.v[i] - 3u * rm.v[i] + b.v[i];  // |limb| < 2^31
-            f29_normalize(rhs, rhs);                                                  // N'
-            f29_sqrt_chain(y0, rhs);
-            f29_sqr_ilp(yy, y0);
-            f29_sub(d, yy, rhs);  // |limb| < 2^30, |.| < 2^259
-            has_r0 = f29_zero_mod_p_any(d);
-        }
-        probe("helper_square", lane == 0);
+        // No square test here (round 5): whether x = r is on the curve at all (r^3 - 3r + b a
+        // square) is decided by the comparison itself; only an irregular end of the ladders
+        // (Z_T or W_V = 0, never for an honest tuple) needs it, and the verify wavefronts compute
+        // it for that case (the irregular branch of the final comparison)
         if (mine) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
@@ -1722,10 +1708,10 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                 gsum[(9 + k) * T + lane] = g.y.v[k];
                 gsum[(18 + k) * T + lane] = g.z.v[k];
             }
-            gsum[27 * T + lane] = (ginf ? 1u : 0u) | (has_r0 ? 2u : 0u);
+            gsum[27 * T + lane] = ginf ? 1u : 0u;
         }
         __syncthreads();  // #2: hand-over to the verify wavefronts
-        probe_dump("helper sinv,hgcd,published,barrier1,hash,comb,square", lane == 0);
+        probe_dump("helper sinv,hgcd,published,barrier1,hash,comb", lane == 0);
         return;
     }
 
@@ -1911,7 +1897,6 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     __syncthreads();  // #2: the helper's (v u1) G and the square test are in gsum
     probe("verify_barrier2", tid == 0);
     const u32 gflags = gsum[27 * T + pr];
-    const bool has_r0 = (gflags & 2u) != 0;  // x = r is on the curve
     {
         jp29 g;
 #pragma unroll
@@ -1935,16 +1920,40 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             inf = (hz && !twice) || (inf && ginf);
         }
     }
-    // T = acc (pair A), V on E_c: x(V) = X_V / W_V. Accept iff T != infinity and X_T W_V == X_V Z_T^2
-    bool accept, exc;
+    // T = acc (pair A), V on E_c: x(V) = X_V / W_V. Accept iff T != infinity and X_T W_V == X_V Z_T^2.
+    // No square test is needed for a regular end (Z_T, W_V != 0): if c = r^3 - 3r + b is not a
+    // square, E_c is the quadratic twist, and x(V) = X_V / W_V has f(x) = x^3 - 3x + b = (Y_V / c)^2
+    // / c a non-square (f has no root: the curve has no point of order 2), so it is the x of no
+    // point of the curve, T's included, and the comparison fails -- as Go's x(R) = r must, since
+    // no point has x = r. (A twist point of small order, which could end V at infinity, is out of
+    // reach: the twist order is 3 5 13 179 times a 241-bit prime, and P' is fixed by r.)
+    bool accept, exc = false;
     {
         f29 zt2, lhs, rhs2, d;
         f29_sqr(zt2, acc.z);
         f29_mul(lhs, acc.x, VW);
         f29_mul(rhs2, VX, zt2);
         f29_sub(d, lhs, rhs2);  // |limb| < 2^29.2, |.| < 2^257
-        accept = has_r0 && f29_zero_mod_p_any(d);
-        exc = has_r0 && (f29_zero_mod_p(acc.z) || f29_zero_mod_p(VW));  // never expected: fixup net
+        const bool irregular = f29_zero_mod_p(acc.z) || f29_zero_mod_p(VW);
+        accept = !irregular && f29_zero_mod_p_any(d);
+        // never for a valid honest tuple; an invalid one (rejected whatever its pairs computed)
+        // must not send its wavefront down this path
+        if (__builtin_expect(__any(irregular && !inf && valid && !fb), 0)) {
+            // the fixup net takes it if x = r is on the curve (then it is truly exceptional);
+            // otherwise it is a rejection. r^3 - 3r + b a square: y = (.)^((p+1)/4), y^2 == it
+            f29 rmm, t2, t3, cv, y0, yy, dd;
+            const f29 b = f29_const(C29_B);
+            f29_mul_ilp(rmm, f29_from_u256(r), f29_const(C29_R2));
+            f29_sqr_ilp(t2, rmm);
+            f29_mul_ilp(t3, t2, rmm);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) cv.v[i] = t3.v[i] - 3u * rmm.v[i] + b.v[i];  // |limb| < 2^31
+            f29_normalize(cv, cv);                                                    // N'
+            f29_sqrt_chain(y0, cv);
+            f29_sqr_ilp(yy, y0);
+            f29_sub(dd, yy, cv);  // |limb| < 2^30, |.| < 2^259
+            exc = irregular && f29_zero_mod_p_any(dd);  // fixup net
+        }
     }
     if (__builtin_expect(__any(fb), 0)) {
         bool exc_f;

@@ -430,6 +430,68 @@ def test_w_ladder_on_the_isomorphic_curve(seed):
             assert plain(X) * pow(plain(W), -1, P) % P == ref[0], step
 
 
+def _ec_add(A, p1, p2):
+    """Affine addition on y^2 = x^3 + A x + B' (None = infinity); B' never enters the formulas."""
+    if p1 is None:
+        return p2
+    if p2 is None:
+        return p1
+    (x1, y1), (x2, y2) = p1, p2
+    if x1 == x2 and (y1 + y2) % P == 0:
+        return None
+    if p1 == p2:
+        lam = (3 * x1 * x1 + A) * pow(2 * y1, -1, P) % P
+    else:
+        lam = (y2 - y1) * pow(x2 - x1, -1, P) % P
+    x3 = (lam * lam - x1 - x2) % P
+    return x3, (lam * (x1 - x3) - y1) % P
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_w_ladder_on_the_twist_never_matches(seed):
+    """Why the half kernel needs no square test (round 5): when c = r^3 - 3r + b is NOT a square,
+    pair B's ladder runs on E_c, now the quadratic twist, from P' = (c r, c^2), and the x it ends
+    with, X / W = x(V) / c, has f(x) = x^3 - 3x + b a non-square at every step -- the x of no point
+    of the curve, so the final comparison with T (a curve point) fails, as Go's x(R) = r does when
+    no point has x = r. Same kernel model (dbl_w / add_aff_w, limb contracts, W = c Z^2), with the
+    reference ladder on E_c itself."""
+    rng = random.Random(seed)
+    done = 0
+    while done < 2:
+        r = rng.randrange(1, P)
+        c = (r ** 3 - 3 * r + pyref.B) % P
+        if pow(c, (P - 1) // 2, P) != P - 1:
+            continue  # c a square: covered by test_w_ladder_on_the_isomorphic_curve
+        done += 1
+        A = (-3 * c * c) % P  # E_c: y^2 = x^3 - 3 c^2 x + b c^3
+        base = (c * r % P, c * c % P)
+        assert (base[1] ** 2 - base[0] ** 3 - A * base[0] - pyref.B * c ** 3) % P == 0
+        X, Y = mont_of(base[0]), mont_of(base[1])
+        Z, W = mont_of(1), mont_of(c)
+        ref = base
+        for step in range(80):
+            X = relimb(X, rng, -(1 << 26) + 1, (1 << 29) + (1 << 26), 0, 1 << 24)   # N'
+            W = relimb(W, rng, 0, 1 << 29)                                           # N
+            if step % 5 == 4:
+                q = base
+                for _ in range(rng.randrange(1, 8)):
+                    q = _ec_add(A, q, base)
+                x2, y2 = mont_of(q[0] * pow(c, -1, P) % P), mont_of(q[1] * pow(c, -1, P) % P)  # entry / c
+                X, Y, Z, W = add_aff_w(X, Y, Z, W, x2, y2)
+                ref = _ec_add(A, ref, q)
+                Y = relimb(Y, rng, -(1 << 29) + 1, 1 << 29)  # N+-
+            else:
+                Y = relimb(Y, rng, -(1 << 26) + 1, (1 << 29) + (1 << 26), 0, 1 << 24)   # N'
+                X, Y, Z, W = dbl_w(X, Y, Z, W)
+                ref = _ec_add(A, ref, ref)
+            z = plain(Z)
+            assert plain(W) == c * z * z % P, step
+            xv = plain(X) * pow(plain(W), -1, P) % P
+            assert xv == ref[0] * pow(c, -1, P) % P, step
+            fx = (xv ** 3 - 3 * xv + pyref.B) % P
+            assert pow(fx, (P - 1) // 2, P) == P - 1, step  # the x of no curve point
+
+
 def test_w_extreme_operands():
     top = (1 << 29) + (1 << 26) - 1
     Np_max = [top] * 8 + [(1 << 24) - 1]
