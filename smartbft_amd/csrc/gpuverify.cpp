@@ -2043,7 +2043,10 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
         c.out_off = in_bytes;
         return SBFT_GV_OK;
     }
-    HIPCHK(hipEventRecord(zl->done, st));
+    if (hipEventRecord(zl->done, st) != hipSuccess) {
+        (void)hipStreamSynchronize(st);  // the kernel still writes into the lane's buffer: drain it
+        return SBFT_GV_EDEVICE;
+    }
     const auto t2 = std::chrono::steady_clock::now();
     auto t3 = t2;
     size_t seen = 0;
