@@ -931,8 +931,7 @@ SBFT_DEV void add_aff_fix(jp29& acc, bool& inf, Dbl dbl, Reload reload) {
 #define SBFT_ILP_LA 4
 #endif
 template <bool SQ>
-SBFT_DEV i64 f29_column(int k, const f29& a, const f29& b, const u32 (&d)[9]) {
-    i64 c = 0;
+SBFT_DEV i64 f29_column(int k, const f29& a, const f29& b, const u32 (&d)[9], i64 c = 0) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
         const int j = k - i;
@@ -995,6 +994,36 @@ template <bool SQ, int NA>
 SBFT_DEV void f29_mulsq_add_ilp(f29& r, const f29& a, const f29& b, const f29* const (&v)[NA], const u32 (&c)[NA],
                                 u32 hmask) {
     f29_mulsq_core<SQ, NA>(r, a, b, v, c, hmask);
+}
+// f29_mul_sub in the pipelined ILP form: Mont(a b + c nd) with nd = -d supplied by the caller
+// (a lane that wants a plain product passes nd = 0). Each column is one mad chain over both
+// products (the look-ahead columns fill its wait states), then the reduction terms and the carry
+// as in f29_mulsq_core. f29_mul_sub's contract; output N.
+SBFT_DEV void f29_mul_sub_ilp(f29& r, const f29& a, const f29& b, const f29& c, const f29& nd) {
+    const f29_red K = f29_red_consts();
+    const u32 unused[9] = {};
+    i64 col[17];
+    constexpr int LA = SBFT_ILP_LA > 0 ? SBFT_ILP_LA : 17;
+#pragma unroll
+    for (int k = 0; k < LA && k < 17; ++k)
+        col[k] = f29_column<false>(k, c, nd, unused, f29_column<false>(k, a, b, unused));
+    u32 m[9];
+    i64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+        if (k + LA < 17)
+            col[k + LA] = f29_column<false>(k + LA, c, nd, unused, f29_column<false>(k + LA, a, b, unused));
+        i64 x = col[k];
+        if (k >= 3 && k - 3 <= 8) x = smad(m[k - 3], K.c9, x);
+        if (k >= 6 && k - 6 <= 8) x = smad(m[k - 6], K.c18, x);
+        if (k >= 7 && k - 7 <= 8) x = smad(m[k - 7], K.c7, x);
+        if (k >= 8 && k - 8 <= 8) x = smad(m[k - 8], K.c8, x);
+        acc = k == 0 ? x : x + acc;
+        if (k < 9) m[k] = lo29(acc);
+        else r.v[k - 9] = lo29(acc);
+        acc = sar29(acc);
+    }
+    r.v[8] = (u32)acc;
 }
 SBFT_DEV void f29_mul_ilp(f29& r, const f29& a, const f29& b) { f29_mulsq_ilp<false>(r, a, b); }
 SBFT_DEV void f29_sqr_ilp(f29& r, const f29& a) { f29_mulsq_ilp<true>(r, a, a); }
@@ -1346,7 +1375,51 @@ SBFT_DEV void p29_dbl_plw(plw29& P) {
 //   4: Z3 = Z1 H | X3 = r^2 - HHH - 2V   5: Y1 HHH | r (V - X3)   6: W3 = W HH (both lanes)
 // (x2'', y2'') = the entry divided by c, in both lanes (N, y2'' N+- when negated). Out: X3 in
 // N', Y3 in N+-, Z3, W3 in N.
+#ifndef SBFT_ADD_PLW5
+#define SBFT_ADD_PLW5 1
+#endif
+// Five paired steps instead of six: W3 = W HH moves onto the even lane of the last step, whose
+// odd lane computes Y3 = r (V - X3) - Y1 HHH in one f29_mul_sub_ilp (the even lane's second
+// product is c 0). One reduction, the Y1 swap, the result swap and the Y3 subtraction fewer.
+//   1: U2 = x2'' W | T = Z1 W   2: HH = H^2 | S2 = y2'' T   3: V = X1 HH | HHH
+//   4: Z3 = Z1 H | X3 = r^2 - HHH - 2V   5: W3 = W HH | Y3 = r (V - X3) - Y1 HHH
+// Out: X3 in N', Y3, Z3, W3 in N.
+SBFT_DEV void p29_add_aff_plw5(plw29& P, const f29& x2, const f29& y2) {
+    const u32 om = sel_pair(0u, ~0u);
+    f29 o1, s1, h, o2, s2, hh, o3, s3, r, o4, a, b, nd, o5;
+    f29_mul_ilp(o1, f29_sel_pair(x2, P.zo), P.w);             // U2 | T
+    s1 = f29_swap_pair(o1);                                   // T | U2
+#pragma unroll
+    for (int i = 0; i < 9; ++i) h.v[i] = sel_pair(o1.v[i], s1.v[i]) - P.xb.v[i];  // H: (-2^29.2, 2^29 + 2^25)
+    f29_mul_ilp(o2, f29_sel_pair(h, y2), f29_sel_pair(h, o1)); // HH | S2
+    s2 = f29_swap_pair(o2);                                   // S2 | HH
+    hh = f29_sel_pair(o2, s2);                                // HH in both lanes
+    f29_mul_ilp(o3, f29_sel_pair(P.xb, h), hh);               // V | HHH
+    s3 = f29_swap_pair(o3);                                   // HHH | V
+    f29_sub(r, o2, P.zy);                                     // r = S2 - Y1 (odd lane): |.| < 2^29.2
+    {
+        const f29* const v[2] = {&o3, &s3};
+        const u32 c[2] = {sel_pair(0u, (u32)-1), sel_pair(0u, (u32)-2)};
+        f29_mulsq_add_ilp<false, 2>(o4, f29_sel_pair(P.zy, r), f29_sel_pair(h, r), v, c,
+                                    sel_pair(0u, ~0u));       // Z3 = Z1 H: N | X3 = r^2 - HHH - 2V: N'
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        a.v[i] = sel_pair(P.w.v[i], r.v[i]);                  // W | r
+        b.v[i] = sel_pair(hh.v[i], s3.v[i] - o4.v[i]);        // HH | V - X3: (-2^29.2, 2^29 + 2^25)
+        nd.v[i] = (0u - o3.v[i]) & om;                        // 0 | -HHH
+    }
+    f29_mul_sub_ilp(o5, a, b, P.zy, nd);                      // W3 | Y3 = r (V - X3) - Y1 HHH: N
+    P.xb = f29_bcast_pair(o4, true);                          // X3 in both lanes
+    P.zy = f29_sel_pair(o4, o5);                              // Z3 | Y3
+    P.zo = f29_swap_pair(o4);                                 // Z3 (odd lane)
+    P.w = f29_bcast_pair(o5, false);                          // W3 in both lanes
+}
 SBFT_DEV void p29_add_aff_plw(plw29& P, const f29& x2, const f29& y2) {
+    if (SBFT_ADD_PLW5) {
+        p29_add_aff_plw5(P, x2, y2);
+        return;
+    }
     f29 o1, s1, h, o2, s2, hh, o3, s3, r, o4, szy, a, b, o5, s5, s4, o6;
     f29_mul_ilp(o1, f29_sel_pair(x2, P.zo), P.w);             // U2 | T
     s1 = f29_swap_pair(o1);                                   // T | U2

@@ -312,9 +312,9 @@ def dbl_w(X, Y, Z, W):
 
 
 def add_aff_w(X, Y, Z, W, x2, y2):
-    """p29_add_aff_plw: the mixed addition with W = c Z1^2 for the table entries (x/c, y/c):
+    """p29_add_aff_plw5: the mixed addition with W = c Z1^2 for the table entries (x/c, y/c):
       U2 = x2 W | T = Z1 W;  HH = H^2 | S2 = y2 T;  V = X1 HH | HHH;  Z3 = Z1 H | X3 = r^2 - HHH - 2V;
-      Y1 HHH | r (V - X3);  W3 = W HH."""
+      W3 = W HH | Y3 = r (V - X3) - Y1 HHH (f29_mul_sub_ilp; the even lane's second product is Z1 0)."""
     u2 = mont(x2, W)
     T = mont(Z, W)
     h = sub(u2, X)
@@ -326,11 +326,9 @@ def add_aff_w(X, Y, Z, W, x2, y2):
     Z3 = mont(Z, h, addends=[(hhh, 0), (V, 0)])
     X3 = mont(rr, rr, addends=[(hhh, -1), (V, -2)], fold=True)
     t = sub(V, X3)
-    a = mont(Y, hhh)
-    b = mont(rr, t)
-    Y3 = sub(b, a)
-    W3 = mont(W, hh)
-    for v in (u2, T, hh, s2, V, hhh, Z3, a, b, W3):
+    Y3 = mul_sub(rr, t, Y, hhh)
+    W3 = mul_sub(W, hh, Z, [0] * 9)
+    for v in (u2, T, hh, s2, V, hhh, Z3, Y3, W3):
         check_N(v)
     check_Np(X3)
     return X3, Y3, Z3, W3
