@@ -377,6 +377,58 @@ __device__ __forceinline__ void inv_mod_wave(uint32_t out[8], const uint32_t x[8
     add_kn(d, 0, P);
     reduce_unpack(out, d, P);
 }
+
+// inv_mod on a lane pair (2t, 2t + 1) that holds the same x (the half kernel's table build: both
+// lanes of a ladder pair invert the same z c). The even lane keeps (f, g), the odd lane (d, e),
+// and each batch updates both with ONE update_de per lane: on (f, g) the low 30 bits of T (f, g)
+// are zero, so the correction multiple update_de computes there is 0 and the update is
+// update_fg's exact division. The divsteps run on both lanes from the even lane's low words (two
+// DPP moves per batch, as the g == 0 test). Per batch one 9-limb update instead of two; the
+// batches, divsteps and result are inv_mod's (c = 1). A pair's two lanes leave the loop together.
+__device__ __forceinline__ int32_t pair_even(int32_t x) {  // the even lane's x, in both lanes
+    return __builtin_amdgcn_mov_dpp(x, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
+}
+__device__ __forceinline__ void inv_mod_pair(uint32_t out[8], const uint32_t x[8], const uint32_t* tab, bool P,
+                                             bool odd) {
+    int32_t M[9];
+    mod30(M, P);
+    s30 xs, a, b;  // even lane: a = f, b = g; odd lane: a = d, b = e
+    pack30(xs, x);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        a.v[i] = odd ? 0 : M[i];
+        b.v[i] = odd ? (i == 0 ? 1 : 0) : xs.v[i];
+    }
+    int32_t u, v, q, r;
+    int32_t delta = divsteps30(1, (uint32_t)M[0], (uint32_t)xs.v[0], tab, u, v, q, r);
+    SBFT_UNROLL1
+    for (int batch = 0; batch < 26; ++batch) {
+        if (pair_even(is_zero30(b) ? 1 : 0)) break;  // g == 0
+        // the next batch's divsteps from the low limb of T (f, g) / 2^30 (the even lane's)
+        const int64_t lf = (mac(mac(0, u, a.v[0]), v, b.v[0]) >> 30) + (int64_t)u * a.v[1] + (int64_t)v * b.v[1];
+        const int64_t lg = (mac(mac(0, q, a.v[0]), r, b.v[0]) >> 30) + (int64_t)q * a.v[1] + (int64_t)r * b.v[1];
+        const uint32_t lf0 = (uint32_t)pair_even((int32_t)((uint32_t)lf & SBFT_M30));
+        const uint32_t lg0 = (uint32_t)pair_even((int32_t)((uint32_t)lg & SBFT_M30));
+        int32_t u2, v2, q2, r2;
+        const int32_t delta2 = divsteps30(delta, lf0, lg0, tab, u2, v2, q2, r2);
+        update_de(a, b, u, v, q, r, P);
+        delta = delta2;
+        u = u2;
+        v = v2;
+        q = q2;
+        r = r2;
+    }
+    // f = +-1 (the even lane's a): x^-1 = f d, on the odd lane
+    if (pair_even(a.v[8] < 0 ? 1 : 0)) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) a.v[i] = -a.v[i];
+        add_kn(a, 0, P);
+    }
+    uint32_t o[8];
+    reduce_unpack(o, a, P);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int32_t)o[i], 0xF5, 0xF, 0xF, false);
+}
 #endif
 
 #if defined(__HIPCC__)

@@ -1495,6 +1495,9 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
 #define SBFT_HALF_TUPLES 48
 #endif
 constexpr int kHalfTuples = SBFT_HALF_TUPLES;  // per workgroup
+#ifndef SBFT_HALF_INV_PAIR
+#define SBFT_HALF_INV_PAIR 1  // the table's inversion split over the pair (inv::inv_mod_pair)
+#endif
 static_assert(kHalfTuples % 16 == 0 && kHalfTuples <= 64, "16 quads per verify wavefront, one helper wavefront");
 constexpr int kHalfVerifyThreads = 4 * kHalfTuples;
 constexpr int kHalfThreads = kHalfVerifyThreads + 64;
@@ -1770,9 +1773,10 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         };
         build_q_table_pair_w(
             px, py, ac, cc, odd,
-            [&](const fe& zp) {
+            [&](const fe& zp) {  // both lanes of the pair hold the same z c
                 fe zi;
-                inv::inv_mod(zi.v, zp.v, dtab, true);
+                if (SBFT_HALF_INV_PAIR) inv::inv_mod_pair(zi.v, zp.v, dtab, true, odd);
+                else inv::inv_mod(zi.v, zp.v, dtab, true);
                 return zi;
             },
             [&](int m) { probe(m ? "verify_inverse" : "verify_chain", tid == 0); }, st, ld,
