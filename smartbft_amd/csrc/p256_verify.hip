@@ -811,6 +811,9 @@ SBFT_DEV void build_q_table_pair_w(const f29& qxm, const f29& qym, const f29& ac
         pmul(X, Y, X, l2k, yl, l2k);
         st(k, X, Y);
         lam = nxt;  // 1 / Z(T_{k-1})
+#ifdef SBFT_HALF_PROBE_TAB  // development: marks after the first and the fourth conversion
+        if (k == kQTab - 1 || k == kQTab - 4) mark(2);
+#endif
     }
     f29 x0, y0;
     pmul(x0, y0, qxm, kap, qym, kap);  // the base itself, divided by c
@@ -1556,20 +1559,29 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     inv::stage_divstep_table(dtab);  // ends with a barrier
 #ifdef SBFT_HALF_PROBE  // development: phase times of workgroup 0 (tools/half_probe.py), 100 MHz ticks,
                         // kept in registers and printed once at the end (a printf is a blocking host call)
-    const uint64_t probe_t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t probe_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // (and the shader-clock counter beside it: the clock of a phase is its s_memtime ticks over its
+    // real-time ticks times 100 MHz)
+    const uint64_t probe_t0 = __builtin_amdgcn_s_memrealtime(), probe_c0 = __builtin_amdgcn_s_memtime();
+    uint32_t probe_t[8] = {0, 0, 0, 0, 0, 0, 0, 0}, probe_c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int probe_n = 0;
     auto probe = [&](const char*, bool) {
         const uint32_t t = (uint32_t)(__builtin_amdgcn_s_memrealtime() - probe_t0);
+        const uint32_t c = (uint32_t)(__builtin_amdgcn_s_memtime() - probe_c0);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-            if (i == probe_n) probe_t[i] = t;
+            if (i == probe_n) {
+                probe_t[i] = t;
+                probe_c[i] = c;
+            }
         ++probe_n;
     };
     auto probe_dump = [&](const char* who, bool me) {
-        if (me && blockIdx.x == 0)
+        if (me && blockIdx.x == 0) {
             printf("half-probe %s %u %u %u %u %u %u %u %u\n", who, probe_t[0], probe_t[1], probe_t[2], probe_t[3],
                    probe_t[4], probe_t[5], probe_t[6], probe_t[7]);
+            printf("half-probe-clk %s %u %u %u %u %u %u %u %u\n", who, probe_c[0], probe_c[1], probe_c[2], probe_c[3],
+                   probe_c[4], probe_c[5], probe_c[6], probe_c[7]);
+        }
     };
 #else
     auto probe = [](const char*, bool) {};
@@ -1972,7 +1984,9 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         exc = false;
     }
     probe("verify_final", tid == 0);
-    probe_dump("verify inputs,chain,inverse,tables,barrier1,ladder,barrier2,final", tid == 0);
+    probe_dump(tid == 0 ? "verify inputs,chain,inverse,tables,barrier1,ladder,barrier2,final"
+                        : (tid == 64 ? "verify-w1" : "verify-w2"),
+               tid == 0 || tid == 64 || tid == 128);
     if (active && (tid & 3) == 0) {
         if (exc && valid) {
             if constexpr (FRAMED) {  // the fixup kernel's inputs
