@@ -1524,6 +1524,30 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     const auto t1 = TC::now();
     const int prc = prepare(off, len);
     const auto t2 = TC::now();
+    // While the helper still stages the payload copy (it ends ~20 us after the parse): check the
+    // parsed offsets and put them into the mapped host memory the launches below read -- all
+    // that needs only the parse (~7 us of a 10k-request call). Errors are returned after the
+    // helper has finished (its job holds references to this frame).
+    const size_t n = off.size();
+    const bool split = n >= ctx->min_split && ctx->slots.size() > 1;
+    const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256);
+    int src = SBFT_GV_OK;
+    if (!prc && n > 0 && !split) {
+        if (len.size() != n || n > 0xffffffffu) src = SBFT_GV_EINVAL;
+        for (size_t k = 0; !src && k < n; ++k) {
+            if (off[k] + len[k] > blob_len || off[k] + len[k] < off[k]) src = SBFT_GV_EINVAL;
+            const int64_t end = (int64_t)(off[k] + len[k]);
+            for (int32_t rel : {sig_rel, pub_rel})
+                if (end + rel < 0 || (uint64_t)(end + rel) + 64 > blob_len) src = SBFT_GV_EINVAL;
+        }
+        // room for both layouts: offsets | lengths | key ids | verdicts (registered) and
+        // offsets | lengths | verdicts | fix-up flag (generic)
+        if (!src) src = sl->reserve_vmap(fo + 2 * fl + align_up(n, 256) + 256);
+        if (!src) {
+            std::memcpy(sl->vmap, off.data(), 8 * n);
+            std::memcpy(sl->vmap + fo, len.data(), 4 * n);
+        }
+    }
     if (async) ctx->helper.wait();
     // No stream synchronisation here: the launches below queue behind the payload copy on the
     // same stream, so the verify starts as the DMA ends instead of one host round trip later
@@ -1550,22 +1574,23 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     } drain{sl->stream, true};
     struct Tr {
         bool on;
-        TC::time_point a, b, c, d;
+        TC::time_point a, b, c, d, e, f;  // e: offsets staged, f: launch returned (fused path)
         bool async;
         ~Tr() {
             if (!on) return;
             auto us = [](TC::time_point x, TC::time_point y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
-            fprintf(stderr, "vp async=%d submit=%.1f parse=%.1f copy_wait_sync=%.1f rest=%.1f us\n", (int)async, us(a, b),
-                    us(b, c), us(c, d), us(d, TC::now()));
+            const TC::time_point z = TC::now();
+            if (f == TC::time_point{}) e = f = d;
+            fprintf(stderr, "vp async=%d submit=%.1f parse=%.1f copy_wait_sync=%.1f stage=%.1f launch=%.1f rest=%.1f us\n",
+                    (int)async, us(a, b), us(b, c), us(c, d), us(d, e), us(e, f), us(f, z));
         }
-    } tr{trace, t0, t1, t2, t3, async};
+    } tr{trace, t0, t1, t2, t3, {}, {}, async};
     if (prc) return prc;
     if (sync_rc) return sync_rc;
-    const size_t n = off.size();
     ok.assign(n, 0);
     if (n == 0) return SBFT_GV_OK;
     if (len.size() != n || n > 0xffffffffu) return SBFT_GV_EINVAL;
-    if (n >= ctx->min_split && ctx->slots.size() > 1) {  // large: the multi-device split path
+    if (split) {  // large: the multi-device split path
         // each share copies its own slice of the payload: this slot's copy is not used
         drain.armed = false;
         if (stream_sync(sl->stream) != hipSuccess) return SBFT_GV_EDEVICE;
@@ -1586,26 +1611,17 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
                                 ok.data(), nullptr, rebased[i], fr);
         });
     }
-    for (size_t k = 0; k < n; ++k) {
-        if (off[k] + len[k] > blob_len || off[k] + len[k] < off[k]) return SBFT_GV_EINVAL;
-        const int64_t end = (int64_t)(off[k] + len[k]);
-        for (int32_t rel : {sig_rel, pub_rel})
-            if (end + rel < 0 || (uint64_t)(end + rel) + 64 > blob_len) return SBFT_GV_EINVAL;
-    }
+    if (src) return src;  // the bounds checks and the offsets' staging above
     // Every request signed by a registered client key (kid[k] != 0 for all k, filled by
     // prepare): the keyed four-lane kernel over the clients' comb tables, hashing on a fifth
     // wavefront per workgroup and reading r || s from the payload; key ids beside the offsets
     // in mapped host memory. Smaller batches go through the caller's other paths.
     if (kid && kid->size() == n && ctx->keyed_lanes_min && n >= ctx->keyed_lanes_min) {
         const uint32_t nkeys = (uint32_t)ctx->nkeys.load();
-        const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256);
         rc = ensure_tables(sl, nkeys);
         if (!rc) rc = sl->reserve(align_up(n, 256));
-        if (!rc) rc = sl->reserve_vmap(fo + 2 * fl + align_up(n, 256));
         if (rc) return rc;
-        std::memcpy(sl->vmap, off.data(), 8 * n);
-        std::memcpy(sl->vmap + fo, len.data(), 4 * n);
-        std::memcpy(sl->vmap + fo + fl, kid->data(), 4 * n);
+        std::memcpy(sl->vmap + fo + fl, kid->data(), 4 * n);  // offsets, lengths: staged above
         const uint8_t* vd = sl->vmap_dev;
         // verdicts straight to mapped host memory (no device-to-host copy after the launch)
         if (sbft_launch_p256_verify_keyed_framed(sl->bbuf, (const uint64_t*)vd, (const uint32_t*)(vd + fo), sig_rel,
@@ -1623,10 +1639,9 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     // over PCIe, and the gather launch (first on the stream) zeroes both counters: no copy and
     // no memset launch between the parse and the hash (a pageable copy each and two memsets
     // cost ~40 us of the ~1 ms call, one pinned copy still ~25 us with its engine hand-off).
-    const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256), fd = align_up(32 * n, 256);
+    const size_t fd = align_up(32 * n, 256);
     const size_t fw = align_up(sbft_verify_work_bytes(n), 256);
     rc = sl->reserve(256 + fw + 5 * fd + align_up(n, 256));
-    if (!rc) rc = sl->reserve_vmap(fo + fl + align_up(n, 256) + 256);
     if (rc) return rc;
     uint8_t* b = sl->dbuf;
     uint8_t *d_ctr = b, *d_work = d_ctr + 256, *d_dig = d_work + fw;
@@ -1634,8 +1649,6 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     uint8_t* d_ok = v + 4 * fd;
     const void* gcomb = sl->gcomb_table();
     if (!gcomb) return SBFT_GV_ENOMEM;
-    std::memcpy(sl->vmap, off.data(), 8 * n);
-    std::memcpy(sl->vmap + fo, len.data(), 4 * n);
     const uint64_t* d_off = (const uint64_t*)sl->vmap_dev;
     const uint32_t* d_len = (const uint32_t*)(sl->vmap_dev + fo);
     // Small batches (lanes 2 / 4) hash inside the verify launch, on a second wavefront per
@@ -1645,6 +1658,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     if (framed_fused_on() && lanes >= 2) {
         // the verdicts go straight to mapped host memory (n bytes over PCIe from the kernels'
         // stores): no device-to-host copy and no copy-engine hand-off after the verify
+        if (trace) tr.e = TC::now();
         uint8_t* const h_ok = sl->vmap + fo + fl;
         uint8_t* const d_hok = sl->vmap_dev + fo + fl;
         // the fixup kernel (the exact net for flagged tuples, which the in-place repair leaves
@@ -1657,6 +1671,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
                                            v + 2 * fd, v + 3 * fd, d_hok, (uint32_t*)d_work, gcomb, sl->stream, lanes,
                                            (uint32_t*)(d_hok + align_up(n, 256))))
             return SBFT_GV_ELAUNCH;
+        if (trace) tr.f = TC::now();
         if (during) during();
         HIPCHK(stream_sync(sl->stream));
         if (*flag) {
