@@ -1432,7 +1432,7 @@ int sbft_gv_selftest_field(sbft_gv_ctx* ctx, int op, const uint8_t* a, const uin
                            uint8_t* out) {
     if (!ctx) return SBFT_GV_EINVAL;
     if (n == 0) return SBFT_GV_OK;
-    if (!a || !b || !out || op < 0 || op > 22 || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    if (!a || !b || !out || op < 0 || op > 26 || n > 0xffffffffu) return SBFT_GV_EINVAL;
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) { return enqueue_selftest(c, op, a, b, out); });
 }
 

@@ -116,12 +116,44 @@ SBFT_DEV fe selftest_f29(int op, const fe& x, const fe& y, const uint32_t* dtab)
     }
 }
 
+// Ops 23..26 run on lane pairs (2t, 2t + 1), both lanes on element 2t's inputs, as the half
+// kernel's ladder pairs do: 23 / 24 inv::inv_mod_pair mod p / mod n (x^-1, plain); 25 / 26 x / y
+// of 33P through the lane-local W ladder (p29_dbl_plw x5, then p29_add_aff_plw with P itself,
+// c = 1: W = Z^2). Every lane of the pair computes; both store the result.
+SBFT_DEV fe selftest_pair(int op, const fe& x, const fe& y, const uint32_t* dtab, bool odd) {
+    fe r = fe_zero();
+    if (op == 23 || op == 24) {
+        inv::inv_mod_pair(r.v, x.v, dtab, op == 23, odd);
+        return r;
+    }
+    const f29 px = to_mont29(x), py = to_mont29(y), one = f29_const(C29_ONE);
+    plw29 q;
+    q.xb = px;
+    q.zy = f29_sel_pair(one, py);
+    q.zo = one;
+    q.w = one;
+    for (int k = 0; k < 5; ++k) p29_dbl_plw(q);
+    p29_add_aff_plw(q, px, py);
+    jp29 t;
+    plw29_to(t, q);
+    fe ox, oy;
+    affine29(t, ox, oy, dtab);
+    return op == 25 ? ox : oy;
+}
+
 __global__ __launch_bounds__(256) void selftest_kernel(int op, const uint8_t* __restrict__ a,
                                                        const uint8_t* __restrict__ b,
                                                        uint8_t* __restrict__ out, uint32_t n) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     if (op == 10 || op >= 13) inv::stage_divstep_table(dtab);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (op >= 23 && op <= 26) {  // lane pairs: no lane leaves before its partner
+        const uint32_t e = ((i & ~1u) < n ? i : n - 1) & ~1u;
+        const fe x = load_be32(a + 32ull * e), y = load_be32(b + 32ull * e);
+        const fe r = selftest_pair(op, x, y, dtab, (i & 1u) != 0);
+        if (i < n) store_be32(out + 32ull * i, r);
+        return;
+    }
     if (i >= n) return;
     const fe x = load_be32(a + 32ull * i), y = load_be32(b + 32ull * i);
     fe r = fe_zero();

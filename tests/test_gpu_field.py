@@ -131,3 +131,31 @@ def test_f29_point_ops(gpu):
     assert _run(gpu, 17, pts) == [_mul(3, p)[0] for p in pts], "x(2P + P), mixed addition"
     assert _run(gpu, 18, pts) == [_mul(6, p)[1] for p in pts], "y(4P + 2P), Jacobian addition"
     assert _run(gpu, 19, pts) == [_mul(3, p)[1] for p in pts], "y(2P + P), negated twice"
+
+
+def test_pair_inversion(gpu):
+    """inv::inv_mod_pair (the half kernel's table inversion, split over a lane pair: the even lane
+    keeps f, g, the odd lane d, e) mod p and mod n, on element 2t's input in both lanes of the pair;
+    odd element counts leave the last pair half outside the batch (the kernel still runs it)."""
+    rng = random.Random(23)
+    for op, mod in ((23, P), (24, N)):
+        xs = [0, 1, 2, 3, mod - 1, mod - 2, (1 << 255) % mod, (1 << 224) % mod, 0xFFFFFFFF]
+        xs += [rng.randrange(1, mod) for _ in range(1200)]
+        for count in (len(xs), len(xs) - 1):
+            pairs = [(x, 0) for x in xs[:count]]
+            got = _run(gpu, op, pairs)
+            want = [pow(xs[i & ~1], -1, mod) if xs[i & ~1] else 0 for i in range(count)]
+            bad = [(i, hex(xs[i & ~1])) for i in range(count) if got[i] != want[i]]
+            assert not bad, (op, count, bad[:3])
+
+
+def test_pair_w_ladder(gpu):
+    """The half kernel's lane-local W ladder (p29_dbl_plw x5, then the five-step p29_add_aff_plw
+    with P itself; c = 1, so W = Z^2) against the group law: x and y of 33P on element 2t's point,
+    in both lanes of the pair."""
+    rng = random.Random(33)
+    pts = [(GX, GY)] + [_mul(rng.randrange(1, N), (GX, GY)) for _ in range(40)]
+    pts += [_mul(k, (GX, GY)) for k in (2, 3, N - 1, (N + 1) // 2)]
+    want = [_mul(33, pts[i & ~1]) for i in range(len(pts))]
+    assert _run(gpu, 25, pts) == [q[0] for q in want], "x(33P)"
+    assert _run(gpu, 26, pts) == [q[1] for q in want], "y(33P)"
