@@ -28,6 +28,7 @@
 
 #include "../../include/sbft_gpuverify.h"
 #include "engine_internal.h"
+#include "sinv_host.hpp"
 #include "sbft_kernels.h"
 
 static inline void cpu_relax() {
@@ -526,6 +527,11 @@ struct sbft_gv_ctx {
     // ... and batches of at least this many the four-lane kernel (p256_verify_keyed_lanes_kernel,
     // batched s^-1) instead of a wavefront per signature; SBFT_KEYED_LANES_MIN overrides (0 = never)
     size_t keyed_lanes_min = 1025;
+    // zero-copy keyed batches of at most this many signatures get s^-1 from the host (a batched
+    // inversion: one safegcd and ~4 products mod n per signature, ~7 us for a 67-signature quorum)
+    // instead of the kernel's second wavefront (~15 us: the divstep table and the wave-parallel
+    // safegcd); SBFT_KEYED_HOST_SINV_MAX overrides (0 = always on the device)
+    size_t keyed_host_sinv_max = 96;
     // registered public keys (x || y big-endian); index = key id, entry 0 = the generator
     std::mutex keys_mu;
     std::vector<std::array<uint8_t, 64>> keys;
@@ -684,6 +690,8 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     if (const char* e = getenv("SBFT_GV_CLIENT_TABLE_BYTES")) ctx->client_cap = strtoull(e, nullptr, 10);
     if (const char* e = getenv("SBFT_KEYED_ZC_MAX")) ctx->keyed_zc_max = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("SBFT_KEYED_LANES_MIN")) ctx->keyed_lanes_min = (size_t)strtoull(e, nullptr, 10);
+    if (const char* e = getenv("SBFT_KEYED_HOST_SINV_MAX"))
+        ctx->keyed_host_sinv_max = (size_t)strtoull(e, nullptr, 10);
     // slots per device (sbft_gv_opts.slots_per_device, SBFT_GV_SLOTS_PER_DEVICE): > 1 runs the
     // multi-device split on one GPU, each slot standing in for a device of its own
     uint32_t spd = opts && opts->slots_per_device ? opts->slots_per_device : 1u;
@@ -1968,7 +1976,7 @@ int build_tables(Slot* sl, const std::vector<std::array<uint8_t, 64>>& keys, siz
 //     commit-quorum call). A fault is caught by polling the stream now and then.
 int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t blob_len, const uint64_t* off,
                   const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint32_t* key, uint32_t nkeys,
-                  void** keytab, Slot::ZcLane* zl, uint8_t* ok_out, size_t lanes_min) {
+                  void** keytab, Slot::ZcLane* zl, uint8_t* ok_out, size_t lanes_min, size_t host_sinv_max) {
     Slot* sl = c.slot;
     const bool zc = zl != nullptr;
     hipStream_t st = zc ? zl->stream : sl->stream;  // (the lane's stream is created by its reserve)
@@ -1989,9 +1997,12 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
     const size_t fblob = align_up(span + SBFT_GV_SHA_BLOB_PAD, 256);  // + the hash kernel's over-read
     const size_t fmsg = blob ? fblob + align_up(8 * n, 256) + fk : f32;
     const size_t fok = align_up(n, 256);
-    const size_t in_bytes = 2 * f32 + fk + fmsg;
     // large batches: the four-lane kernel, with digests from the hash kernel (counter | digests)
     const bool lanes = !zc && lanes_min && n >= lanes_min;
+    // s^-1 from the host (modn::sinv_batch_mont) for small wavefront-kernel batches: | w after the messages
+    const bool host_sinv = !lanes && n > 0 && n <= host_sinv_max;
+    const size_t fw = host_sinv ? f32 : 0;
+    const size_t in_bytes = 2 * f32 + fk + fmsg + fw;
     const size_t fextra = lanes ? 256 + f32 : 0;
     HIPCHK(hipSetDevice(sl->device));
     int rc;
@@ -2023,6 +2034,7 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
     } else {
         std::memcpy(m, digest + 32 * b, 32 * n);
     }
+    if (host_sinv) sbft::modn::sinv_batch_mont(s + 32 * b, n, (uint32_t*)(h + 2 * f32 + fk + fmsg));
     volatile uint8_t* okh = h + in_bytes;
     if (zc) {
         std::memset((void*)okh, 0, n);
@@ -2050,7 +2062,8 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
             return SBFT_GV_ELAUNCH;
     } else if (sbft_launch_p256_verify_keyed(blob ? nullptr : dm, d_blob, d_off, d_len, d, d + f32,
                                              (const uint32_t*)(d + 2 * f32), (const void* const*)keytab, nkeys,
-                                             d_ok, (uint32_t)n, zc ? 2 : 0, st)) {
+                                             d_ok, (uint32_t)n, zc ? 2 : 0,
+                                             host_sinv ? (const uint32_t*)(d + 2 * f32 + fk + fmsg) : nullptr, st)) {
         return SBFT_GV_ELAUNCH;
     }
     if (!zc) {
@@ -2138,13 +2151,14 @@ int run_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* blob, size
             }
             std::unique_lock<std::mutex> zlk;
             Slot::ZcLane& zl = c.slot->acquire_zc(zlk);
-            return enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, keytab, &zl, ok_out, 0);
+            return enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, keytab, &zl, ok_out, 0,
+                                 ctx->keyed_host_sinv_max);
         }
         std::lock_guard<std::mutex> lk(c.slot->mu);
         int rc = ensure_tables(c.slot, nkeys);
         if (rc == SBFT_GV_OK)
             rc = enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, c.slot->d_keytab, nullptr,
-                               ok_out, ctx->keyed_lanes_min);
+                               ok_out, ctx->keyed_lanes_min, ctx->keyed_host_sinv_max);
         (void)hipSetDevice(c.slot->device);
         if (stream_sync(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
         // the verdicts sit in the slot's pinned staging, which the lock still protects

@@ -463,11 +463,11 @@ __global__ __launch_bounds__(128) void p256_verify_keyed_wave_kernel(
     const uint8_t* __restrict__ digest, const uint8_t* __restrict__ blob, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint8_t* __restrict__ rr, const uint8_t* __restrict__ ss,
     const uint32_t* __restrict__ key, const uint4* const* __restrict__ keytab, uint32_t nkeys,
-    uint8_t* __restrict__ ok, uint32_t n, uint8_t mark) {
+    uint8_t* __restrict__ ok, uint32_t n, uint8_t mark, const uint32_t* __restrict__ winv) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     __shared__ u32 w_lds[8];
     SBFT_KEYED_MARK(0);
-    inv::stage_divstep_table(dtab);
+    if (!winv) inv::stage_divstep_table(dtab);  // (kernel-uniform: winv is an argument)
     SBFT_KEYED_MARK(1);
     const uint32_t t = blockIdx.x;
     const u32 lane = threadIdx.x & 63u;
@@ -481,7 +481,11 @@ __global__ __launch_bounds__(128) void p256_verify_keyed_wave_kernel(
     const bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
                        kid >= 1 && kid < nkeys && keytab[kid] != nullptr;
     fe e_raw;
-    if (wave == 1) {
+    if (wave == 1 && winv) {  // s^-1 R mod n from the host (host_sinv_batch, gpuverify.cpp)
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w_lds[k] = winv[8ull * t + k];
+    } else if (wave == 1) {
         // w = s^-1 (plain)
         fe sv = s, w;
         if (!valid) {
@@ -698,11 +702,12 @@ extern "C" size_t sbft_comb_table_bytes(void) { return (size_t)COMB_KEY_U4 * 16;
 extern "C" int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint8_t* d_blob, const uint64_t* d_off,
                                              const uint32_t* d_len, const uint8_t* d_r, const uint8_t* d_s,
                                              const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
-                                             uint8_t* d_ok, uint32_t n, uint8_t mark, hipStream_t stream) {
+                                             uint8_t* d_ok, uint32_t n, uint8_t mark, const uint32_t* d_winv,
+                                             hipStream_t stream) {
     if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
     if (!d_digest && (!d_blob || !d_off || !d_len)) return -1;
     hipLaunchKernelGGL(sbft::p256_verify_keyed_wave_kernel, dim3(n), dim3(128), 0, stream, d_digest, d_blob, d_off,
-                       d_len, d_r, d_s, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n, mark);
+                       d_len, d_r, d_s, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n, mark, d_winv);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

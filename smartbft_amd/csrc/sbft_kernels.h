@@ -119,5 +119,6 @@ int sbft_launch_p256_verify_keyed_framed(const uint8_t* d_blob, const uint64_t* 
 int sbft_launch_p256_verify_keyed(const uint8_t* d_digest, const uint8_t* d_blob, const uint64_t* d_off,
                                   const uint32_t* d_len, const uint8_t* d_r, const uint8_t* d_s,
                                   const uint32_t* d_key, const void* const* d_keytab, uint32_t nkeys,
-                                  uint8_t* d_ok, uint32_t n, uint8_t mark, hipStream_t stream);
+                                  uint8_t* d_ok, uint32_t n, uint8_t mark, const uint32_t* d_winv,
+                                  hipStream_t stream);
 }

@@ -107,3 +107,24 @@ def test_half_gcd_matches_euclid(tmp_path, rounds):
         assert (w, sv) == (w_x, v_x), hex(u)
         assert (sv * u - w) % N == 0 and 0 < w < 1 << 128 and 0 < v < 1 << 128, hex(u)
     assert nfail < 60  # only the crafted large-quotient inputs
+
+
+@pytest.mark.parametrize("count", [1, 2, 67, 96, 500])
+def test_host_batch_sinv(tmp_path, count):
+    """modn::sinv_batch_mont (sinv_host.hpp): the keyed path's host-side s^-1 for a batch, by
+    Montgomery's trick and one safegcd, in the Montgomery form the keyed kernel takes
+    (s^-1 2^256 mod n); s = 0 and s >= n stand in as 1."""
+    exe = str(tmp_path / "sinv_test")
+    subprocess.run(["g++", "-O2", "-Wall", "-Werror", "-o", exe,
+                    os.path.join(ROOT, "tests", "native", "sinv_test.cpp")], check=True)
+    rng = random.Random(count)
+    n = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+    edge = [1, 2, n - 1, n, n + 1, 0, (1 << 256) - 1, 1 << 255, 0xFFFFFFFF]
+    ss = (edge + [rng.randrange(1, n) for _ in range(count)])[:count] if count > len(edge) else \
+        [rng.randrange(1, n) for _ in range(count)]
+    out = subprocess.run([exe], input="".join("%064x\n" % x for x in ss), capture_output=True, text=True,
+                         check=True).stdout.split()
+    assert len(out) == count
+    for x, got in zip(ss, out):
+        v = x if 0 < x < n else 1
+        assert int(got, 16) == pow(v, -1, n) * (1 << 256) % n, hex(x)

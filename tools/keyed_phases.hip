@@ -82,7 +82,7 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 20; ++rep) {
         CHK(hipEventRecord(a));
         if (sbft_launch_p256_verify_keyed(de, nullptr, nullptr, nullptr, r, s, dkey, (const void* const*)keytab, 2,
-                                          dok, n, 0, 0))
+                                          dok, n, 0, nullptr, 0))
             return 1;
         CHK(hipEventRecord(b));
         CHK(hipEventSynchronize(b));
