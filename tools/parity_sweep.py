@@ -5,6 +5,9 @@ crypto/ecdsa.Verify: the checker, as in the tests). Prints one JSON line.
 
   python tools/parity_sweep.py --n 2000000 --threads 16
 
+With --hash / --framed, messages hashed on the GPU as well (config 5's HBM and streamed paths, the
+VerifyProposal layout through the fused half kernel): see hash_sweep.
+
 Kinds (a tuple gets one; ~30% stay untouched):
   flip r / s / e bit, r = 0, s = 0, s = n, r = n + small, r = n - 1, s = n - s (high-s form, still
   valid), Qy -> Qy + 1 (off the curve), Q -> -Q (a valid point, the wrong key), Qx / Qy >= p,
@@ -98,12 +101,113 @@ def build(gv, n, seed):
     return e, r, s, qx, qy, kind
 
 
+def hash_sweep(gv, a, out, record_to):
+    """Messages hashed on the GPU, then verified: the HBM path (config 5), the streamed path, and
+    the VerifyProposal layout (body ending in qx || qy, r || s after it; the fused half kernel at
+    10k per call, the size-selected kernels at 50k). Corruptions: a body byte flipped after
+    signing, r or s flipped, the key's last byte flipped (framed: off the curve, and a different
+    digest). The oracle gets hashlib's digests."""
+    import hashlib
+    rng = np.random.default_rng(a.seed + 1)
+
+    def keys_and_sigs(bodies):
+        m = len(bodies)
+        d, k = scalars(rng, m), scalars(rng, m)
+        one = np.zeros((m, 32), dtype=np.uint8)
+        one[:, 31] = 1
+        qx, qy, _, _, st = gv.sign(d, one, one)
+        assert (st == 1).all()
+        return d, k, np.array(qx), np.array(qy)
+
+    def sign(d, k, bodies):
+        e = np.frombuffer(b"".join(hashlib.sha256(b).digest() for b in bodies), dtype=np.uint8).reshape(-1, 32)
+        _, _, r, s, st = gv.sign(d, k, e)
+        assert (st == 1).all()
+        return np.array(r), np.array(s)
+
+    def check(name, got, bodies, r, s, qx, qy):
+        e = np.frombuffer(b"".join(hashlib.sha256(b).digest() for b in bodies), dtype=np.uint8).reshape(-1, 32)
+        want = oracle.verify_batch(e, r, s, qx, qy, nthreads=a.threads)
+        bad = int((got != want).sum())
+        record_to[name] = {"tuples": int(len(got)), "bad": bad, "accepts": int(want.sum())}
+        print(name, len(got), "bad", bad, flush=True)
+
+    # config-5 layout: free-standing messages
+    m = a.hash
+    lens = rng.integers(0, 4097, size=m)
+    raw = rng.integers(0, 256, size=int(lens.sum()) + m * 3, dtype=np.uint8).tobytes()
+    bodies, pos = [], 0
+    for ln in lens:
+        pos += int(rng.integers(0, 4))  # unaligned starts
+        bodies.append(raw[pos:pos + int(ln)])
+        pos += int(ln)
+    d, k, qx, qy = keys_and_sigs(bodies)
+    r, s = sign(d, k, bodies)
+    kind = rng.integers(0, 4, size=m)
+    bodies = [bytearray(b) for b in bodies]
+    for i in np.nonzero(kind == 1)[0]:
+        if len(bodies[i]):
+            bodies[i][int(rng.integers(0, len(bodies[i])))] ^= 1
+    for i in np.nonzero(kind == 2)[0]:
+        r[i, 31] ^= 1
+    for i in np.nonzero(kind == 3)[0]:
+        s[i, 0] ^= 0x80
+    bodies = [bytes(b) for b in bodies]
+    off = np.zeros(m, dtype=np.uint64)
+    p = 0
+    for i, b in enumerate(bodies):
+        p += i % 4
+        off[i] = p
+        p += len(b)
+    blob = bytearray(p)
+    for i, b in enumerate(bodies):
+        blob[int(off[i]):int(off[i]) + len(b)] = b
+    blob = np.frombuffer(bytes(blob), dtype=np.uint8)
+    ln = np.array([len(b) for b in bodies], dtype=np.uint32)
+    check("hash_verify_hbm", gv.sha256_verify(blob, off, ln, r, s, qx, qy), bodies, r, s, qx, qy)
+    check("hash_verify_stream", gv.sha256_verify_stream(blob, off, ln, r, s, qx, qy, window_bytes=64 << 20),
+          bodies, r, s, qx, qy)
+
+    # VerifyProposal layout: body = payload || qx || qy, then r || s
+    f = a.framed
+    d, k, qx, qy = keys_and_sigs([b""] * f)
+    pay = [rng.integers(0, 256, size=int(rng.integers(0, 400)), dtype=np.uint8).tobytes() for _ in range(f)]
+    bodies = [pay[i] + qx[i].tobytes() + qy[i].tobytes() for i in range(f)]
+    r, s = sign(d, k, bodies)
+    kind = rng.integers(0, 4, size=f)
+    bodies = [bytearray(b) for b in bodies]
+    for i in np.nonzero(kind == 1)[0]:
+        bodies[i][int(rng.integers(0, len(bodies[i])))] ^= 4
+    for i in np.nonzero(kind == 2)[0]:
+        s[i, 31] ^= 1
+    for i in np.nonzero(kind == 3)[0]:
+        bodies[i][-1] ^= 1  # the key's last byte: off the curve (and another digest)
+    bodies = [bytes(b) for b in bodies]
+    qxf = np.frombuffer(b"".join(b[-64:-32] for b in bodies), dtype=np.uint8).reshape(f, 32)
+    qyf = np.frombuffer(b"".join(b[-32:] for b in bodies), dtype=np.uint8).reshape(f, 32)
+    parts, offs, lns, p = [], [], [], 1
+    for i, b in enumerate(bodies):
+        offs.append(p)
+        lns.append(len(b))
+        parts.append(b + r[i].tobytes() + s[i].tobytes())
+        p += len(b) + 64
+    blob = np.frombuffer(b"\0" + b"".join(parts), dtype=np.uint8)
+    offs, lns = np.array(offs, dtype=np.uint64), np.array(lns, dtype=np.uint32)
+    got = np.concatenate([gv.sha256_verify_framed(blob, offs[i:i + 10_000], lns[i:i + 10_000], 0, -64)
+                          for i in range(0, f, 10_000)])
+    check("framed_10k_calls", got, bodies, r, s, qxf, qyf)
+    check("framed_one_call", gv.sha256_verify_framed(blob, offs, lns, 0, -64), bodies, r, s, qxf, qyf)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=2_000_000)
     ap.add_argument("--seed", type=int, default=2605)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--exact", type=int, default=200_000, help="tuples through the exact (8x32) kernel")
+    ap.add_argument("--hash", type=int, default=300_000,
+                    help="messages (0-4096 B, unaligned, hashed on the GPU) for the hash + verify paths")
+    ap.add_argument("--framed", type=int, default=50_000, help="signed requests in the VerifyProposal layout")
     ap.add_argument("--keyed", type=int, default=3000,
                     help="tuples through the keyed paths (a 512 KiB comb table per registered key)")
     a = ap.parse_args()
@@ -144,6 +248,8 @@ def main():
         record(name, got, sel)
     record("keyed_lanes", gv.verify_keyed(e[sel], r[sel], s[sel], kid), sel)  # >= 1025: four lanes
     out["keyed_registered"] = int(okk.sum())
+    if a.hash:
+        hash_sweep(gv, a, out, record_to=out["mismatches"])
     out["pass"] = all(v["bad"] == 0 for v in out["mismatches"].values())
     print(json.dumps(out), flush=True)
     gv.close()
