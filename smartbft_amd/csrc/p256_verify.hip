@@ -811,9 +811,6 @@ SBFT_DEV void build_q_table_pair_w(const f29& qxm, const f29& qym, const f29& ac
         pmul(X, Y, X, l2k, yl, l2k);
         st(k, X, Y);
         lam = nxt;  // 1 / Z(T_{k-1})
-#ifdef SBFT_HALF_PROBE_TAB  // development: marks after the first and the fourth conversion
-        if (k == kQTab - 1 || k == kQTab - 4) mark(2);
-#endif
     }
     f29 x0, y0;
     pmul(x0, y0, qxm, kap, qym, kap);  // the base itself, divided by c
@@ -873,6 +870,23 @@ SBFT_DEV int q_digit(const fe& k2, int i) {
     constexpr int tab = 1 << (W - 1);
     const int b = W * i + 1, lw = b >> 5;
     const u32 lo = k2.v[lw], hi = lw < 7 ? k2.v[lw + 1] : 0u;
+    return 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & (2 * tab - 1)) - (2 * tab - 1);
+}
+
+// q_digit with the two words picked by selects instead of a runtime index into k2: a runtime
+// index makes k2 an alloca, which LLVM promotes to LDS (8 KB of the half kernel's workgroup, read
+// back every digit); its absence measured 13 us less per 10k-tuple launch (profiles/
+// r05ad_nolds_ab.txt: the table build ends ~10 us earlier). 16 selects per digit.
+template <int W = kQWin>
+SBFT_DEV int q_digit_sel(const fe& k2, int i) {
+    constexpr int tab = 1 << (W - 1);
+    const int b = W * i + 1, lw = b >> 5;
+    u32 lo = 0u, hi = 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        lo = lw == j ? k2.v[j] : lo;
+        hi = lw + 1 == j ? k2.v[j] : hi;
+    }
     return 2 * (int)(__builtin_amdgcn_alignbit(hi, lo, b & 31) & (2 * tab - 1)) - (2 * tab - 1);
 }
 
@@ -1498,6 +1512,9 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
 #define SBFT_HALF_TUPLES 48
 #endif
 constexpr int kHalfTuples = SBFT_HALF_TUPLES;  // per workgroup
+#ifndef SBFT_HALF_DIGIT_SEL
+#define SBFT_HALF_DIGIT_SEL 1  // digits by selects (q_digit_sel): no alloca, no LDS promotion
+#endif
 #ifndef SBFT_HALF_INV_PAIR
 #define SBFT_HALF_INV_PAIR 1  // the table's inversion split over the pair (inv::inv_mod_pair)
 #endif
@@ -1560,20 +1577,24 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
 #ifdef SBFT_HALF_PROBE  // development: phase times of workgroup 0 (tools/half_probe.py), 100 MHz ticks,
                         // kept in registers and printed once at the end (a printf is a blocking host call)
     // (and the shader-clock counter beside it: the clock of a phase is its s_memtime ticks over its
-    // real-time ticks times 100 MHz)
+    // real-time ticks times 100 MHz). Marks take constant slot numbers, so the stamps stay in
+    // (scalar) registers: a runtime slot index put the arrays in scratch, whose stores then
+    // lengthened the waits in front of the barriers (~20 us of a probed launch).
     const uint64_t probe_t0 = __builtin_amdgcn_s_memrealtime(), probe_c0 = __builtin_amdgcn_s_memtime();
     uint32_t probe_t[8] = {0, 0, 0, 0, 0, 0, 0, 0}, probe_c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int probe_n = 0;
-    auto probe = [&](const char*, bool) {
+    auto probe = [&](int i) {
         const uint32_t t = (uint32_t)(__builtin_amdgcn_s_memrealtime() - probe_t0);
         const uint32_t c = (uint32_t)(__builtin_amdgcn_s_memtime() - probe_c0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if (i == probe_n) {
-                probe_t[i] = t;
-                probe_c[i] = c;
-            }
-        ++probe_n;
+        switch (i) {  // constant at every call site once inlined
+        case 0: probe_t[0] = t; probe_c[0] = c; break;
+        case 1: probe_t[1] = t; probe_c[1] = c; break;
+        case 2: probe_t[2] = t; probe_c[2] = c; break;
+        case 3: probe_t[3] = t; probe_c[3] = c; break;
+        case 4: probe_t[4] = t; probe_c[4] = c; break;
+        case 5: probe_t[5] = t; probe_c[5] = c; break;
+        case 6: probe_t[6] = t; probe_c[6] = c; break;
+        default: probe_t[7] = t; probe_c[7] = c; break;
+        }
     };
     auto probe_dump = [&](const char* who, bool me) {
         if (me && blockIdx.x == 0) {
@@ -1584,7 +1605,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         }
     };
 #else
-    auto probe = [](const char*, bool) {};
+    auto probe = [](int) {};
     auto probe_dump = [](const char*, bool) {};
 #endif
 
@@ -1633,7 +1654,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         fn_mul(u2, r, wm);
         fn_canon(u2, u2);
         if (!valid) u2 = one;
-        probe("helper_sinv", lane == 0);
+        probe(0);
         hgcd::state hs;
         hgcd::init(hs, u2.v);
 #pragma unroll 1
@@ -1654,7 +1675,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             fn_canon(t, t);
             good = good && fe_eq(t, vneg ? mod_n_neg(w) : w);
         }
-        probe("helper_hgcd", lane == 0);
+        probe(1);
         const bool fb = valid && (!good || fe_lt(r, P256_PMN));  // the classic way: v = 1, w = u2
         fe ka = w, kb = va;
         if (fb || !valid) {
@@ -1670,9 +1691,9 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             }
             hsc[16 * T + lane] = (vneg ? 1u : 0u) | (fb ? 2u : 0u) | (valid ? 4u : 0u);
         }
-        probe("helper_published", lane == 0);
+        probe(2);
         __syncthreads();  // #1: the scalars are in hsc (the verify wavefronts' tables in qtab)
-        probe("helper_barrier1", lane == 0);
+        probe(3);
         fe e_raw;
         if constexpr (FRAMED) {
             uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
@@ -1693,7 +1714,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         } else {
             e_raw = load_be32(digest + 32ull * ic);
         }
-        probe("helper_hash", lane == 0);
+        probe(4);
         fe e, u1, c;
         fn_canon(e, e_raw);
         fn_mul(u1, e, wm);
@@ -1711,7 +1732,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         bool ginf = true;  // the first addition returns its addend (add_aff_fix)
         comb_add_u1g(g, c, neg1, gcomb, [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
                      [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
-        probe("helper_comb", lane == 0);
+        probe(5);
         // No square test here (round 5): whether x = r is on the curve at all (r^3 - 3r + b a
         // square) is decided by the comparison itself; only an irregular end of the ladders
         // (Z_T or W_V = 0, never for an honest tuple) needs it, and the verify wavefronts compute
@@ -1758,7 +1779,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         for (int i = 0; i < 9; ++i) rhs.v[i] = t3.v[i] - 3u * rm.v[i] + b.v[i];  // |limb| < 2^31, |.| < 2^259
         f29_normalize(rhs, rhs);                                                  // c (N')
     }
-    probe("verify_inputs", tid == 0);
+    probe(0);
     const bool onc = role == 1;  // this pair runs on E_c (pair A on the curve, c = 1)
     f29 px, py, cc, ac;
     {
@@ -1791,7 +1812,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                 else inv::inv_mod(zi.v, zp.v, dtab, true);
                 return zi;
             },
-            [&](int m) { probe(m ? "verify_inverse" : "verify_chain", tid == 0); }, st, ld,
+            [&](int m) { probe(m ? (m == 1 ? 2 : 3) : 1); }, st, ld,
             [&](int m, const f29& h) {
 #pragma unroll
                 for (int k = 0; k < 9; ++k) hrat[(m * 9 + k) * 2 * T + col] = h.v[k];
@@ -1801,9 +1822,9 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                 for (int k = 0; k < 9; ++k) h.v[k] = hrat[(m * 9 + k) * 2 * T + col];
             });
     }
-    probe("verify_tables", tid == 0);
+    probe(3);
     __syncthreads();  // #1: tables in qtab, the helper's scalars in hsc
-    probe("verify_barrier1", tid == 0);
+    probe(4);
 
     const u32 flags = hsc[16 * T + pr];
     const bool valid = (flags & 4u) != 0;
@@ -1832,7 +1853,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         }
     };
     auto qentry = [&](int i, f29& x, f29& y) {
-        const int d = q_digit(k, i);
+        const int d = SBFT_HALF_DIGIT_SEL ? q_digit_sel(k, i) : q_digit(k, i);
         tab_entry((d < 0 ? -d : d) >> 1, x, y);
         if ((d < 0) != negb) f29_neg(y, y);
     };
@@ -1902,7 +1923,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             inf = infa;
         }
     }
-    probe("verify_ladder", tid == 0);
+    probe(5);
     f29 VX, VW;  // pair B's X and W = c Z^2 of v R0, on pair A's lanes (quad_perm [2,3,2,3])
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
@@ -1911,7 +1932,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     }
 
     __syncthreads();  // #2: the helper's (v u1) G and the square test are in gsum
-    probe("verify_barrier2", tid == 0);
+    probe(6);
     const u32 gflags = gsum[27 * T + pr];
     {
         jp29 g;
@@ -1983,7 +2004,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         accept = false;
         exc = false;
     }
-    probe("verify_final", tid == 0);
+    probe(7);
     probe_dump(tid == 0 ? "verify inputs,chain,inverse,tables,barrier1,ladder,barrier2,final"
                         : (tid == 64 ? "verify-w1" : "verify-w2"),
                tid == 0 || tid == 64 || tid == 128);
