@@ -877,6 +877,9 @@ SBFT_DEV int q_digit(const fe& k2, int i) {
 // index makes k2 an alloca, which LLVM promotes to LDS (8 KB of the half kernel's workgroup, read
 // back every digit); its absence measured 13 us less per 10k-tuple launch (profiles/
 // r05ad_nolds_ab.txt: the table build ends ~10 us earlier). 16 selects per digit.
+#ifndef SBFT_PAIR_DIGIT_SEL
+#define SBFT_PAIR_DIGIT_SEL 1  // the pair kernel's digits by selects as well
+#endif
 template <int W = kQWin>
 SBFT_DEV int q_digit_sel(const fe& k2, int i) {
     constexpr int tab = 1 << (W - 1);
@@ -1376,7 +1379,7 @@ __global__ __launch_bounds__((small_kernel_threads<LPT, FRAMED>())) void p256_ve
 #define SBFT_PAIR_LADDER_DIGITS kQDigits
 #endif
     auto qentry = [&](int i, f29& x, f29& y) {
-        const int d2 = q_digit(k2, i);
+        const int d2 = SBFT_PAIR_DIGIT_SEL ? q_digit_sel(k2, i) : q_digit(k2, i);  // (see q_digit_sel)
         const int m2 = (d2 < 0 ? -d2 : d2) >> 1;
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
