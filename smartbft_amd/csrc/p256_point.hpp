@@ -428,11 +428,24 @@ SBFT_DEV void store_be32(uint8_t* p, const fe& a) {
 #define COMB_KEY_U4 (COMB_WINDOWS * COMB_ENTRIES * COMB_ENTRY_U4)
 
 // byte w (0..31, little-endian) of a 256-bit value, w lane-varying
+#ifndef SBFT_BYTE_OF_REGS
+#define SBFT_BYTE_OF_REGS 0  // measured: no gain (profiles/r05ag_byteof_ab.txt)
+#endif
+// LLVM rewrites this select chain into a 32-B stack array and one indexed scratch load (the keyed
+// wave kernel's 36-B private segment). SBFT_BYTE_OF_REGS=1 puts an empty asm after each select to
+// keep it in registers (private segment 0); the keyed wave kernel measured 0.1-0.4 us slower that
+// way (35.6-35.9 vs 35.3-35.5 us, profiles/r05ag_byteof_ab.txt): the scratch load issues early
+// and hides behind the entry loads, the 14 extra VALU per byte do not.
 SBFT_DEV u32 byte_of(const fe& a, u32 w) {
     const u32 limb_i = w >> 2;
     u32 limb = a.v[0];
 #pragma unroll
-    for (int k = 1; k < 8; ++k) limb = (limb_i == (u32)k) ? a.v[k] : limb;
+    for (int k = 1; k < 8; ++k) {
+        limb = (limb_i == (u32)k) ? a.v[k] : limb;
+#if SBFT_BYTE_OF_REGS
+        asm("" : "+v"(limb));
+#endif
+    }
     return (limb >> (8 * (w & 3))) & 255u;
 }
 
