@@ -1028,6 +1028,36 @@ SBFT_DEV void f29_mul_sub_ilp(f29& r, const f29& a, const f29& b, const f29& c, 
 SBFT_DEV void f29_mul_ilp(f29& r, const f29& a, const f29& b) { f29_mulsq_ilp<false>(r, a, b); }
 SBFT_DEV void f29_sqr_ilp(f29& r, const f29& a) { f29_mulsq_ilp<true>(r, a, a); }
 
+// p29_add_aff_lean_f with the pipelined ILP products (one lane, no pairing): the same 8M + 3S,
+// the same values limb for limb (the column sums are exact either way), but at one wave per SIMD
+// the chain form's dependent mads leave most issue slots idle. For the latency kernels whose
+// lanes each run their own additions (the registered-client comb, p256_verify_keyed_lanes_kernel).
+SBFT_DEV void p29_add_aff_lean_ilp(jp29& acc, const f29& x2, const f29& y2) {
+    f29 z1z1, u2, t, h, s2, hh, rr, hhh, v, x3, nd;
+    f29_sqr_ilp(z1z1, acc.z);
+    f29_mul_ilp(u2, x2, z1z1);
+    f29_mul_ilp(t, acc.z, z1z1);
+    f29_sub(h, u2, acc.x);           // (-2^29.2, 2^29 + 2^25)
+    f29_mul_ilp(s2, y2, t);          // S2 = y2 Z1^3
+    f29_sqr_ilp(hh, h);
+    f29_sub(rr, s2, acc.y);          // (-2^29.2, 2^29.2)
+    f29_mul_ilp(hhh, hh, h);
+    f29_mul_ilp(v, acc.x, hh);       // V = X1 H^2
+    f29_mul_ilp(acc.z, acc.z, h);    // Z3 = Z1 H
+    {
+        const f29* const va[2] = {&hhh, &v};
+        const u32 c[2] = {(u32)-1, (u32)-2};
+        f29_mulsq_add_ilp<true, 2>(x3, rr, rr, va, c, ~0u);  // X3 = r^2 - HHH - 2V: N'
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        t.v[i] = v.v[i] - x3.v[i];   // (-2^29.2, 2^29 + 2^25)
+        nd.v[i] = 0u - hhh.v[i];
+    }
+    f29_mul_sub_ilp(acc.y, rr, t, acc.y, nd);  // r t - Y1 H^3: N
+    acc.x = x3;
+}
+
 SBFT_DEV f29 f29_pick(bool odd, const f29& even_v, const f29& odd_v) {
     f29 r;
 #pragma unroll

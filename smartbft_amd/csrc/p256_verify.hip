@@ -2075,18 +2075,54 @@ SBFT_DEV void quad_combine(jp29& acc, bool& inf) {
 // (fr.blob/off/len, r || s at the body's end + fr.sig_rel); a fifth wavefront per workgroup
 // hashes the workgroup's 64 bodies into LDS while the four verify wavefronts invert s, and
 // the digests are picked up after that barrier. No hash kernel in front.
+#ifndef SBFT_KEYED_LANES_ILP
+#define SBFT_KEYED_LANES_ILP 1  // the comb's additions in the pipelined ILP product form
+#endif
+#ifndef SBFT_KEYED_LANES_PINGPONG
+#define SBFT_KEYED_LANES_PINGPONG 1  // the comb's entries in two fixed buffers (see the kernel)
+#endif
+// FRAMED: signatures per workgroup (a multiple of 16). 48: three verify wavefronts and the hash
+// wavefront, one per SIMD, so the hash (the comb's wait for its digests) does not share a SIMD
+// with an inverting wavefront; 64: four verify wavefronts and the hash wavefront on five.
+#ifndef SBFT_KEYED_FRAMED_TPB
+#define SBFT_KEYED_FRAMED_TPB 48
+#endif
 template <bool FRAMED = false>
-__global__ __launch_bounds__(FRAMED ? 320 : 256) void p256_verify_keyed_lanes_kernel(
+__global__ __launch_bounds__(FRAMED ? 4 * SBFT_KEYED_FRAMED_TPB + 64 : 256) void p256_verify_keyed_lanes_kernel(
     const uint8_t* __restrict__ digest, const uint8_t* __restrict__ rr, const uint8_t* __restrict__ ss,
     const uint32_t* __restrict__ key, const uint4* const* __restrict__ keytab, uint32_t nkeys,
     uint8_t* __restrict__ ok, uint32_t n, FramedIn fr) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     __shared__ u32 edig[FRAMED ? 8 * 64 : 1];  // FRAMED: [word][signature of the workgroup]
     inv::stage_divstep_table(dtab);  // ends with a barrier
+#ifdef SBFT_KEYED_PROBE  // development: phase times of workgroup 0 (tools/keyed_lanes_probe.py), as the
+                         // half kernel's SBFT_HALF_PROBE: 100 MHz real-time ticks in constant slots
+    const uint64_t probe_t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t probe_t[6] = {0, 0, 0, 0, 0, 0};
+    auto probe = [&](int i) {
+        const uint32_t t = (uint32_t)(__builtin_amdgcn_s_memrealtime() - probe_t0);
+        switch (i) {
+        case 0: probe_t[0] = t; break;
+        case 1: probe_t[1] = t; break;
+        case 2: probe_t[2] = t; break;
+        case 3: probe_t[3] = t; break;
+        case 4: probe_t[4] = t; break;
+        default: probe_t[5] = t; break;
+        }
+    };
+    auto probe_dump = [&](const char* who) {
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0)
+            printf("keyed-probe %s %u %u %u %u %u %u\n", who, probe_t[0], probe_t[1], probe_t[2], probe_t[3],
+                   probe_t[4], probe_t[5]);
+    };
+#else
+    auto probe = [](int) {};
+    auto probe_dump = [](const char*) {};
+#endif
     if constexpr (FRAMED) {
-        if (threadIdx.x >= 256) {  // the hash wavefront
-            const uint32_t lane = threadIdx.x - 256, th = blockIdx.x * 64 + lane;
-            if (th < n) {
+        if (threadIdx.x >= 4 * SBFT_KEYED_FRAMED_TPB) {  // the hash wavefront
+            const uint32_t lane = threadIdx.x - 4 * SBFT_KEYED_FRAMED_TPB, th = blockIdx.x * SBFT_KEYED_FRAMED_TPB + lane;
+            if (lane < SBFT_KEYED_FRAMED_TPB && th < n) {
                 const uint8_t* msg = fr.blob + fr.off[th];
                 const uint32_t L = fr.len[th], nb = sha256_nblocks(L);
                 uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
@@ -2099,11 +2135,14 @@ __global__ __launch_bounds__(FRAMED ? 320 : 256) void p256_verify_keyed_lanes_ke
 #pragma unroll
                 for (int k = 0; k < 8; ++k) edig[k * 64 + lane] = h[k];
             }
+            probe(0);
             __syncthreads();  // the verify wavefronts' digest barrier
+            probe(1);
+            probe_dump("hash");
             return;
         }
     }
-    const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t gid = blockIdx.x * (FRAMED ? 4 * SBFT_KEYED_FRAMED_TPB : 256) + threadIdx.x;
     const uint32_t t = gid >> 2, j = gid & 3u;
     const bool active = t < n;
     const uint32_t idx = active ? t : n - 1;
@@ -2131,9 +2170,11 @@ __global__ __launch_bounds__(FRAMED ? 320 : 256) void p256_verify_keyed_lanes_ke
         const fe rn = fe_const(C_ONEN);  // 2^256 mod n
         inv::inv_mod(w.v, sv.v, dtab, false, rn.v);
     }
+    probe(0);
     fe e, u;
     if constexpr (FRAMED) {
         __syncthreads();  // the hash wavefront's digests
+        probe(1);
         fe d;
         const uint32_t sl = threadIdx.x >> 2;
 #pragma unroll
@@ -2144,31 +2185,22 @@ __global__ __launch_bounds__(FRAMED ? 320 : 256) void p256_verify_keyed_lanes_ke
     }
     fn_mul(u, j < 2 ? e : r, w);  // u1 = e s^-1 (j < 2) or u2 = r s^-1 (plain)
     fn_canon(u, u);
+#ifdef SBFT_KEYED_HOT_TABLE  // development (timing only, wrong verdicts): every u2 Q from one key's table
+    const uint4* tab = keytab[j < 2 ? 0u : (valid ? 1u : 0u)];
+#else
     const uint4* tab = keytab[j < 2 ? 0u : (valid ? kid : 0u)];
+#endif
     const u32 w0 = 16u * (j & 1u);
-    // 16 entries, the next one's loads issued before the current addition
     jp29 acc;
     bool inf = true;
     acc.z = f29_const(C29_ONE);
-    uint4 cur[4], nxt[4];
-    auto entry = [&](u32 i, uint4 (&en)[4]) {
-        const u32 win = w0 + i;
-        const uint4* p = tab + (size_t)(win * COMB_ENTRIES + byte_of(u, win)) * COMB_ENTRY_U4;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) en[k] = p[k];
-    };
-    entry(0, nxt);
-#pragma unroll 1
-    for (u32 i = 0; i < 16; ++i) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-        if (i < 15) entry(i + 1, nxt);
-        const bool zero = byte_of(u, w0 + i) == 0;
+    auto add_entry = [&](const uint4 (&cur)[4], bool zero) {
         const fe ex = {{cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w}};
         const fe ey = {{cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w}};
         const f29 x2 = f29_from_mont256(ex), y2 = f29_from_mont256(ey);
         jp29 sum = acc;
-        p29_add_aff_lean(sum, x2, y2);
+        if (SBFT_KEYED_LANES_ILP) p29_add_aff_lean_ilp(sum, x2, y2);
+        else p29_add_aff_lean(sum, x2, y2);
         if (!zero) {
             if (inf) {
                 acc.x = x2;
@@ -2179,11 +2211,73 @@ __global__ __launch_bounds__(FRAMED ? 320 : 256) void p256_verify_keyed_lanes_ke
             }
             inf = false;
         }
+    };
+    probe(2);
+    if (SBFT_KEYED_LANES_PINGPONG) {
+        // 16 entries in two fixed buffers, the loop unrolled by two: each entry's loads are issued
+        // one addition before it is used and never waited on to move registers (the rotated
+        // buffer of the form below waited on them at every iteration, as did the digit's scratch
+        // load queued behind them). The lane's 16 scalar bytes (windows w0 .. w0 + 15: words
+        // 4 (j & 1) .. + 3 of u) are shifted out of registers, and the table is read with global
+        // (not flat) loads.
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef const __attribute__((address_space(1))) uint4 gu4;
+#else
+        typedef const uint4 gu4;  // the kernel body's host pass (HIP_vector_type has no such overload)
+#endif
+        gu4* const gtab = (gu4*)tab;
+        u32 ub[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ub[k] = (j & 1u) ? u.v[4 + k] : u.v[k];
+        uint4 ea[4], eb[4];
+        auto entry = [&](u32 i, u32 byte, uint4 (&en)[4]) {
+            gu4* p = gtab + (size_t)((w0 + i) * COMB_ENTRIES + byte) * COMB_ENTRY_U4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) en[k] = p[k];
+            __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk towards their use
+        };
+        entry(0, ub[0] & 255u, ea);
+#pragma unroll 1
+        for (u32 i = 0; i < 16; i += 2) {
+            const u32 b0 = ub[0] & 255u, b1 = (ub[0] >> 8) & 255u;
+            entry(i + 1, b1, eb);
+            add_entry(ea, b0 == 0);
+            // unconditional (the last pass reloads entry 15, unused): a load behind a branch
+            // made the wait below it count every load in flight
+            const bool more = i + 2 < 16;
+            entry(more ? i + 2 : i + 1, more ? (ub[0] >> 16) & 255u : b1, ea);
+            add_entry(eb, b1 == 0);
+            ub[0] = __builtin_amdgcn_alignbit(ub[1], ub[0], 16);
+            ub[1] = __builtin_amdgcn_alignbit(ub[2], ub[1], 16);
+            ub[2] = __builtin_amdgcn_alignbit(ub[3], ub[2], 16);
+            ub[3] >>= 16;
+        }
+    } else {
+        // 16 entries, the next one's loads issued before the current addition
+        uint4 cur[4], nxt[4];
+        auto entry = [&](u32 i, uint4 (&en)[4]) {
+            const u32 win = w0 + i;
+            const uint4* p = tab + (size_t)(win * COMB_ENTRIES + byte_of(u, win)) * COMB_ENTRY_U4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) en[k] = p[k];
+        };
+        entry(0, nxt);
+#pragma unroll 1
+        for (u32 i = 0; i < 16; ++i) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+            if (i < 15) entry(i + 1, nxt);
+            add_entry(cur, byte_of(u, w0 + i) == 0);
+        }
     }
+    probe(3);
     quad_combine<0xB1>(acc, inf);  // quad_perm [1,0,3,2]: u1 G on lanes 0-1, u2 Q on lanes 2-3
     quad_combine<0x4E>(acc, inf);  // quad_perm [2,3,0,1]: R on every lane
+    probe(4);
     bool exc = false;
     bool accept = verify_final(acc, r, exc) && !inf;
+    probe(5);
+    probe_dump("verify");
     exc = exc && !inf;
     if (__builtin_expect(__any(exc), 0)) {  // rare: the exact recomputation on the quad's lane 0
         fe u1v, u2v;  // every lane of the quad gets both scalars (DPP before the branch)
@@ -2341,9 +2435,11 @@ extern "C" int sbft_launch_p256_verify_keyed_framed(const uint8_t* d_blob, const
                                                     uint32_t n, hipStream_t stream) {
     if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
-    const unsigned kblocks = (unsigned)((n + 63) / 64);  // 64 signatures per workgroup
+    constexpr unsigned tpb = SBFT_KEYED_FRAMED_TPB;  // signatures per workgroup
+    static_assert(tpb % 16 == 0 && tpb <= 64, "whole verify wavefronts, one hash wavefront");
+    const unsigned kblocks = (unsigned)((n + tpb - 1) / tpb);
     const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
-    hipLaunchKernelGGL(sbft::p256_verify_keyed_lanes_kernel<true>, dim3(kblocks), dim3(320), 0, stream, nullptr,
+    hipLaunchKernelGGL(sbft::p256_verify_keyed_lanes_kernel<true>, dim3(kblocks), dim3(4 * tpb + 64), 0, stream, nullptr,
                        nullptr, nullptr, d_key, (const uint4* const*)d_keytab, nkeys, d_ok, n, fr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
