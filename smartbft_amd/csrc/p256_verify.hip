@@ -877,6 +877,9 @@ SBFT_DEV int q_digit(const fe& k2, int i) {
 // index makes k2 an alloca, which LLVM promotes to LDS (8 KB of the half kernel's workgroup, read
 // back every digit); its absence measured 13 us less per 10k-tuple launch (profiles/
 // r05ad_nolds_ab.txt: the table build ends ~10 us earlier). 16 selects per digit.
+#ifndef SBFT_HALF_ENTRY_EARLY
+#define SBFT_HALF_ENTRY_EARLY 1  // the half kernel's ladder reads a digit's entry before its doublings
+#endif
 #ifndef SBFT_PAIR_DIGIT_SEL
 #define SBFT_PAIR_DIGIT_SEL 1  // the pair kernel's digits by selects as well
 #endif
@@ -1876,10 +1879,24 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     }
 #pragma unroll 1
     for (int i = L - 1; i >= 1; --i) {
+        f29 x2, y2;
+        bool ng = false;
+        if (SBFT_HALF_ENTRY_EARLY) {
+            // the digit's LDS reads issued before the doublings (pinned there), its sign applied
+            // after them: read after the doublings, each digit waited on LDS latency
+            const int d = SBFT_HALF_DIGIT_SEL ? q_digit_sel(k, i) : q_digit(k, i);
+            tab_entry((d < 0 ? -d : d) >> 1, x2, y2);
+            ng = (d < 0) != negb;
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int d = 0; d < kQWin; ++d) p29_dbl_plw(q);
-        f29 x2, y2;
-        qentry(i, x2, y2);
+        if (SBFT_HALF_ENTRY_EARLY) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) y2.v[t] = ng ? 0u - y2.v[t] : y2.v[t];
+        } else {
+            qentry(i, x2, y2);
+        }
         p29_add_aff_plw(q, x2, y2);
     }
 #pragma unroll

@@ -12,6 +12,6 @@ gv = GpuVerifier(device_mask=1)
 reqs = make_signed_requests(gv, 10_000, start=4242)
 v = plugin.Verifier(gv, 0)
 p = plugin.Proposal(plugin.encode_payload(reqs), b"h", b"m", 0)
-for _ in range(4):
+for _ in range(int(os.environ.get("HALF_PROBE_CALLS", "4"))):  # more for a rocprofv3 average
     assert len(v.VerifyProposal(p)) == len(reqs)
 sys.stdout.flush()
