@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 evidence on the final build (+ the registered-client keyed kernel's ping-pong comb, 48 per workgroup): the whole GPU suite, smoke, the default bench line,
+# Round-5 evidence on the final build (+ the registered-client keyed kernel's ping-pong comb, 48 per workgroup; the half kernel's entries read before the doublings): the whole GPU suite, smoke, the default bench line,
 # rocprofv3 kernel-trace stats over 20 timed steps (tools/trace_summary.py compares the same
 # dispatches with the bench's HIP events), the PMC passes (separate runs, counters within the
 # per-block limits), and kernel stats of the latency path (configs 3/4).
