@@ -2101,6 +2101,9 @@ SBFT_DEV void quad_combine(jp29& acc, bool& inf) {
 // FRAMED: signatures per workgroup (a multiple of 16). 48: three verify wavefronts and the hash
 // wavefront, one per SIMD, so the hash (the comb's wait for its digests) does not share a SIMD
 // with an inverting wavefront; 64: four verify wavefronts and the hash wavefront on five.
+#ifndef SBFT_KEYED_LANES_ZPRE
+#define SBFT_KEYED_LANES_ZPRE 1  // the comb's next Z^2, Z^3 formed inside the current addition
+#endif
 #ifndef SBFT_KEYED_FRAMED_TPB
 #define SBFT_KEYED_FRAMED_TPB 48
 #endif
@@ -2247,6 +2250,53 @@ __global__ __launch_bounds__(FRAMED ? 4 * SBFT_KEYED_FRAMED_TPB + 64 : 256) void
 #pragma unroll
         for (int k = 0; k < 4; ++k) ub[k] = (j & 1u) ? u.v[4 + k] : u.v[k];
         uint4 ea[4], eb[4];
+        // SBFT_KEYED_LANES_ZPRE: the next accumulator's Z^2 and Z^3 are formed inside the current
+        // addition, beside its X3 and Y3 products (whose Montgomery passes were single-product
+        // stages with their serial chains exposed); the values are the same as forming them at the
+        // start of the next addition.
+        const f29 one29 = f29_const(C29_ONE);
+        f29 zz = one29, zzz = one29;  // acc.z^2, acc.z^3 (acc starts at infinity with Z = 1)
+        auto add_entry_zz = [&](const uint4 (&cur)[4], bool zero) {
+            const fe ex = {{cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w}};
+            const fe ey = {{cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w}};
+            const f29 x2 = f29_from_mont256(ex), y2 = f29_from_mont256(ey);
+            f29 u2, s2, h, rr, hh, hhh, v, z3, x3, y3, t, nd, zn, zz2, zzz2;
+            f29_mul_ilp(u2, x2, zz);
+            f29_mul_ilp(s2, y2, zzz);         // S2 = y2 Z1^3
+            f29_sub(h, u2, acc.x);            // (-2^29.2, 2^29 + 2^25)
+            f29_sub(rr, s2, acc.y);           // (-2^29.2, 2^29.2)
+            f29_sqr_ilp(hh, h);
+            f29_mul_ilp(hhh, hh, h);
+            f29_mul_ilp(v, acc.x, hh);        // V = X1 H^2
+            f29_mul_ilp(z3, acc.z, h);        // Z3 = Z1 H
+#pragma unroll
+            for (int k = 0; k < 9; ++k) zn.v[k] = zero ? acc.z.v[k] : (inf ? one29.v[k] : z3.v[k]);
+            {
+                const f29* const va[2] = {&hhh, &v};
+                const u32 c[2] = {(u32)-1, (u32)-2};
+                f29_mulsq_add_ilp<true, 2>(x3, rr, rr, va, c, ~0u);  // X3 = r^2 - HHH - 2V: N'
+            }
+            f29_sqr_ilp(zz2, zn);             // the next addition's Z1^2 ...
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                t.v[k] = v.v[k] - x3.v[k];    // (-2^29.2, 2^29 + 2^25)
+                nd.v[k] = 0u - hhh.v[k];
+            }
+            f29_mul_sub_ilp(y3, rr, t, acc.y, nd);  // r t - Y1 H^3: N
+            f29_mul_ilp(zzz2, zn, zz2);       // ... and Z1^3
+            if (!zero) {
+                acc.x = inf ? x2 : x3;
+                acc.y = inf ? y2 : y3;
+                inf = false;
+            }
+            acc.z = zn;
+            zz = zz2;
+            zzz = zzz2;
+        };
+        auto add_pp = [&](const uint4 (&cur)[4], bool zero) {
+            if (SBFT_KEYED_LANES_ZPRE) add_entry_zz(cur, zero);
+            else add_entry(cur, zero);
+        };
         auto entry = [&](u32 i, u32 byte, uint4 (&en)[4]) {
             gu4* p = gtab + (size_t)((w0 + i) * COMB_ENTRIES + byte) * COMB_ENTRY_U4;
 #pragma unroll
@@ -2258,12 +2308,12 @@ __global__ __launch_bounds__(FRAMED ? 4 * SBFT_KEYED_FRAMED_TPB + 64 : 256) void
         for (u32 i = 0; i < 16; i += 2) {
             const u32 b0 = ub[0] & 255u, b1 = (ub[0] >> 8) & 255u;
             entry(i + 1, b1, eb);
-            add_entry(ea, b0 == 0);
+            add_pp(ea, b0 == 0);
             // unconditional (the last pass reloads entry 15, unused): a load behind a branch
             // made the wait below it count every load in flight
             const bool more = i + 2 < 16;
             entry(more ? i + 2 : i + 1, more ? (ub[0] >> 16) & 255u : b1, ea);
-            add_entry(eb, b1 == 0);
+            add_pp(eb, b1 == 0);
             ub[0] = __builtin_amdgcn_alignbit(ub[1], ub[0], 16);
             ub[1] = __builtin_amdgcn_alignbit(ub[2], ub[1], 16);
             ub[2] = __builtin_amdgcn_alignbit(ub[3], ub[2], 16);
