@@ -51,7 +51,8 @@ typedef struct sbft_gv_ctx sbft_gv_ctx;
 
 typedef struct sbft_gv_opts {
     uint32_t device_mask;   /* bit d selects HIP device d; 0 = all visible devices */
-    uint32_t min_split;     /* batches smaller than this stay on one device (0 = default 65536) */
+    uint32_t min_split;     /* batches smaller than this stay on one device (0 = default: 65536, or
+                               halfq_max + 1 when the wide half kernel is on) */
     int32_t pair_max;       /* per-device batches of at most this many tuples run the latency kernel
                                (two lanes per tuple); 0 = default SBFT_GV_PAIR_MAX_DEFAULT, < 0 = never
                                (and then no latency kernel at all unless half_max is set explicitly:
@@ -77,7 +78,15 @@ typedef struct sbft_gv_opts {
                                     budget stay unregistered (their requests take the generic
                                     launch, same verdicts), so client registration can never
                                     use the memory the verify paths stage in. */
-    uint64_t reserved[1];
+    int32_t halfq_max;      /* per-device batches of at most this many tuples run the wide form of the
+                               half-size-scalar kernel (eight lanes per tuple: each 128-bit ladder on a
+                               quad, 15 steps per 4-bit digit instead of 21; checked before half_max),
+                               sized so that its workgroups fit one per CU; 0 = default, 24 x the
+                               device's CUs (6,144 on an MI355X), < 0 = never. The environment variable
+                               SBFT_GV_HALFQ_MAX overrides it. With more than one slot and the default
+                               min_split, a batch larger than this is split, so that each share runs
+                               the wide kernel (a 10k proposal over 2-8 GPUs). */
+    int32_t reserved1;      /* must be 0 */
 } sbft_gv_opts;
 
 #define SBFT_GV_PAIR_MAX_DEFAULT 32768u
@@ -114,13 +123,15 @@ int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* 
                         const uint8_t* qx, const uint8_t* qy, size_t n, uint8_t* ok_out);
 /* sbft_gv_verify_p256 on a named kernel instead of the one the batch size selects (tests and
  * diagnostics; same verdicts whichever kernel runs): SBFT_GV_KERNEL_THROUGHPUT (one lane per
- * tuple), _PAIR (two lanes), _HALF (half-size scalars, four lanes), or _EXACT: every tuple
+ * tuple), _PAIR (two lanes), _HALF (half-size scalars, four lanes), _HALF_WIDE (half-size
+ * scalars, eight lanes: a quad per ladder), or _EXACT: every tuple
  * through the exact case-split kernel alone -- the net the others hand flagged tuples to
  * (Booth digits, explicit infinity and doubling branches; slow, one lane per tuple). */
 #define SBFT_GV_KERNEL_EXACT 0
 #define SBFT_GV_KERNEL_THROUGHPUT 1
 #define SBFT_GV_KERNEL_PAIR 2
 #define SBFT_GV_KERNEL_HALF 3
+#define SBFT_GV_KERNEL_HALF_WIDE 4
 int sbft_gv_verify_p256_kernel(sbft_gv_ctx* ctx, int kernel, const uint8_t* digest, const uint8_t* r,
                                const uint8_t* s, const uint8_t* qx, const uint8_t* qy, size_t n, uint8_t* ok_out);
 

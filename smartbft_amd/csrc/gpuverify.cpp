@@ -517,10 +517,11 @@ struct sbft_gv_ctx {
     // kernel; 0 = never (sbft_gv_opts.pair_max)
     uint32_t pair_max = SBFT_GV_PAIR_MAX_DEFAULT;
     uint32_t half_max = SBFT_GV_HALF_MAX_DEFAULT;  // ... half-size scalars (sbft_gv_opts.half_max)
+    uint32_t halfq_max = 0;  // ... their wide form (sbft_gv_opts.halfq_max; set by sbft_gv_init)
     std::atomic<uint32_t> rr{0};
-    // verify kernel for a per-device batch of n: 3 = half-size scalars (four lanes per tuple),
-    // 2 = pair kernel, 1 = throughput kernel
-    int lanes_for(size_t n) const { return n <= half_max ? 3 : n <= pair_max ? 2 : 1; }
+    // verify kernel for a per-device batch of n: 4 = half-size scalars on quads (eight lanes per
+    // tuple), 3 = half-size scalars (four lanes), 2 = pair kernel, 1 = throughput kernel
+    int lanes_for(size_t n) const { return n <= halfq_max ? 4 : n <= half_max ? 3 : n <= pair_max ? 2 : 1; }
     // keyed batches (per device) of at most this many signatures take the zero-copy path
     // (enqueue_keyed); SBFT_KEYED_ZC_MAX overrides (0 = never)
     size_t keyed_zc_max = 1024;
@@ -603,7 +604,7 @@ static int power_on_selftest(Slot* sl) {
     // every verify kernel on the same workspace, back to back, the exact fixup net last (0): it
     // serves the others' flagged tuples, and in rounds 4-5 it had faulted unseen because nothing
     // reached it
-    for (int lanes : {1, 2, 3, 0}) {
+    for (int lanes : {1, 2, 3, 4, 0}) {
         cur = lanes;
         POSTCHK(hipMemsetAsync(base + 5 * f, 0xEE, n, sl->stream), "verdict memset");
         if (sbft_launch_p256_verify(base, base + f, base + 2 * f, base + 3 * f, base + 4 * f, base + 5 * f, (uint32_t)n,
@@ -677,7 +678,10 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
     const uint32_t mask = (opts && opts->device_mask) ? opts->device_mask : 0xffffffffu;
     auto* ctx = new (std::nothrow) sbft_gv_ctx();
     if (!ctx) return SBFT_GV_ENOMEM;
-    if (opts && opts->min_split) ctx->min_split = opts->min_split;
+    if (opts && (opts->reserved0 || opts->reserved1)) {  // reserved fields must be 0 (a retired field's
+        delete ctx;                                      // old meaning is never read as a new one)
+        return SBFT_GV_EINVAL;
+    }
     if (opts && opts->pair_max) ctx->pair_max = opts->pair_max < 0 ? 0u : (uint32_t)opts->pair_max;
     // pair_max < 0 means "no latency kernel": the half kernel too, unless half_max asks for it
     if (opts && opts->pair_max < 0 && !opts->half_max) ctx->half_max = 0;
@@ -686,6 +690,24 @@ int sbft_gv_init(const sbft_gv_opts* opts, sbft_gv_ctx** out) {
         const long v = strtol(e, nullptr, 10);
         ctx->half_max = v < 0 ? 0u : (uint32_t)v;
     }
+    {
+        // the wide half kernel: one 24-tuple workgroup per CU of the first selected device (its
+        // three verify wavefronts and the helper on the CU's four SIMDs); off with the half kernel
+        int dev0 = 0, cus = 0;
+        while (dev0 < ndev && !(mask & (1u << dev0))) ++dev0;
+        if (dev0 >= ndev || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev0) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        ctx->halfq_max = ctx->half_max ? 24u * (uint32_t)cus : 0u;
+        if (opts && opts->halfq_max) ctx->halfq_max = opts->halfq_max < 0 ? 0u : (uint32_t)opts->halfq_max;
+        if (const char* e = getenv("SBFT_GV_HALFQ_MAX")) {
+            const long v = strtol(e, nullptr, 10);
+            ctx->halfq_max = v < 0 ? 0u : (uint32_t)v;
+        }
+    }
+    // min_split: a batch the wide kernel cannot take whole is split when there are devices to
+    // split it over (a 10k proposal over 2-8 GPUs: shares of <= halfq_max, each on the wide kernel)
+    ctx->min_split = opts && opts->min_split ? opts->min_split : ctx->halfq_max ? ctx->halfq_max + 1 : 65536u;
     if (opts) ctx->client_cap = opts->client_table_bytes;
     if (const char* e = getenv("SBFT_GV_CLIENT_TABLE_BYTES")) ctx->client_cap = strtoull(e, nullptr, 10);
     if (const char* e = getenv("SBFT_KEYED_ZC_MAX")) ctx->keyed_zc_max = (size_t)strtoull(e, nullptr, 10);
@@ -1407,7 +1429,7 @@ int sbft_gv_verify_p256(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* 
 
 int sbft_gv_verify_p256_kernel(sbft_gv_ctx* ctx, int kernel, const uint8_t* digest, const uint8_t* r,
                                const uint8_t* s, const uint8_t* qx, const uint8_t* qy, size_t n, uint8_t* ok_out) {
-    if (!ctx || kernel < SBFT_GV_KERNEL_EXACT || kernel > SBFT_GV_KERNEL_HALF) return SBFT_GV_EINVAL;
+    if (!ctx || kernel < SBFT_GV_KERNEL_EXACT || kernel > SBFT_GV_KERNEL_HALF_WIDE) return SBFT_GV_EINVAL;
     if (n == 0) return SBFT_GV_OK;
     if (!digest || !r || !s || !qx || !qy || !ok_out || n > 0xffffffffu) return SBFT_GV_EINVAL;
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) {
@@ -1440,7 +1462,7 @@ int sbft_gv_selftest_field(sbft_gv_ctx* ctx, int op, const uint8_t* a, const uin
                            uint8_t* out) {
     if (!ctx) return SBFT_GV_EINVAL;
     if (n == 0) return SBFT_GV_OK;
-    if (!a || !b || !out || op < 0 || op > 26 || n > 0xffffffffu) return SBFT_GV_EINVAL;
+    if (!a || !b || !out || op < 0 || op > 30 || n > 0xffffffffu) return SBFT_GV_EINVAL;
     return run_chunks(ctx, n, [&](const Chunk& c, size_t) { return enqueue_selftest(c, op, a, b, out); });
 }
 

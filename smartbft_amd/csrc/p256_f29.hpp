@@ -1489,6 +1489,180 @@ SBFT_DEV void plw29_to(jp29& p, const plw29& q) {
     p.z = f29_bcast_pair(q.zy, false);
 }
 
+// ---------------------------------------------------------------- quads, W = c Z^2 carried
+// The half kernel's wide form (p256_verify_half_kernel<FRAMED, true>: per-device shares of at
+// most one workgroup per CU, e.g. a 10k proposal split over 2-8 GPUs) runs each 128-bit ladder on
+// the four lanes of a quad instead of a pair. A step is still one product per lane in one
+// instruction stream, so a step now carries four products. The doubling's depth is 3 (the Y
+// chain: g = Y^2, then b and L, then Y3), the mixed addition's is 4, and its first step rides on
+// the spare lanes of the doubling in front of it:
+//   doubling:  1: a' = (X - W)(X + W) | g = Y^2 | Z3 = Y Z | (Y^2, unused)
+//              2: h^2 | L = g^2 | b = X g | W3 = W g                 (h = 3a'/2, halved representative)
+//              3: Y3 = h (3b - h^2) - L | X3 = h^2 - 2b [| U2 = x2'' W3 | T = Z3 W3]
+//   addition:  2: - | HH = H^2 | Z3 = Z1 H | S2 = y2'' T              (H = U2 - X1)
+//              3: V = X1 HH | HHH = H HH | W3 = W HH | r^2          (r = S2 - Y1)
+//              4: r (V - X3) | Y1 HHH                                (X3 = r^2 - HHH - 2V: limb ops)
+// (Y3 = h (b - X3) - L with b - X3 = 3b - h^2, so Y3 and X3 come out of the same step.) A 4-bit
+// digit is 4 x 3 + 3 = 15 steps instead of the pair's 21. Every product is one the pair forms
+// compute, with the same operand contracts except 3b - h^2 (limbs in (-2^29, 3 2^29): 9 column
+// terms < 2^62.75, with the reduction terms < 2^62.8); tests/test_f29_bounds.py (dbl_q4,
+// add_aff_q4) checks every column, limb and contract, W = c Z^2 and X / W = x(k R0).
+// Lanes and registers (a value "@j" lives on lane j of its register):
+//   doubling:  1: [a', g, Z3, a']       2: [h^2, L, W3, b]      3: [Y3, (U2), (T), X3]
+//   addition:  2: [HH, HH, Z3, S2]      3: [V, HHH, W3, r^2]    4: [r (V - X3), Y1 HHH]
+// a' runs on lanes 0 and 3, so h is on both lanes of step 3 without a move; the state is
+// xy = [X, Y, Y, X] (one DPP of step 3's output), z = Z@2, w = W@2 (step 2's output) and
+// wm = [W, 0, 0, W], so step 1's operands are xy - wm | xy + wm (lane 2: z) with one select.
+// In: X in N', Y in N' or N+-, Z, W in N. Out: X3 in N', Y3 in N' (doubling) or N+- (addition),
+// Z3, W3 in N.
+struct q4w {
+    f29 xy, z, w, wm;
+};
+constexpr u64 kQL0 = 0x1111111111111111ull, kQL1 = 0x2222222222222222ull, kQL2 = 0x4444444444444444ull,
+              kQL3 = 0x8888888888888888ull;
+template <u64 M>
+SBFT_DEV u32 qsel(u32 a, u32 b) {  // b on the quad lanes of M, a elsewhere (one v_cndmask, as sel_pair)
+    u32 r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(M));
+    return r;
+}
+template <u64 M>
+SBFT_DEV f29 f29_qsel(const f29& a, const f29& b) {
+    f29 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = qsel<M>(a.v[i], b.v[i]);
+    return r;
+}
+template <int CTRL>
+SBFT_DEV f29 f29_qperm(const f29& a) {  // quad_perm DPP: lane j gets lane ((CTRL >> 2j) & 3)'s limbs
+    f29 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = (u32)__builtin_amdgcn_update_dpp(0, (int)a.v[i], CTRL, 0xF, 0xF, true);
+    return r;
+}
+// b on the quad lanes of M, quad_perm CTRL of a elsewhere: one v_cndmask_b32_dpp per limb (the DPP
+// applies to the select's src0), so a move and a select cost one instruction. The mask goes to VCC
+// in the block; s_nop 1 covers the DPP read of a VGPR the instruction in front may have written.
+template <u64 M, int CTRL>
+SBFT_DEV f29 f29_qselp(const f29& a, const f29& b) {
+    f29 r;
+#define SBFT_QP "quad_perm:[%10,%11,%12,%13] row_mask:0xf bank_mask:0xf\n"
+    asm("s_mov_b64 vcc, %9\n"
+        "s_nop 1\n"
+        "v_cndmask_b32_dpp %0, %14, %23, vcc " SBFT_QP
+        "v_cndmask_b32_dpp %1, %15, %24, vcc " SBFT_QP
+        "v_cndmask_b32_dpp %2, %16, %25, vcc " SBFT_QP
+        "v_cndmask_b32_dpp %3, %17, %26, vcc " SBFT_QP
+        "v_cndmask_b32_dpp %4, %18, %27, vcc " SBFT_QP
+        "v_cndmask_b32_dpp %5, %19, %28, vcc " SBFT_QP
+        "v_cndmask_b32_dpp %6, %20, %29, vcc " SBFT_QP
+        "v_cndmask_b32_dpp %7, %21, %30, vcc " SBFT_QP
+        "v_cndmask_b32_dpp %8, %22, %31, vcc " SBFT_QP
+        : "=&v"(r.v[0]), "=&v"(r.v[1]), "=&v"(r.v[2]), "=&v"(r.v[3]), "=&v"(r.v[4]), "=&v"(r.v[5]), "=&v"(r.v[6]),
+          "=&v"(r.v[7]), "=&v"(r.v[8])
+        : "s"(M), "n"(CTRL & 3), "n"((CTRL >> 2) & 3), "n"((CTRL >> 4) & 3), "n"((CTRL >> 6) & 3), "v"(a.v[0]),
+          "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]), "v"(a.v[6]), "v"(a.v[7]), "v"(a.v[8]),
+          "v"(b.v[0]), "v"(b.v[1]), "v"(b.v[2]), "v"(b.v[3]), "v"(b.v[4]), "v"(b.v[5]), "v"(b.v[6]), "v"(b.v[7]),
+          "v"(b.v[8])
+        : "vcc");
+#undef SBFT_QP
+    return r;
+}
+SBFT_DEV void q4w_set_w(q4w& P, const f29& w2) {  // W from lane 2 of w2
+    P.w = w2;
+    P.wm = f29_qselp<kQL1 | kQL2, 0xAA>(w2, f29{});
+}
+// The ladder's start: (x, y) on the curve (or E_c), Z = 1, W = c (every lane).
+SBFT_DEV void q4w_init(q4w& P, const f29& x, const f29& y, const f29& one, const f29& c) {
+    P.xy = f29_qsel<kQL1 | kQL2>(x, y);
+    P.z = one;
+    q4w_set_w(P, c);
+}
+// ADD: the next mixed addition's first step on lanes 1-2 of step 3 (U2 = x2 W3 | T = Z3 W3, in ut)
+template <bool ADD>
+SBFT_DEV void q4_dbl(q4w& P, const f29& x2, f29& ut) {
+    f29 a, b, o1, h, o2, o3;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        a.v[i] = P.xy.v[i] - P.wm.v[i];                                  // X - W: |.| < 2^29.2 | Y | Y | X - W
+        b.v[i] = qsel<kQL2>(P.xy.v[i] + P.wm.v[i], P.z.v[i]);            // X + W < 2^30.1 | Y | Z | X + W
+    }
+    f29_mul_ilp(o1, a, b);                   // a' | g | Z3 | a'
+    f29_triple_half(h, o1);                  // h = 3a'/2 (lanes 0, 3; limbs < 2^29 + 3)
+    b = f29_qselp<kQL0, 0x54>(o1, h);        // h | g | g | g (quad_perm [0,1,1,1])
+#pragma unroll
+    for (int i = 0; i < 9; ++i) a.v[i] = qsel<kQL2 | kQL3>(b.v[i], qsel<kQL3>(P.w.v[i], P.xy.v[i]));  // h | g | W | X
+    f29_mul_ilp(o2, a, b);                   // h^2 | L | W3 | b
+    const f29 bq = f29_qperm<0xFF>(o2);      // b (lane 0)
+    const f29 v = f29_qperm<0xF5>(o2);       // quad_perm [1,1,3,3]: L (lane 0) | b (lane 3)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const u32 t = bq.v[i] * 3u - o2.v[i];  // 3b - h^2 (lane 0): (-2^29, 3 2^29)
+        b.v[i] = qsel<kQL3>(t, h.v[i]);        // 3b - h^2 | - | - | h
+        a.v[i] = ADD ? qsel<kQL1>(qsel<kQL2>(h.v[i], o1.v[i]), x2.v[i]) : h.v[i];  // h | x2 | Z3 | h
+    }
+    if (ADD) b = f29_qselp<kQL0 | kQL3, 0xAA>(o2, b);  // 3b - h^2 | W3 | W3 | h
+    {
+        const f29* const vv[1] = {&v};
+        const u32 c[1] = {qsel<kQL3>(qsel<kQL0>(0u, (u32)-1), (u32)-2)};
+        f29_mulsq_add_ilp<false, 1>(o3, a, b, vv, c, qsel<kQL0 | kQL3>(0u, ~0u));  // Y3 | (U2 | T: N) | X3: N'
+    }
+    P.xy = f29_qperm<0xC3>(o3);  // quad_perm [3,0,0,3]: X3 | Y3 | Y3 | X3
+    P.z = o1;                    // Z3 (lane 2)
+    q4w_set_w(P, o2);            // W3 (lane 2)
+    if (ADD) ut = o3;
+}
+// The mixed addition's steps 2-4 after q4_dbl<true> (ut = U2 | T on lanes 1 | 2), the entry
+// (x2'', y2'') divided by c on every lane (y2'' N+- when negated). Y1 must be N' (a doubling's).
+SBFT_DEV void q4_add_rest(q4w& P, const f29& y2, const f29& ut) {
+    f29 h, a, b, o2, r, o3, t, x3, o4, y3;
+    const f29 u = f29_qperm<0x95>(ut);    // quad_perm [1,1,1,2]: U2 | U2 | U2 | T
+    const f29 xb = f29_qperm<0x00>(P.xy); // X1
+    const f29 yb = f29_qperm<0x55>(P.xy); // Y1
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        h.v[i] = u.v[i] - xb.v[i];                                    // H = U2 - X1: (-2^29.2, 2^29 + 2^26)
+        a.v[i] = qsel<kQL2>(qsel<kQL3>(h.v[i], y2.v[i]), P.z.v[i]);  // H | H | Z1 | y2
+        b.v[i] = qsel<kQL3>(h.v[i], u.v[i]);                          // H | H | H | T
+    }
+    f29_mul_ilp(o2, a, b);                // HH | HH | Z3 | S2
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        r.v[i] = o2.v[i] - yb.v[i];  // r = S2 - Y1 (lane 3): |.| < 2^29.2
+        a.v[i] = qsel<kQL1>(qsel<kQL2>(qsel<kQL3>(xb.v[i], r.v[i]), P.w.v[i]), h.v[i]);  // X1 | H | W | r
+    }
+    b = f29_qselp<kQL3, 0x00>(o2, r);     // HH | HH | HH | r
+    f29_mul_ilp(o3, a, b);                // V | HHH | W3 | r^2
+    const f29 vb = f29_qperm<0x00>(o3), hhh = f29_qperm<0x55>(o3), r2 = f29_qperm<0xFF>(o3);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] = r2.v[i] - hhh.v[i] - (vb.v[i] << 1);  // r^2 - HHH - 2V: (-3 2^29, 2^29)
+    f29_normalize(x3, t);                 // X3 (N')
+    a = f29_qselp<kQL1, 0xFF>(r, yb);     // r | Y1
+#pragma unroll
+    for (int i = 0; i < 9; ++i) b.v[i] = qsel<kQL1>(vb.v[i] - x3.v[i], hhh.v[i]);  // V - X3: (-2^29.2, 2^29 + 2^26) | HHH
+    f29_mul_ilp(o4, a, b);                // r (V - X3) | Y1 HHH
+    const f29 p0 = f29_qperm<0x00>(o4), p1 = f29_qperm<0x55>(o4);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) y3.v[i] = p0.v[i] - p1.v[i];  // Y3 (N+-)
+    P.xy = f29_qsel<kQL1 | kQL2>(x3, y3);
+    P.z = o2;  // Z3 (lane 2)
+    q4w_set_w(P, o3);  // W3 (lane 2)
+}
+// A whole mixed addition (its first step on its own): Y1 brought to N' first, so any state qualifies.
+SBFT_DEV void q4_add_full(q4w& P, const f29& x2, const f29& y2) {
+    f29 ut;
+    f29_normalize(P.xy, P.xy);
+    f29_mul_ilp(ut, f29_qsel<kQL2>(x2, P.z), f29_qperm<0xAA>(P.w));  // U2 (lane 1) | T (lane 2)
+    q4_add_rest(P, y2, ut);
+}
+// Jacobian (X, Y, Z) on every lane of the quad; Y in N'.
+SBFT_DEV void q4w_to(jp29& p, const q4w& q) {
+    p.x = f29_qperm<0x00>(q.xy);
+    f29_normalize(p.y, f29_qperm<0x55>(q.xy));
+    p.z = f29_qperm<0xAA>(q.z);
+}
+SBFT_DEV f29 q4w_w(const q4w& q) { return f29_qperm<0xAA>(q.w); }  // W on every lane
+
 // ---------------------------------------------------------------- co-Z table building
 // Odd multiples [1, 3, ..., 2^w - 1]Q with Meloni's co-Z additions (2007): every point of the
 // chain shares the Z of the running 2Q, so an addition costs 4M + 2S and only the Z ratios

@@ -141,12 +141,43 @@ SBFT_DEV fe selftest_pair(int op, const fe& x, const fe& y, const uint32_t* dtab
     return op == 25 ? ox : oy;
 }
 
+// Ops 27..30 run on quads (4t .. 4t + 3), every lane on element 4t's inputs, as the wide half
+// kernel's ladders do (q4_dbl / q4_add_rest / q4_add_full, c = 1: W = Z^2): 27 / 28 x / y of 33P
+// (four doublings, a fifth carrying the addition's first step, the addition's rest with P itself);
+// 29 / 30 x / y of 32P = 33P + (-P) (then a whole addition of -P, from the N+- Y of the first).
+SBFT_DEV fe selftest_quad(int op, const fe& x, const fe& y, const uint32_t* dtab) {
+    const f29 px = to_mont29(x), py = to_mont29(y), one = f29_const(C29_ONE);
+    q4w q;
+    q4w_init(q, px, py, one, one);
+    f29 ut;
+    for (int k = 0; k < 4; ++k) q4_dbl<false>(q, px, ut);
+    q4_dbl<true>(q, px, ut);
+    q4_add_rest(q, py, ut);
+    if (op >= 29) {
+        f29 ny;
+        f29_neg(ny, py);
+        q4_add_full(q, px, ny);
+    }
+    jp29 t;
+    q4w_to(t, q);
+    fe ox, oy;
+    affine29(t, ox, oy, dtab);
+    return (op & 1) ? ox : oy;
+}
+
 __global__ __launch_bounds__(256) void selftest_kernel(int op, const uint8_t* __restrict__ a,
                                                        const uint8_t* __restrict__ b,
                                                        uint8_t* __restrict__ out, uint32_t n) {
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     if (op == 10 || op >= 13) inv::stage_divstep_table(dtab);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (op >= 27 && op <= 30) {  // quads: no lane leaves before the others of its quad
+        const uint32_t e = ((i & ~3u) < n ? i : n - 1) & ~3u;
+        const fe x = load_be32(a + 32ull * e), y = load_be32(b + 32ull * e);
+        const fe r = selftest_quad(op, x, y, dtab);
+        if (i < n) store_be32(out + 32ull * i, r);
+        return;
+    }
     if (op >= 23 && op <= 26) {  // lane pairs: no lane leaves before its partner
         const uint32_t e = ((i & ~1u) < n ? i : n - 1) & ~1u;
         const fe x = load_be32(a + 32ull * e), y = load_be32(b + 32ull * e);

@@ -1525,8 +1525,15 @@ constexpr int kHalfTuples = SBFT_HALF_TUPLES;  // per workgroup
 #define SBFT_HALF_INV_PAIR 1  // the table's inversion split over the pair (inv::inv_mod_pair)
 #endif
 static_assert(kHalfTuples % 16 == 0 && kHalfTuples <= 64, "16 quads per verify wavefront, one helper wavefront");
+// The wide form (QUAD): each ladder on a quad of its own (q4_dbl / q4_add_rest, p256_f29.hpp), eight
+// lanes per tuple, 24 tuples per workgroup: three verify wavefronts and the helper, as before. It
+// takes per-device batches of at most one workgroup per CU (sbft_gv_opts.halfq_max), where the
+// 1,024 SIMDs have room for the extra wavefronts.
+constexpr int kHalfTuplesQ = 24;
+static_assert(kHalfTuplesQ % 8 == 0 && kHalfTuplesQ <= 64, "8 tuples per verify wavefront, one helper wavefront");
 constexpr int kHalfVerifyThreads = 4 * kHalfTuples;
 constexpr int kHalfThreads = kHalfVerifyThreads + 64;
+static_assert(8 * kHalfTuplesQ + 64 == kHalfThreads, "both forms launch 256-thread workgroups");
 constexpr int kHalfDigits = 32;  // radix-16 digits of an odd k < 2^129
 // b 2^261 mod p (radix 2^29) and p - n (8 x 32, < 2^127); tests/test_abi.py checks both
 __device__ __constant__ static const u32 C29_B[9] = {0x1897bbfbu, 0x1cdf6229u, 0x018486c4u, 0x01732821u, 0x1dad59e0u,
@@ -1563,7 +1570,7 @@ SBFT_DEV void f29_sqrt_chain(f29& y, const f29& x) {
     y = t;
 }
 
-template <bool FRAMED>
+template <bool FRAMED, bool QUAD = false>
 __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const uint8_t* __restrict__ digest,
                                                                     const uint8_t* __restrict__ rr,
                                                                     const uint8_t* __restrict__ ss,
@@ -1572,7 +1579,8 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                                                                     uint8_t* __restrict__ ok, uint32_t n,
                                                                     uint32_t* __restrict__ work,
                                                                     const uint4* __restrict__ gcomb, FramedIn fr) {
-    constexpr int T = kHalfTuples;
+    constexpr int T = QUAD ? kHalfTuplesQ : kHalfTuples;
+    constexpr int VT = (QUAD ? 8 : 4) * T;  // verify threads (then the helper wavefront)
     __shared__ __attribute__((aligned(16))) uint32_t dtab[SBFT_DIVSTEP5_WORDS];
     __shared__ u32 qtab[kQTab * 18 * 2 * T];    // [entry][x limbs, y limbs][pair A | pair B][tuple]
     __shared__ u32 hrat[(kQTab - 1) * 9 * 2 * T]; // the table build's Z ratios, [ratio][limb][column]
@@ -1641,8 +1649,8 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         return t;
     };
 
-    if (threadIdx.x >= kHalfVerifyThreads) {  // the helper wavefront (wave-uniform branch)
-        const uint32_t lane = threadIdx.x - kHalfVerifyThreads;
+    if (threadIdx.x >= VT) {  // the helper wavefront (wave-uniform branch)
+        const uint32_t lane = threadIdx.x - VT;
         const bool mine = lane < (uint32_t)T;
         const uint32_t slot = mine ? lane : 0u;
         const uint32_t tc = blockIdx.x * T + slot;
@@ -1758,8 +1766,9 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     }
 
     const int tid = threadIdx.x;
-    const int pr = tid >> 2;                // tuple in the workgroup
-    const int role = (tid >> 1) & 1;        // 0: pair A (w Q), 1: pair B (v R0)
+    const int pr = QUAD ? tid >> 3 : tid >> 2;                // tuple in the workgroup
+    const int role = QUAD ? (tid >> 2) & 1 : (tid >> 1) & 1;  // 0: pair / quad A (w Q), 1: B (v R0)
+    // odd lane of a pair: the table build runs on pairs (QUAD: lanes 2-3 of a quad repeat 0-1)
     const bool odd = (tid & 1) != 0;
     const int col = role * T + pr;          // this pair's column of qtab
     const uint32_t t = blockIdx.x * T + pr;
@@ -1868,60 +1877,110 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         if (!negb) f29_neg(y, y);
     };
     auto dblp = [odd](jp29& p) { p29_dbl_pair(p, p, odd); };
-    plw29 q;  // the top term 16^L (k = 16^L + sum d_i 16^i): the base itself, Z = 1, W = c
-    {
-        f29 y0 = py;
-        if (negb) f29_neg(y0, y0);
-        q.xb = px;
-        q.zy = f29_sel_pair(one29, y0);
-        q.zo = one29;
-        q.w = cc;
-    }
+    // acc: the ladder's end (after digit 0's addition and, for an even k, the base's subtraction),
+    // vw: its W = c Z^2; q (q4): the state before digit 0's addition, where the classic ladders'
+    // exact repairs start
+    jp29 acc;
+    f29 vw;
+    plw29 q;
+    q4w q4;
+    if constexpr (QUAD) {
+        // the top term 16^L: the base itself, Z = 1, W = c
+        {
+            f29 y0 = py;
+            if (negb) f29_neg(y0, y0);
+            q4w_init(q4, px, y0, one29, cc);
+        }
+        f29 ut;
 #pragma unroll 1
-    for (int i = L - 1; i >= 1; --i) {
-        f29 x2, y2;
-        bool ng = false;
-        if (SBFT_HALF_ENTRY_EARLY) {
-            // the digit's LDS reads issued before the doublings (pinned there), its sign applied
-            // after them: read after the doublings, each digit waited on LDS latency
-            const int d = SBFT_HALF_DIGIT_SEL ? q_digit_sel(k, i) : q_digit(k, i);
+        for (int i = L - 1; i >= 1; --i) {
+            f29 x2, y2;
+            // the digit's LDS reads issued before the doublings (x2 enters step 3 of the last)
+            const int d = q_digit_sel(k, i);
             tab_entry((d < 0 ? -d : d) >> 1, x2, y2);
-            ng = (d < 0) != negb;
+            const bool ng = (d < 0) != negb;
             __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int dd = 0; dd + 1 < kQWin; ++dd) q4_dbl<false>(q4, x2, ut);
+            q4_dbl<true>(q4, x2, ut);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) y2.v[t] = ng ? 0u - y2.v[t] : y2.v[t];
+            q4_add_rest(q4, y2, ut);
+        }
+        f29 x2, y2;
+        qentry(0, x2, y2);
+#pragma unroll
+        for (int dd = 0; dd + 1 < kQWin; ++dd) q4_dbl<false>(q4, x2, ut);
+        q4_dbl<true>(q4, x2, ut);
+        // the last addition (digit 0) and, for an even k, the subtraction of the base: free of
+        // exceptional cases on the half-size ladders
+        q4w qw = q4;
+        q4_add_rest(qw, y2, ut);
+        if (__any(keven)) {  // k + 1 ran: subtract the base once
+            q4w q2 = qw;
+            base_neg(x2, y2);
+            q4_add_full(q2, x2, y2);
+            if (keven) qw = q2;
+        }
+        q4w_to(acc, qw);
+        vw = q4w_w(qw);
+    } else {
+        // the top term 16^L (k = 16^L + sum d_i 16^i): the base itself, Z = 1, W = c
+        {
+            f29 y0 = py;
+            if (negb) f29_neg(y0, y0);
+            q.xb = px;
+            q.zy = f29_sel_pair(one29, y0);
+            q.zo = one29;
+            q.w = cc;
+        }
+#pragma unroll 1
+        for (int i = L - 1; i >= 1; --i) {
+            f29 x2, y2;
+            bool ng = false;
+            if (SBFT_HALF_ENTRY_EARLY) {
+                // the digit's LDS reads issued before the doublings (pinned there), its sign applied
+                // after them: read after the doublings, each digit waited on LDS latency
+                const int d = SBFT_HALF_DIGIT_SEL ? q_digit_sel(k, i) : q_digit(k, i);
+                tab_entry((d < 0 ? -d : d) >> 1, x2, y2);
+                ng = (d < 0) != negb;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int d = 0; d < kQWin; ++d) p29_dbl_plw(q);
+            if (SBFT_HALF_ENTRY_EARLY) {
+#pragma unroll
+                for (int t = 0; t < 9; ++t) y2.v[t] = ng ? 0u - y2.v[t] : y2.v[t];
+            } else {
+                qentry(i, x2, y2);
+            }
+            p29_add_aff_plw(q, x2, y2);
         }
 #pragma unroll
         for (int d = 0; d < kQWin; ++d) p29_dbl_plw(q);
-        if (SBFT_HALF_ENTRY_EARLY) {
-#pragma unroll
-            for (int t = 0; t < 9; ++t) y2.v[t] = ng ? 0u - y2.v[t] : y2.v[t];
-        } else {
-            qentry(i, x2, y2);
+        // The last addition (digit 0) and, for an even k, the subtraction of the base: free of
+        // exceptional cases on the half-size ladders (both pairs, W kept).
+        plw29 qw = q;
+        {
+            f29 x2, y2;
+            qentry(0, x2, y2);
+            p29_add_aff_plw(qw, x2, y2);
         }
-        p29_add_aff_plw(q, x2, y2);
+        if (__any(keven)) {  // k + 1 ran: subtract the base once
+            plw29 q2 = qw;
+            f29 x2, y2;
+            base_neg(x2, y2);
+            p29_add_aff_plw(q2, x2, y2);
+            if (keven) qw = q2;
+        }
+        plw29_to(acc, qw);
+        vw = qw.w;
     }
-#pragma unroll
-    for (int d = 0; d < kQWin; ++d) p29_dbl_plw(q);
-    // The last addition (digit 0) and, for an even k, the subtraction of the base: free of
-    // exceptional cases on the half-size ladders (both pairs, W kept).
-    plw29 qw = q;
-    {
-        f29 x2, y2;
-        qentry(0, x2, y2);
-        p29_add_aff_plw(qw, x2, y2);
-    }
-    if (__any(keven)) {  // k + 1 ran: subtract the base once
-        plw29 q2 = qw;
-        f29 x2, y2;
-        base_neg(x2, y2);
-        p29_add_aff_plw(q2, x2, y2);
-        if (keven) qw = q2;
-    }
-    jp29 acc;
-    plw29_to(acc, qw);
     bool inf = false;  // only a classic (fb) ladder can meet infinity, at its last addition
     if (__builtin_expect(__any(fb), 0)) {  // classic ladders (pair A, c = 1): the exact repairs
         jp29 a;
-        plw29_to(a, q);
+        if constexpr (QUAD) q4w_to(a, q4);
+        else plw29_to(a, q);
         bool infa = false;
         f29 x2, y2;
         qentry(0, x2, y2);
@@ -1944,11 +2003,14 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         }
     }
     probe(5);
-    f29 VX, VW;  // pair B's X and W = c Z^2 of v R0, on pair A's lanes (quad_perm [2,3,2,3])
+    // pair (quad) B's X and W = c Z^2 of v R0, on pair (quad) A's lanes: quad_perm [2,3,2,3] (QUAD:
+    // row_shl:4, lane i gets lane i + 4's)
+    f29 VX, VW;
+    constexpr int kMoveB = QUAD ? 0x104 : 0xEE;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-        VX.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)acc.x.v[i], 0xEE, 0xF, 0xF, false);
-        VW.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)qw.w.v[i], 0xEE, 0xF, 0xF, false);
+        VX.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)acc.x.v[i], kMoveB, 0xF, 0xF, false);
+        VW.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)vw.v[i], kMoveB, 0xF, 0xF, false);
     }
 
     __syncthreads();  // #2: the helper's (v u1) G and the square test are in gsum
@@ -2028,7 +2090,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     probe_dump(tid == 0 ? "verify inputs,chain,inverse,tables,barrier1,ladder,barrier2,final"
                         : (tid == 64 ? "verify-w1" : "verify-w2"),
                tid == 0 || tid == 64 || tid == 128);
-    if (active && (tid & 3) == 0) {
+    if (active && (tid & (QUAD ? 7 : 3)) == 0) {
         if (exc && valid) {
             if constexpr (FRAMED) {  // the fixup kernel's inputs
                 fe e_raw;
@@ -2449,6 +2511,11 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
         const unsigned hblocks = (n + sbft::kHalfTuples - 1) / sbft::kHalfTuples;
         hipLaunchKernelGGL(sbft::p256_verify_half_kernel<false>, dim3(hblocks), dim3(sbft::kHalfThreads), 0, stream,
                            d_digest, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, sbft::FramedIn{});
+    } else if (lanes == 4) {  // ... a quad per ladder: 24 tuples per workgroup
+        const unsigned hblocks = (n + sbft::kHalfTuplesQ - 1) / sbft::kHalfTuplesQ;
+        hipLaunchKernelGGL((sbft::p256_verify_half_kernel<false, true>), dim3(hblocks), dim3(sbft::kHalfThreads), 0,
+                           stream, d_digest, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb,
+                           sbft::FramedIn{});
     } else if (lanes == 2) {  // 64-lane workgroups of 32 tuples
         const unsigned sblocks = (n + 31) / 32;
         hipLaunchKernelGGL(sbft::p256_verify_small_kernel<2>, dim3(sblocks), dim3(64), 0, stream, d_digest, d_r, d_s,
@@ -2547,7 +2614,7 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
                                               hipStream_t stream, int lanes, uint32_t* h_flagged) {
     if (sbft_fault_hit(2)) return -1;  // SBFT_GV_FAULT_LAUNCH (tests only)
     if (n == 0) return 0;
-    if (lanes != 2 && lanes != 3) return -1;
+    if (lanes != 2 && lanes != 3 && lanes != 4) return -1;
     static int cus = 0;
     if (!cus) {
         int dev = 0;
@@ -2556,9 +2623,14 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
             cus = 256;
     }
     const sbft::FramedIn fr{d_blob, d_off, d_len, sig_rel, pub_rel, d_dig, d_r, d_s, d_qx, d_qy, h_flagged};
-    const unsigned tpw = lanes == 3 ? (unsigned)sbft::kHalfTuples : (unsigned)sbft::small_kernel_tuples<2, true>();
+    const unsigned tpw = lanes == 4   ? (unsigned)sbft::kHalfTuplesQ
+                         : lanes == 3 ? (unsigned)sbft::kHalfTuples
+                                      : (unsigned)sbft::small_kernel_tuples<2, true>();
     const unsigned sblocks = (n + tpw - 1) / tpw;
-    if (lanes == 3)
+    if (lanes == 4)
+        hipLaunchKernelGGL((sbft::p256_verify_half_kernel<true, true>), dim3(sblocks), dim3(sbft::kHalfThreads), 0,
+                           stream, d_dig, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
+    else if (lanes == 3)
         hipLaunchKernelGGL((sbft::p256_verify_half_kernel<true>), dim3(sblocks), dim3(sbft::kHalfThreads), 0, stream,
                            d_dig, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
     else

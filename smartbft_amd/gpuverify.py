@@ -31,7 +31,7 @@ _u8p = ctypes.POINTER(ctypes.c_uint8)
 _vp = ctypes.c_void_p
 
 # sbft_gv_verify_p256_kernel's kernel names (include/sbft_gpuverify.h)
-KERNEL_EXACT, KERNEL_THROUGHPUT, KERNEL_PAIR, KERNEL_HALF = 0, 1, 2, 3
+KERNEL_EXACT, KERNEL_THROUGHPUT, KERNEL_PAIR, KERNEL_HALF, KERNEL_HALF_WIDE = 0, 1, 2, 3, 4
 
 
 class GpuVerifyError(RuntimeError):
@@ -42,7 +42,8 @@ class Opts(ctypes.Structure):
     _fields_ = [("device_mask", ctypes.c_uint32), ("min_split", ctypes.c_uint32),
                 ("pair_max", ctypes.c_int32), ("reserved0", ctypes.c_int32),
                 ("slots_per_device", ctypes.c_uint32), ("half_max", ctypes.c_int32),
-                ("client_table_bytes", ctypes.c_uint64), ("reserved", ctypes.c_uint64 * 1)]
+                ("client_table_bytes", ctypes.c_uint64), ("halfq_max", ctypes.c_int32),
+                ("reserved1", ctypes.c_int32)]
 
 
 _LIB = None
@@ -226,17 +227,20 @@ class GpuVerifier:
     (device-resident) and enqueue on the given (or current) stream."""
 
     def __init__(self, device_mask: int = 0, min_split: int = 0, pair_max: int = 0,
-                 slots_per_device: int = 0, half_max: int = 0, client_table_bytes: int = 0):
-        """pair_max / half_max: per-device batches of at most this many tuples run the pair
-        latency kernel (two lanes per tuple) / the half-size-scalar kernel (four lanes: two 128-bit
-        ladders), half_max taking precedence (0 = library default, negative = never; pair_max < 0
-        with half_max 0 forces the one-lane throughput kernel).
+                 slots_per_device: int = 0, half_max: int = 0, client_table_bytes: int = 0,
+                 halfq_max: int = 0):
+        """pair_max / half_max / halfq_max: per-device batches of at most this many tuples run the
+        pair latency kernel (two lanes per tuple) / the half-size-scalar kernel (four lanes: two
+        128-bit ladders) / its wide form (eight lanes: a quad per ladder), halfq_max then half_max
+        taking precedence (0 = library default, negative = never; pair_max < 0 with half_max 0
+        forces the one-lane throughput kernel).
         slots_per_device > 1: that many engine slots per GPU, each taking a share of a split
         batch as a separate device would (runs the multi-device split on one GPU).
         client_table_bytes: per-device budget of client-key comb tables (0 = 1/8 of the device)."""
         self.L = load_library()
         ctx = _vp()
-        opts = Opts(device_mask, min_split, pair_max, 0, slots_per_device, half_max, client_table_bytes)
+        opts = Opts(device_mask, min_split, pair_max, 0, slots_per_device, half_max, client_table_bytes,
+                    halfq_max, 0)
         rc = self.L.sbft_gv_init(ctypes.byref(opts), ctypes.byref(ctx))
         if rc:
             raise GpuVerifyError(f"sbft_gv_init: {self.L.sbft_gv_strerror(rc).decode()} ({rc})")
@@ -271,7 +275,7 @@ class GpuVerifier:
 
     def verify_kernel(self, kernel: int, digest, r, s, qx, qy) -> np.ndarray:
         """sbft_gv_verify_p256_kernel: the same verify on a named kernel (KERNEL_EXACT,
-        KERNEL_THROUGHPUT, KERNEL_PAIR, KERNEL_HALF)."""
+        KERNEL_THROUGHPUT, KERNEL_PAIR, KERNEL_HALF, KERNEL_HALF_WIDE)."""
         n = len(digest)
         arrs = [_soa(a, n) for a in (digest, r, s, qx, qy)]
         ok = np.zeros(n, dtype=np.uint8)

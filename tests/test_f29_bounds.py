@@ -498,3 +498,111 @@ def test_w_extreme_operands():
     add_aff_w(X3, Y3, Z3, W3, N_max, [(-MASK) & 0xFFFFFFFF] * 8 + [0])
     dbl_w(Np_max, [(-MASK) & 0xFFFFFFFF] * 8 + [(1 << 24) - 1], N_max, N_max)
     add_aff_w(Np_max, [(-MASK) & 0xFFFFFFFF] * 8 + [0], N_max, N_max, N_max, N_max)
+
+
+def dbl_q4(X, Y, Z, W):
+    """q4_dbl (the wide half kernel's quad doubling, p256_f29.hpp): the products of dbl_w, three
+    steps of four lanes:  a' | g | Z3;  h^2 | L = g^2 | b = X g | W3 = W g;
+    Y3 = h (3b - h^2) - L | X3 = h^2 - 2b  (b - X3 = 3b - h^2, so Y3 needs no X3; its operand's
+    limbs reach 3 2^29, the widest any product here takes)."""
+    a1 = mont(sub(X, W), add(X, W))
+    g = mont(Y, Y)
+    Z3 = mont(Y, Z)
+    h = triple_half(a1)
+    h2 = mont(h, h)
+    L = mont(g, g)
+    b = mont(X, g)
+    W3 = mont(W, g)
+    t = [fits32(3 * i32(bb) - i32(hh)) for bb, hh in zip(b, h2)]
+    Y3 = mont(h, t, addends=[(L, -1)], fold=True)
+    X3 = mont(h, h, addends=[(b, -2)], fold=True)
+    for v in (a1, g, Z3, h2, L, b, W3):
+        check_N(v)
+    for v in (X3, Y3):
+        check_Np(v)
+    return X3, Y3, Z3, W3
+
+
+def add_aff_q4(X, Y, Z, W, x2, y2):
+    """q4_dbl<true> + q4_add_rest: U2 = x2 W | T = Z1 W (on the doubling's spare lanes);
+    HH = H^2 | Z3 = Z1 H | S2 = y2 T;  V = X1 HH | HHH | W3 = W HH | r^2;  X3 = r^2 - HHH - 2V
+    (normalised limb arithmetic);  r (V - X3) | Y1 HHH, Y3 their difference (N+-)."""
+    u2 = mont(x2, W)
+    T = mont(Z, W)
+    h = sub(u2, X)
+    hh = mont(h, h)
+    Z3 = mont(Z, h)
+    s2 = mont(y2, T)
+    rr = sub(s2, Y)
+    V = mont(X, hh)
+    hhh = mont(h, hh)
+    W3 = mont(W, hh)
+    r2 = mont(rr, rr)
+    X3 = normalize(sub(sub(r2, hhh), add(V, V)))
+    t = sub(V, X3)
+    p0 = mont(rr, t)
+    p1 = mont(Y, hhh)
+    Y3 = sub(p0, p1)
+    for v in (u2, T, hh, Z3, s2, V, hhh, W3, r2, p0, p1):
+        check_N(v)
+    check_Np(X3)
+    assert all(abs(i32(y)) < 1 << 29 for y in Y3)  # N+-
+    return X3, Y3, Z3, W3
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_quad_ladder_on_the_isomorphic_curve(seed):
+    """The quad forms on the same walk as test_w_ladder_on_the_isomorphic_curve: pair B's E_c from
+    P' = (c r, c^2) and pair A's curve (c = 1), operands re-limbed at the edges of their contracts
+    (Y into the doubling as N' or N+-, into the addition as N': the kernel normalises Y before an
+    addition that follows an addition). No overflow, every contract, W = c Z^2, X / W = x(k R0)."""
+    rng = random.Random(seed)
+    G = pyref.G
+    for c_is_one in (False, True):
+        R0 = pyref.mul(rng.randrange(1, pyref.N), G)
+        r, y0 = R0
+        c = 1 if c_is_one else (r ** 3 - 3 * r + pyref.B) % P
+        yscale = 1 if c_is_one else y0
+        X, Y = (mont_of(r), mont_of(y0)) if c_is_one else (mont_of(c * r % P), mont_of(c * c % P))
+        Z, W = mont_of(1), mont_of(c)
+        ref = R0
+        for step in range(150):
+            X = relimb(X, rng, -(1 << 26) + 1, (1 << 29) + (1 << 26), 0, 1 << 24)   # N'
+            W = relimb(W, rng, 0, 1 << 29)                                           # N
+            if step % 5 == 4:
+                q = pyref.mul(rng.randrange(1, pyref.N), R0)
+                x2, y2 = mont_of(q[0]), mont_of(yscale * q[1] % P)
+                if rng.random() < 0.5:
+                    y2 = [(-i32(w)) & 0xFFFFFFFF for w in y2]
+                    q = (q[0], (-q[1]) % P)
+                Y = relimb(Y, rng, -(1 << 26) + 1, (1 << 29) + (1 << 26), 0, 1 << 24)   # N'
+                X, Y, Z, W = add_aff_q4(X, Y, Z, W, x2, y2)
+                ref = pyref.add(ref, q)
+                Y = relimb(Y, rng, -(1 << 29) + 1, 1 << 29)  # N+-
+            else:
+                if rng.random() < 0.5:
+                    Y = relimb(Y, rng, -(1 << 29) + 1, 1 << 29)                          # N+-
+                else:
+                    Y = relimb(Y, rng, -(1 << 26) + 1, (1 << 29) + (1 << 26), 0, 1 << 24)   # N'
+                X, Y, Z, W = dbl_q4(X, Y, Z, W)
+                ref = pyref.add(ref, ref)
+            z = plain(Z)
+            assert plain(W) == c * z * z % P, step
+            assert plain(X) * pow(plain(W), -1, P) % P == ref[0], step
+
+
+def test_quad_extreme_operands():
+    """Every limb at the top of its contract; and 3b - h^2's product at its analytic worst case
+    (h limbs 2^29 + 2, the operand's 3 (2^29 - 1), the reduction's m limbs 2^29 - 1)."""
+    top = (1 << 29) + (1 << 26) - 1
+    Np_max = [top] * 8 + [(1 << 24) - 1]
+    N_max = [MASK] * 8 + [(1 << 24) - 1]
+    neg = [(-MASK) & 0xFFFFFFFF] * 8 + [(1 << 24) - 1]
+    dbl_q4(Np_max, Np_max, N_max, N_max)
+    dbl_q4(Np_max, neg, N_max, N_max)
+    add_aff_q4(Np_max, Np_max, N_max, N_max, N_max, [(-MASK) & 0xFFFFFFFF] * 8 + [0])
+    h = [(1 << 29) + 2] * 8 + [(1 << 26)]
+    t = [3 * MASK] * 8 + [3 << 26]
+    worst = 9 * ((1 << 29) + 2) * 3 * MASK + MASK * sum(c for _, c in RED)
+    assert worst < I64
+    mont(h, t, addends=[(N_max, -1)], fold=True)

@@ -25,7 +25,8 @@ pytestmark = pytest.mark.gpu
 
 KERNEL_OPTS = {"lane": dict(pair_max=-1, half_max=-1),
                "pair": dict(pair_max=1 << 30, half_max=-1),
-               "half": dict(half_max=1 << 30)}
+               "half": dict(half_max=1 << 30, halfq_max=-1),
+               "halfw": dict(halfq_max=1 << 30)}
 
 
 # ---------------------------------------------------------------- config 3

@@ -46,10 +46,11 @@ def crafted():
 
 MODE_OPTS = {"lane": dict(pair_max=-1, half_max=-1),
              "pair": dict(pair_max=1 << 30, half_max=-1),
-             "half": dict(half_max=1 << 30)}
+             "half": dict(half_max=1 << 30, halfq_max=-1),
+             "halfw": dict(halfq_max=1 << 30)}
 
 
-@pytest.mark.parametrize("mode", ["lane", "pair", "half"])
+@pytest.mark.parametrize("mode", ["lane", "pair", "half", "halfw"])
 def test_crafted_exceptional_verdicts(crafted, mode):
     from smartbft_amd import GpuVerifier
     opts = MODE_OPTS[mode]
@@ -66,7 +67,7 @@ def test_crafted_exceptional_verdicts(crafted, mode):
         gv.close()
 
 
-@pytest.mark.parametrize("mode", ["pair", "half"])
+@pytest.mark.parametrize("mode", ["pair", "half", "halfw"])
 def test_crafted_exceptional_framed(crafted, mode):
     """The same tuples as framed requests (VerifyProposal's fused hash + verify launch): the
     digest is SHA-256 of the body, so the crafted scalars need e = SHA-256(body): re-derive s and
@@ -110,7 +111,7 @@ def _sbr1(i: int, pl: bytes, qx: bytes, qy: bytes) -> bytes:
             len(pl).to_bytes(4, "little") + pl + b"\x04" + qx + qy)
 
 
-@pytest.mark.parametrize("mode", ["pair", "half"])
+@pytest.mark.parametrize("mode", ["pair", "half", "halfw"])
 def test_crafted_exceptional_proposal(crafted, mode):
     """The crafted tuples as signed requests inside a VerifyProposal of honest ones
     (sbft_gv_framed_overlapped: fused hash + verify launch, verdicts in mapped host memory).

@@ -159,3 +159,22 @@ def test_pair_w_ladder(gpu):
     want = [_mul(33, pts[i & ~1]) for i in range(len(pts))]
     assert _run(gpu, 25, pts) == [q[0] for q in want], "x(33P)"
     assert _run(gpu, 26, pts) == [q[1] for q in want], "y(33P)"
+
+
+def test_quad_w_ladder(gpu):
+    """The wide half kernel's quad W ladder (p256_f29.hpp q4_dbl / q4_add_rest / q4_add_full; c = 1,
+    so W = Z^2) against the group law, on element 4t's point in all four lanes of the quad:
+    x and y of 33P (four doublings, a fifth carrying the addition's first step on lanes 2-3, the
+    addition's rest with P itself) and of 32P = 33P + (-P) (then a whole addition from the first
+    one's N+- Y). Ragged counts leave a partial last quad."""
+    rng = random.Random(34)
+    pts = [(GX, GY)] + [_mul(rng.randrange(1, N), (GX, GY)) for _ in range(60)]
+    pts += [_mul(k, (GX, GY)) for k in (2, 3, 5, N - 1, N - 2, (N + 1) // 2)]
+    for count in (len(pts), len(pts) - 1, len(pts) - 2):
+        sub = pts[:count]
+        want33 = [_mul(33, sub[i & ~3]) for i in range(count)]
+        want32 = [_mul(32, sub[i & ~3]) for i in range(count)]
+        assert _run(gpu, 27, sub) == [q[0] for q in want33], ("x(33P)", count)
+        assert _run(gpu, 28, sub) == [q[1] for q in want33], ("y(33P)", count)
+        assert _run(gpu, 29, sub) == [q[0] for q in want32], ("x(32P)", count)
+        assert _run(gpu, 30, sub) == [q[1] for q in want32], ("y(32P)", count)

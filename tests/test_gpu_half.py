@@ -15,7 +15,8 @@ from oracle import pyref
 pytestmark = pytest.mark.gpu
 
 N = pyref.N
-MODES = {"half": dict(half_max=1 << 30), "pair": dict(pair_max=1 << 30, half_max=-1),
+MODES = {"half": dict(half_max=1 << 30, halfq_max=-1), "halfw": dict(halfq_max=1 << 30),
+         "pair": dict(pair_max=1 << 30, half_max=-1),
          "lane": dict(pair_max=-1, half_max=-1)}
 
 

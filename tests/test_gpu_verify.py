@@ -291,7 +291,8 @@ def test_throughput_grid_shapes(gpu, n):
 # for big batches too) and the half-size-scalar kernel (p256_verify_half_kernel)
 KERNEL_OPTS = {"lane": dict(pair_max=-1, half_max=-1),
                "pair": dict(pair_max=1 << 30, half_max=-1),
-               "half": dict(half_max=1 << 30)}
+               "half": dict(half_max=1 << 30, halfq_max=-1),
+               "halfw": dict(halfq_max=1 << 30)}
 
 
 @pytest.fixture(scope="module", params=list(KERNEL_OPTS))

@@ -8,8 +8,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from smartbft_amd import GpuVerifier, plugin  # noqa: E402
 from smartbft_amd.workload import make_signed_requests  # noqa: E402
 
-gv = GpuVerifier(device_mask=1)
-reqs = make_signed_requests(gv, 10_000, start=4242)
+# HALF_PROBE_N requests (default 10k: the four-lane kernel on one device); HALF_PROBE_WIDE=1 with
+# N <= 6144 runs the wide form (a quad per ladder), =0 the four-lane one at the same N
+n = int(os.environ.get("HALF_PROBE_N", "10000"))
+gv = GpuVerifier(device_mask=1, halfq_max=0 if os.environ.get("HALF_PROBE_WIDE", "1") == "1" else -1)
+reqs = make_signed_requests(gv, n, start=4242)
 v = plugin.Verifier(gv, 0)
 p = plugin.Proposal(plugin.encode_payload(reqs), b"h", b"m", 0)
 for _ in range(int(os.environ.get("HALF_PROBE_CALLS", "4"))):  # more for a rocprofv3 average

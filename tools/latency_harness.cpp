@@ -15,9 +15,10 @@
 //   quorum-hook VOTERS NEED DECISIONS INFLIGHT
 //       the processCommits batch hook with arriving votes (go/patches/internal_bft_commits.patch),
 //       at most INFLIGHT (default 2) batch calls in flight.
-//   quorum-pipe CHANNELS DECISIONS gpu|cpu
+//   quorum-pipe CHANNELS DECISIONS gpu|cpu|cpu-batched
 //       pipelined decisions: CHANNELS consensus instances on one node, each deciding back to
-//       back (prev-commit batch, then the commit votes), all in flight at once.
+//       back (prev-commit batch, then the commit votes), all in flight at once; cpu-batched is
+//       the CPU plugin under the same patched call sequence as gpu (prev-commit batch over the cores).
 //   sign CALLS
 //       one signature at a time from one thread: sbft_signer_sign (RFC 6979, and with the
 //       pre-signature pool of 1,024) vs OpenSSL ECDSA_do_sign.
@@ -863,7 +864,61 @@ static int quorum_vote_cpu(int voters, int need, int decisions, int threads) {
     return wrong ? 2 : 0;
 }
 
-// quorum-pipe CHANNELS DECISIONS gpu|cpu: pipelined decisions at n = 100 (config 4). CHANNELS
+// VerifyConsenterSigs on the CPU (the prev-commit batch hook with an OpenSSL plugin): the batch's
+// signatures spread over the calling thread and `helpers` pool threads pulling indices from an
+// atomic counter, as a Go plugin would fan them out over goroutines on GOMAXPROCS threads. The
+// caller blocks (bounded spin, then a futex) until the last signature is verified.
+struct CpuBatchPool {
+    std::vector<std::thread> th;
+    std::atomic<int> gen{0}, next{0}, left{0}, bad{0};
+    std::atomic<bool> stop{false};
+    const std::vector<CpuTuple>* job = nullptr;  // the same vector every call (one channel's batch)
+    Waker done;
+    void start(int helpers, const std::vector<CpuTuple>* batch) {
+        job = batch;
+        done.spin_us = env_long("SBFT_HOOK_COLLECT_SPIN_US", 20);
+        for (int j = 0; j < helpers; ++j)
+            th.emplace_back([this] {
+                pthread_setname_np(pthread_self(), "h-cpubatch");
+                int seen = 0;
+                for (;;) {
+                    int g;
+                    while ((g = gen.load(std::memory_order_acquire)) == seen && !stop.load())
+                        futex(&gen, FUTEX_WAIT_PRIVATE, seen);
+                    if (stop.load()) return;
+                    seen = g;
+                    work();
+                }
+            });
+    }
+    void work() {
+        const int n = (int)job->size();
+        int i, mine = 0;
+        while ((i = next.fetch_add(1, std::memory_order_acq_rel)) < n) {
+            if (!cpu_verify((*job)[i])) bad.fetch_add(1, std::memory_order_relaxed);
+            ++mine;
+        }
+        if (mine && left.fetch_sub(mine, std::memory_order_acq_rel) == mine) done.notify();
+    }
+    int verify_all() {  // failures in the batch
+        bad.store(0, std::memory_order_relaxed);
+        left.store((int)job->size(), std::memory_order_relaxed);
+        next.store(0, std::memory_order_release);
+        gen.fetch_add(1, std::memory_order_release);
+        futex(&gen, FUTEX_WAKE_PRIVATE, INT_MAX);
+        work();
+        done.wait([&] { return left.load(std::memory_order_acquire) == 0; });
+        return bad.load();
+    }
+    void finish() {
+        stop.store(true);
+        gen.fetch_add(1);
+        futex(&gen, FUTEX_WAKE_PRIVATE, INT_MAX);
+        for (auto& t : th) t.join();
+    }
+};
+
+// quorum-pipe CHANNELS DECISIONS gpu|cpu|cpu-batched: pipelined decisions at n = 100 (config 4). CHANNELS
 // consensus instances on one node (e.g. one SmartBFT orderer per channel, sharing the node's
 // cores and GPU) each decide back to back, so CHANNELS decisions are always in flight. A
 // decision is what the View verifies per block: the previous decision's 67 commit signatures
@@ -874,8 +929,11 @@ static int quorum_vote_cpu(int voters, int need, int decisions, int threads) {
 //   cpu: the stock library with an OpenSSL plugin: the prev-commit loop verifies serially on
 //        the View goroutine; every vote is verified by its own goroutine (a voter thread here),
 //        and the View continues once 66 are valid.
+//   cpu-batched: the patched library with an OpenSSL plugin (the fair CPU leg):
+//        the prev-commit hook's VerifyConsenterSigs spreads the 67 signatures over the channel's
+//        share of the job's cores (CpuBatchPool); votes as in cpu (each verified as it arrives).
 // Reports decisions/s over all channels, p50/p99 per decision and CPU ms per decision (cgroup).
-static int quorum_pipe(int channels, int decisions, bool gpu) {
+static int quorum_pipe(int channels, int decisions, bool gpu, bool batched = false) {
     const int voters = 67, need = 66;
     channels = std::max(1, channels);
     // the node's goroutines run on GOMAXPROCS threads: the job's cores, shared by the channels
@@ -979,6 +1037,13 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
         }
         std::vector<std::unique_ptr<std::atomic<int>>> gen;
         for (int c = 0; c < channels; ++c) gen.emplace_back(new std::atomic<int>(-1));
+        // cpu-batched: each channel's View plus host_cores / channels - 1 pool threads
+        std::vector<std::unique_ptr<CpuBatchPool>> pools;
+        if (batched)
+            for (int c = 0; c < channels; ++c) {
+                pools.emplace_back(new CpuBatchPool());
+                pools.back()->start(std::max(0, (int)host_cores() / channels - 1), &prev[c]);
+            }
         std::atomic<bool> stop{false};
         std::vector<std::thread> vth;
         // the View blocks on the valid-vote channel as the GPU side's collector does (Waker)
@@ -1012,7 +1077,9 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
             pthread_setname_np(pthread_self(), "h-collect");
             for (int g = from; g < to; ++g) {
                 const auto t0 = Clock::now();
-                for (int i = 0; i < voters; ++i) wrong += !cpu_verify(prev[c][i]);  // serial (view.go:630-644)
+                if (batched) wrong += pools[c]->verify_all();  // the prev-commit hook, over the cores
+                else
+                    for (int i = 0; i < voters; ++i) wrong += !cpu_verify(prev[c][i]);  // serial (view.go:630-644)
                 gen[c]->store(g, std::memory_order_release);
                 futex(gen[c].get(), FUTEX_WAKE_PRIVATE, INT_MAX);
                 wk[c]->wait([&] { return valid[c][g].load(std::memory_order_acquire) >= need; });
@@ -1043,6 +1110,7 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
             futex(gen[c].get(), FUTEX_WAKE_PRIVATE, INT_MAX);
         }
         for (auto& t : vth) t.join();
+        for (auto& pl : pools) pl->finish();
         for (int c = 0; c < channels; ++c)
             for (int k = 5; k < total; ++k)
                 if (valid[c][k].load() < need) wrong++;
@@ -1055,7 +1123,7 @@ static int quorum_pipe(int channels, int decisions, bool gpu) {
                 "\"engine_call_cpu_ms_per_decision\": %.3f, \"cpu_ms_per_decision_by_thread\": %s, "
                 "\"delivery_threads_per_channel\": %d, "
                 "\"launches_per_decision\": %.2f, \"cgroup_throttled\": %lld, \"wrong_verdicts\": %d}\n",
-                gpu ? "gpu" : "cpu", channels, decisions, nd / wall_s, pct(all, 50) / 1e3, pct(all, 99) / 1e3,
+                gpu ? "gpu" : batched ? "cpu-batched" : "cpu", channels, decisions, nd / wall_s, pct(all, 50) / 1e3, pct(all, 99) / 1e3,
                 (cpu1 - cpu0) / 1e3 / nd, engine_ns.load() / 1e6 / nd, cpu_json(tc1.since(tc0), nd).c_str(),
                 deliverers > 0 ? std::min(deliverers, voters) : voters,
                 gpu ? 1.0 + (double)launches / nd : 0.0, cg1.nr_throttled - cg0.nr_throttled, wrong.load());
@@ -1272,7 +1340,10 @@ int main(int argc, char** argv) {
     if (mode == "quorum-batch") return quorum_batch(arg(2, 67), arg(3, 200));
     if (mode == "quorum-hook") return quorum_hook(arg(2, 67), arg(3, 66), arg(4, 200), arg(5, 2));
     if (mode == "sign") return sign_both(arg(2, 200));
-    if (mode == "quorum-pipe") return quorum_pipe(arg(2, 2), arg(3, 200), !(argc > 4 && !std::strcmp(argv[4], "cpu")));
+    if (mode == "quorum-pipe") {
+        const std::string b = argc > 4 ? argv[4] : "gpu";
+        return quorum_pipe(arg(2, 2), arg(3, 200), b != "cpu" && b != "cpu-batched", b == "cpu-batched");
+    }
     if (mode == "quorum-cpu") return quorum_cpu(arg(2, 66), arg(3, 200), arg(4, 66));
     if (mode == "quorum-vote-cpu") return quorum_vote_cpu(arg(2, 67), arg(3, 66), arg(4, 200), arg(5, 67));
     if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
