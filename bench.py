@@ -130,14 +130,15 @@ def _mapped(pattern: str) -> list:
         return []
 
 
-def _harness(*args, timeout=600):
-    """tools/latency_harness (per-call latency of configs 3 and 4, GPU and CPU); None if absent."""
-    exe = os.path.join(ROOT, "tools", "latency_harness")
+def _harness(*args, timeout=600, tool="latency_harness"):
+    """tools/latency_harness (per-call latency of configs 3 and 4, GPU and CPU), or another tools/
+    measurement binary; None if absent."""
+    exe = os.path.join(ROOT, "tools", tool)
     if not os.path.exists(exe):
         return None
     out = subprocess.run([exe, *[str(a) for a in args]], capture_output=True, text=True, timeout=timeout)
     if out.returncode != 0:
-        raise RuntimeError(f"latency_harness {args}: rc={out.returncode} {out.stderr[-500:]}")
+        raise RuntimeError(f"{tool} {args}: rc={out.returncode} {out.stderr[-500:]}")
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
@@ -263,6 +264,84 @@ def _pcts(ts):
     return round(float(np.percentile(ts, 50)), 3), round(float(np.percentile(ts, 99)), 3)
 
 
+def split_latency(nd: int, calls: int):
+    """BASELINE config 3 as north_star splits it: VerifyProposal over a 10k-request proposal with
+    the engine's context over the node's first nd GPUs (host batch split, a share and a stream per
+    device, no collective; each share of 10k / nd <= halfq_max runs the wide half kernel), against
+    a context on GPU 0 alone, interleaved call by call in the same run. Driven from rank 0 while
+    the other ranks wait on a CPU-side barrier, so nothing else runs on their GPUs."""
+    import ctypes
+    from smartbft_amd import GpuVerifier, plugin
+    from smartbft_amd.workload import make_signed_requests
+    gvs = {"one_gpu": GpuVerifier(device_mask=1), "split": GpuVerifier(device_mask=(1 << nd) - 1)}
+    reqs = make_signed_requests(gvs["one_gpu"], 10_000)
+    prop = plugin.Proposal(plugin.encode_payload(reqs), b"header", b"metadata", 1)
+    keep = []
+    cprop = plugin._prop(prop, keep)
+    cap = 64 + len(prop.Payload)
+    infos = ctypes.create_string_buffer(cap)
+    count, bad = ctypes.c_size_t(), ctypes.c_int64()
+    err = ctypes.create_string_buffer(512)
+    vs = {k: plugin.Verifier(g, 1) for k, g in gvs.items()}
+    want = vs["one_gpu"].VerifyProposal(prop)
+    assert len(want) == 10_000
+    ts = {k: [] for k in vs}
+    for k, v in vs.items():  # warm-up (staging, mapped buffers, both kernels' first launches)
+        assert v.VerifyProposal(prop) == want
+        for _ in range(5):
+            v.L.sbft_verifier_verify_proposal(v.h, ctypes.byref(cprop), infos, cap, ctypes.byref(count),
+                                              ctypes.byref(bad), err, 512)
+    for _ in range(calls):
+        for k, v in vs.items():
+            t0 = time.perf_counter()
+            rc = v.L.sbft_verifier_verify_proposal(v.h, ctypes.byref(cprop), infos, cap, ctypes.byref(count),
+                                                   ctypes.byref(bad), err, 512)
+            ts[k].append(time.perf_counter() - t0)
+            assert rc == 0 and count.value == 10_000, (k, rc, err.value)
+    out = {"devices": nd, "requests": 10_000, "calls": calls, "share": 10_000 // nd,
+           "devices_seen": gvs["split"].device_count}
+    for k in vs:
+        p50, p99 = _pcts(ts[k])
+        out[k] = {"p50_ms": p50, "p99_ms": p99}
+    out["p50_speedup_vs_one_gpu"] = round(out["one_gpu"]["p50_ms"] / out["split"]["p50_ms"], 3)
+    out["path"] = ("sbft_verifier_verify_proposal (C ABI), host buffers; split: one context over GPUs "
+                   "0..nd-1, contiguous shares, one stream per device (sbft_gv_plan_split)")
+    for v in vs.values():
+        v.close()
+    for g in gvs.values():
+        g.close()
+    return out
+
+
+def _call_kernel_times(v, cprop, infos, cap, count, bad, err, calls: int,
+                       kernel: str = "p256_verify_half_kernel<true> (hash on the helper wavefront)"):
+    """The VerifyProposal kernel's own time: HIP events around the call's one launch
+    (sbft_gv_kernel_timing), over a separate set of calls (the events' cost stays out of the
+    timed p50 / p99 above), with the roofline on the throughput kernel's accounting (262,144
+    32x32-bit products per verify against the measured v_mad_i64_i32 peak)."""
+    import ctypes
+    gv = v.gv
+    gv.kernel_timing(True)
+    gv.kernel_time()
+    ks = []
+    for _ in range(max(50, calls // 4)):
+        rc = v.L.sbft_verifier_verify_proposal(v.h, ctypes.byref(cprop), infos, cap, ctypes.byref(count),
+                                               ctypes.byref(bad), err, 512)
+        assert rc == 0, (rc, err.value)
+        nl, ms = gv.kernel_time()
+        if nl == 1:
+            ks.append(ms * 1e3)
+    gv.kernel_timing(False)
+    if not ks:
+        return None
+    p50 = float(np.percentile(ks, 50))
+    ach = 10_000 * PRODUCTS_PER_VERIFY / (p50 * 1e-6) / 1e12
+    return {"name": kernel, "us_p50": round(p50, 1), "us_p99": round(float(np.percentile(ks, 99)), 1),
+            "launches": len(ks), "timing": "HIP events around the launch (sbft_gv_kernel_timing)",
+            "roofline": {"achieved": round(ach, 3), "peak": MAD_PEAK_T, "frac": round(ach / MAD_PEAK_T, 4),
+                         "unit": "T 32x32->64 products/s, 262,144 per verify"}}
+
+
 def latency_configs(gv, calls: int):
     """BASELINE configs 3 and 4 through the plugin mirror (host buffers, PCIe included):
     VerifyProposal on 10k-request proposals (view.go:555) and a 67-signature commit quorum at
@@ -299,7 +378,8 @@ def latency_configs(gv, calls: int):
     out["verify_proposal_10k"] = {"p50_ms": p50, "p99_ms": p99, "calls": calls, "requests": 10_000,
                                   "verifies_per_s": round(10_000 / (p50 / 1e3)),
                                   "python_wrapper_p50_ms": _pcts(tp)[0],
-                                  "path": "sbft_verifier_verify_proposal (C ABI), host buffers, PCIe incl."}
+                                  "path": "sbft_verifier_verify_proposal (C ABI), host buffers, PCIe incl.",
+                                  "kernel": _call_kernel_times(v, cprop, infos, cap, count, bad, err, calls)}
     # the same proposals with the 10k client keys registered (sbft_verifier_add_clients): every
     # request takes the keyed comb-table launch (no doublings, one wavefront per signature)
     vr = plugin.Verifier(gv, 1)
@@ -318,8 +398,20 @@ def latency_configs(gv, calls: int):
     out["verify_proposal_10k_registered_clients"] = {
         "p50_ms": p50, "p99_ms": p99, "calls": calls, "requests": 10_000,
         "registration_s": round(reg_s, 2), "client_tables_GB": round(10_000 * 512 * 1024 / 1e9, 2),
-        "path": "sbft_verifier_verify_proposal with the clients' keys registered (keyed launch), host buffers"}
+        "path": "sbft_verifier_verify_proposal with the clients' keys registered (keyed launch), host buffers",
+        "kernel": _call_kernel_times(vr, cprop, infos, cap, count, bad, err, calls,
+                                     "p256_verify_keyed_lanes_kernel<true> (hash on a fifth wavefront)")}
     vr.close()
+    # where a call's time goes, over all calls and over the calls above p95 (the tail): the
+    # engine's SBFT_VP_TRACE split (parse, copy wait, staging, launch, kernel + verdicts) and the
+    # kernel's HIP-event time per call (tools/latency_harness proposal-phases, C, no ctypes)
+    for reg, key in ((0, "verify_proposal_10k"), (1, "verify_proposal_10k_registered_clients")):
+        try:
+            ph = _harness("proposal-phases", 10_000, max(200, calls), reg)
+        except Exception as e:
+            ph = {"error": repr(e)[:300]}
+        if ph:
+            out[key]["phases"] = ph
     # n = 100 replicas: q = 67 signatures per decision
     import hashlib
     q, f = plugin.compute_quorum(100)
@@ -675,6 +767,9 @@ def main():
     assert launches == args.steps * len(lanes) * S, (launches, args.steps)
     avg_kern_s = kern_total_ms / launches / 1e3
     n_gpus = world * len(devs)
+    # a CPU-side group for the final wait: ranks other than 0 must not sit in a collective kernel
+    # on their GPUs while rank 0 runs config 3 across all of them (split_latency)
+    gloo = dist.new_group(backend="gloo") if world > 1 else None
 
     if rank == 0:
         total = n * world * len(lanes) * args.steps
@@ -765,6 +860,18 @@ def main():
                 (ok[:len(ok_cpu)].cpu().numpy() != ok_cpu).sum())
         if n_gpus == 1 and not rehearsal and S == 1 and not args.no_pipelined:
             rec["pipelined"] = pipelined(gv, wl, dev, args.steps)
+        if n_gpus == 1 and not rehearsal and S == 1:
+            # the same config-2 measurement without torch, on the HIP runtime the engine ships with
+            # (tools/config2_harness: engine-generated workload staged once in HBM, the C ABI's
+            # device-resident verify on one stream); value above runs on torch's libamdhip64
+            try:
+                tf = _harness(n, args.steps, args.warmup, tool="config2_harness", timeout=900)
+            except Exception as e:  # a side leg must not lose the headline line
+                tf = {"error": repr(e)[:300]}
+            if tf:
+                if "verifies_per_s" in tf:
+                    tf["vs_torch_process_value"] = round(tf["verifies_per_s"] / value, 4)
+                rec["torch_free_config2"] = tf
         if world == 1 and not args.no_host_path:
             rec["host_buffer_path"] = host_path(gv, wls, dev)
         if n_gpus == 1 and not rehearsal and not args.no_sha:
@@ -812,8 +919,16 @@ def main():
                             h["speedup_p50_vs_cpu_thread_per_vote"] = round(q67["p50_ms"] / h["p50_ms"], 2)
                             h["speedup_p99_vs_cpu_thread_per_vote"] = round(q67["p99_ms"] / h["p99_ms"], 2)
             rec["latency"] = lat
+        if (world > 1 or len(devs) > 1) and not rehearsal and not args.no_latency:
+            # config 3 split over the node's GPUs, measured on the hardware (no
+            # multi-GPU run of it existed)
+            try:
+                rec["latency_split"] = split_latency(max(world, len(devs)), args.latency_calls)
+            except Exception as e:  # a measurement leg must not lose the headline line
+                rec["latency_split"] = {"error": repr(e)[:300]}
         print(json.dumps(rec), flush=True)
     if world > 1:
+        dist.barrier(group=gloo)
         dist.destroy_process_group()
 
 

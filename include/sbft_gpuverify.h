@@ -258,8 +258,12 @@ int sbft_gv_sha256_verify_p256_keyed(sbft_gv_ctx* ctx, const uint8_t* blob, size
 
 /* Kernel timing (measurement): while enabled, every device-resident verify records HIP
  * events on the caller's stream around its main p256_verify_kernel launch (not the s^-1
- * batching or fixup kernels). sbft_gv_kernel_time waits for the recorded events and returns
- * (then forgets) the number of timed launches and their summed duration in milliseconds. */
+ * batching or fixup kernels), and so do the latency paths around their one launch: the fused
+ * hash + verify kernel of a one-slot VerifyProposal (sbft_verifier_verify_proposal), its
+ * registered-client keyed launch, and the keyed launches of VerifyConsenterSig(s) (with a hash
+ * kernel in front where the batch carries messages). sbft_gv_kernel_time waits for the recorded
+ * events and returns (then forgets) the number of timed launches and their summed duration in
+ * milliseconds. */
 int sbft_gv_kernel_timing(sbft_gv_ctx* ctx, int enable);
 int sbft_gv_kernel_time(sbft_gv_ctx* ctx, uint64_t* launches, double* ms);
 

@@ -840,6 +840,41 @@ void sbft_gv_host_free(void* p) {
     if (p) (void)hipHostFree(p);
 }
 
+}  // extern "C"
+namespace {
+// sbft_gv_kernel_timing for the latency paths (the fused VerifyProposal launch, the keyed
+// launches): HIP events around one launch on its stream, handed to ctx->events for
+// sbft_gv_kernel_time. Inert unless timing is on.
+struct LaunchTimer {
+    sbft_gv_ctx* ctx;
+    hipStream_t st;
+    hipEvent_t a = nullptr, b = nullptr;
+    LaunchTimer(sbft_gv_ctx* c, hipStream_t s) : ctx(c && c->timing.load() ? c : nullptr), st(s) {
+        if (!ctx) return;
+        if (hipEventCreate(&a) != hipSuccess || hipEventRecord(a, st) != hipSuccess) {
+            if (a) (void)hipEventDestroy(a);
+            a = nullptr;
+            ctx = nullptr;
+        }
+    }
+    void end() {
+        if (!ctx) return;
+        if (hipEventCreate(&b) != hipSuccess || hipEventRecord(b, st) != hipSuccess) {
+            (void)hipEventDestroy(a);
+            if (b) (void)hipEventDestroy(b);
+        } else {
+            std::lock_guard<std::mutex> g(ctx->ev_mu);
+            ctx->events.emplace_back(a, b);
+        }
+        ctx = nullptr;
+    }
+    ~LaunchTimer() {
+        if (ctx && a) (void)hipEventDestroy(a);
+    }
+};
+}  // namespace
+extern "C" {
+
 int sbft_gv_kernel_timing(sbft_gv_ctx* ctx, int enable) {
     if (!ctx) return SBFT_GV_EINVAL;
     ctx->timing = enable != 0;
@@ -1549,8 +1584,16 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         if (blob_len && (ce = hipSetDevice(dev)) == hipSuccess)
             ce = hipMemcpyAsync(sl->bbuf, blob, blob_len, hipMemcpyHostToDevice, sl->stream);
     };
-    const bool async = ctx->helper.try_submit(copy);
-    if (!async) copy();
+    // A batch that may be split over the slots copies per share (each device its own slice): the
+    // whole-payload copy to this slot would be wasted, and the split path waits for it. Each framed
+    // message spans at least 128 bytes of the blob (a 64-byte key inside it, r || s after it), so
+    // with blob_len < 128 min_split no split is possible and the copy overlaps the parse as before.
+    const bool may_split = ctx->slots.size() > 1 && blob_len / 128 >= ctx->min_split;
+    bool async = false;
+    if (!may_split) {
+        async = ctx->helper.try_submit(copy);
+        if (!async) copy();
+    }
     const auto t1 = TC::now();
     const int prc = prepare(off, len);
     const auto t2 = TC::now();
@@ -1560,6 +1603,7 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     // helper has finished (its job holds references to this frame).
     const size_t n = off.size();
     const bool split = n >= ctx->min_split && ctx->slots.size() > 1;
+    if (may_split && !split && !prc) copy();  // not split after all: the copy the parse did not overlap
     const size_t fo = align_up(8 * n, 256), fl = align_up(4 * n, 256);
     int src = SBFT_GV_OK;
     if (!prc && n > 0 && !split) {
@@ -1621,9 +1665,9 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     if (n == 0) return SBFT_GV_OK;
     if (len.size() != n || n > 0xffffffffu) return SBFT_GV_EINVAL;
     if (split) {  // large: the multi-device split path
-        // each share copies its own slice of the payload: this slot's copy is not used
+        // each share copies its own slice of the payload (this slot made no copy of the whole)
         drain.armed = false;
-        if (stream_sync(sl->stream) != hipSuccess) return SBFT_GV_EDEVICE;
+        if (!may_split && stream_sync(sl->stream) != hipSuccess) return SBFT_GV_EDEVICE;
         lk.unlock();
         if (during) during();
         Framing fr;
@@ -1654,10 +1698,12 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         std::memcpy(sl->vmap + fo + fl, kid->data(), 4 * n);  // offsets, lengths: staged above
         const uint8_t* vd = sl->vmap_dev;
         // verdicts straight to mapped host memory (no device-to-host copy after the launch)
+        LaunchTimer kt(ctx, sl->stream);
         if (sbft_launch_p256_verify_keyed_framed(sl->bbuf, (const uint64_t*)vd, (const uint32_t*)(vd + fo), sig_rel,
                                                  (const uint32_t*)(vd + fo + fl), (const void* const*)sl->d_keytab,
                                                  nkeys, sl->vmap_dev + fo + 2 * fl, (uint32_t)n, sl->stream))
             return SBFT_GV_ELAUNCH;
+        kt.end();
         if (during) during();  // the caller's host work that does not need the verdicts
         HIPCHK(stream_sync(sl->stream));
         drain.armed = false;
@@ -1695,12 +1741,14 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         // none of in practice) runs only if the verify kernel raised this mapped flag
         volatile uint32_t* const flag = (volatile uint32_t*)(h_ok + align_up(n, 256));
         *flag = 0;
-        if (((!pre_dbuf || sl->dgen != pre_gen) &&
-             hipMemsetAsync(d_work, 0, sizeof(uint32_t), sl->stream) != hipSuccess) ||
-            sbft_launch_p256_verify_framed(sl->bbuf, d_off, d_len, (uint32_t)n, sig_rel, pub_rel, d_dig, v, v + fd,
+        if ((!pre_dbuf || sl->dgen != pre_gen) && hipMemsetAsync(d_work, 0, sizeof(uint32_t), sl->stream) != hipSuccess)
+            return SBFT_GV_ELAUNCH;
+        LaunchTimer kt(ctx, sl->stream);  // sbft_gv_kernel_timing: the fused hash + verify kernel
+        if (sbft_launch_p256_verify_framed(sl->bbuf, d_off, d_len, (uint32_t)n, sig_rel, pub_rel, d_dig, v, v + fd,
                                            v + 2 * fd, v + 3 * fd, d_hok, (uint32_t*)d_work, gcomb, sl->stream, lanes,
                                            (uint32_t*)(d_hok + align_up(n, 256))))
             return SBFT_GV_ELAUNCH;
+        kt.end();
         if (trace) tr.f = TC::now();
         if (during) during();
         HIPCHK(stream_sync(sl->stream));
@@ -1998,7 +2046,8 @@ int build_tables(Slot* sl, const std::vector<std::array<uint8_t, 64>>& keys, siz
 //     commit-quorum call). A fault is caught by polling the stream now and then.
 int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t blob_len, const uint64_t* off,
                   const uint32_t* len, const uint8_t* r, const uint8_t* s, const uint32_t* key, uint32_t nkeys,
-                  void** keytab, Slot::ZcLane* zl, uint8_t* ok_out, size_t lanes_min, size_t host_sinv_max) {
+                  void** keytab, Slot::ZcLane* zl, uint8_t* ok_out, size_t lanes_min, size_t host_sinv_max,
+                  sbft_gv_ctx* tctx = nullptr) {
     Slot* sl = c.slot;
     const bool zc = zl != nullptr;
     hipStream_t st = zc ? zl->stream : sl->stream;  // (the lane's stream is created by its reserve)
@@ -2070,6 +2119,7 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
     const uint32_t* d_len = blob ? (const uint32_t*)((const uint8_t*)d_off + align_up(8 * n, 256)) : nullptr;
     uint8_t* d_ok = d + in_bytes;
     const auto t1 = std::chrono::steady_clock::now();
+    LaunchTimer kt(tctx, st);  // sbft_gv_kernel_timing: the keyed kernel (and its hash kernel, if any)
     if (lanes) {
         uint8_t* x = d + in_bytes + fok;  // hash counter | digests
         const uint8_t* dig = dm;
@@ -2088,6 +2138,7 @@ int enqueue_keyed(Chunk& c, const uint8_t* digest, const uint8_t* blob, size_t b
                                              host_sinv ? (const uint32_t*)(d + 2 * f32 + fk + fmsg) : nullptr, st)) {
         return SBFT_GV_ELAUNCH;
     }
+    kt.end();
     if (!zc) {
         HIPCHK(hipMemcpyAsync(h + in_bytes, d_ok, n, hipMemcpyDeviceToHost, st));
         c.out_off = in_bytes;
@@ -2174,13 +2225,13 @@ int run_keyed(sbft_gv_ctx* ctx, const uint8_t* digest, const uint8_t* blob, size
             std::unique_lock<std::mutex> zlk;
             Slot::ZcLane& zl = c.slot->acquire_zc(zlk);
             return enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, keytab, &zl, ok_out, 0,
-                                 ctx->keyed_host_sinv_max);
+                                 ctx->keyed_host_sinv_max, ctx);
         }
         std::lock_guard<std::mutex> lk(c.slot->mu);
         int rc = ensure_tables(c.slot, nkeys);
         if (rc == SBFT_GV_OK)
             rc = enqueue_keyed(c, digest, blob, blob_len, off, len, r, s, key, nkeys, c.slot->d_keytab, nullptr,
-                               ok_out, ctx->keyed_lanes_min, ctx->keyed_host_sinv_max);
+                               ok_out, ctx->keyed_lanes_min, ctx->keyed_host_sinv_max, ctx);
         (void)hipSetDevice(c.slot->device);
         if (stream_sync(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
         // the verdicts sit in the slot's pinned staging, which the lock still protects

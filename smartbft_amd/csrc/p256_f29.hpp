@@ -1537,7 +1537,9 @@ template <int CTRL>
 SBFT_DEV f29 f29_qperm(const f29& a) {  // quad_perm DPP: lane j gets lane ((CTRL >> 2j) & 3)'s limbs
     f29 r;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) r.v[i] = (u32)__builtin_amdgcn_update_dpp(0, (int)a.v[i], CTRL, 0xF, 0xF, true);
+    // (mov_dpp, not update_dpp(0, ..., bound_ctrl): with the latter ROCm 7.2's DPP combiner folds the
+    // move into a consumer and the quad ladder came out wrong -- tools/isa/quad_unit.hip, round 6)
+    for (int i = 0; i < 9; ++i) r.v[i] = (u32)__builtin_amdgcn_mov_dpp((int)a.v[i], CTRL, 0xF, 0xF, false);
     return r;
 }
 // b on the quad lanes of M, quad_perm CTRL of a elsewhere: one v_cndmask_b32_dpp per limb (the DPP

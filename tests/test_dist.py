@@ -76,3 +76,41 @@ def test_library_plan_split_min_split_and_tiny_shares():
     assert plan_split(3, 8, min_split=1) == [(0, 1), (1, 1), (2, 1)]
     assert plan_split(10, 1, min_split=1) == [(0, 10)]
     assert plan_split(10, 0) == []
+
+
+@pytest.mark.parametrize("nd", [2, 4, 8])
+def test_config3_split_shares_fit_the_wide_kernel(nd):
+    """The engine's default min_split with the wide half kernel on (halfq_max + 1; 24 x 256 CUs + 1 =
+    6,145 on an MI355X): a 10k-request proposal on nd devices is cut into nd contiguous shares, each
+    at most halfq_max tuples, so every device runs the wide kernel; on one device it stays whole."""
+    from smartbft_amd.gpuverify import plan_split
+    halfq = 24 * 256
+    parts = plan_split(10_000, nd, min_split=halfq + 1)
+    assert len(parts) == nd and max(c for _, c in parts) <= halfq
+    assert sum(c for _, c in parts) == 10_000 and parts[0][0] == 0
+    assert plan_split(10_000, 1, min_split=halfq + 1) == [(0, 10_000)]
+    assert plan_split(halfq, nd, min_split=halfq + 1) == [(0, halfq)]
+
+
+def _gloo_wait_worker(rank, world, port, out):
+    # bench.py's end at N > 1: rank 0 runs config 3 across the GPUs while the others wait on a
+    # gloo group's barrier (no collective kernel on their devices), then all leave together
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = dist.new_group(backend="gloo")
+    if rank == 0:
+        import time
+        time.sleep(0.5)
+    dist.barrier(group=g)
+    out[rank] = True
+    dist.destroy_process_group()
+
+
+def test_two_rank_cpu_side_final_barrier():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gloo_wait_worker, args=(world, port, out), nprocs=world, join=True)
+    assert dict(out) == {0: True, 1: True}

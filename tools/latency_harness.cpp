@@ -32,6 +32,7 @@
 //       10th decision has a bad vote, as in quorum-hook.
 //   proposal-cpu REQUESTS DECISIONS THREADS
 //   proposal-gpu REQUESTS DECISIONS
+//   proposal-phases REQUESTS CALLS REGISTERED   (where a VerifyProposal call's time goes)
 //   parse-cpu    REQUESTS ITERS
 //       VerifyProposal (view.go:555) on the CPU: REQUESTS signed requests (distinct keys,
 //       64-256 B bodies) verified by THREADS workers pulling indices from an atomic counter:
@@ -55,6 +56,7 @@
 #include <climits>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -72,6 +74,7 @@
 #include "../include/sbft_verifier.h"
 
 using Clock = std::chrono::steady_clock;
+static int64_t now_ns() { return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count(); }
 
 static double pct(std::vector<double> v, double p) {
     std::sort(v.begin(), v.end());
@@ -426,6 +429,8 @@ struct BatchWorker {
     int rc = 0;
     const std::atomic<int>* armed = nullptr;  // the channel's decision is collecting: stay awake
     Waker* done = nullptr;                    // the collector's wait, notified when a batch is done
+    // phase stamps (ns, steady clock): the collector's at post time, the worker's around the call
+    int64_t post_ns = 0, wake_ns = 0, last_arr_ns = 0, call0_ns = 0, call1_ns = 0;
     std::atomic<int64_t>* engine_ns = nullptr;  // CPU time spent inside the engine's calls
     long spin_us = 10;  // after a batch, spin this long for the next one (SBFT_HOOK_WORKER_SPIN_US)
     void start() {
@@ -445,7 +450,9 @@ struct BatchWorker {
                 if (s == 3) return;
                 res.assign(batch.size(), 0);
                 const int64_t c0 = thread_cpu_ns();
+                call0_ns = now_ns();
                 rc = sbft_verifier_verify_consenter_sigs(v, batch.data(), batch.size(), p, res.data());
+                call1_ns = now_ns();
                 if (engine_ns) engine_ns->fetch_add(thread_cpu_ns() - c0, std::memory_order_relaxed);
                 st.store(2, std::memory_order_release);
                 if (done) done->notify();
@@ -478,7 +485,12 @@ struct HookChannel {
     const std::vector<sbft_proposal>* props;
     const std::vector<std::vector<std::vector<uint8_t>>>*msgs, *vals, *bads;
     std::unique_ptr<std::atomic<int>[]> order;
+    std::unique_ptr<int64_t[]> arr_ns;  // delivery time of arrival k (written before order[k])
     std::atomic<int> arrived{0}, gen{-1};
+    // per decision, the batch that completed the quorum (quorum-hook's breakdown, microseconds):
+    // release -> its last vote delivered | -> the collector awake for it | -> batch posted |
+    // -> the worker in the engine call | the call | -> the View (collector) has the verdicts
+    std::vector<double> ph_arrive, ph_wake, ph_post, ph_pickup, ph_call, ph_view;
     std::atomic<bool> stop_{false};
     std::vector<std::thread> th;
     std::vector<std::unique_ptr<BatchWorker>> w;
@@ -495,6 +507,7 @@ struct HookChannel {
     void start() {
         waker.spin_us = env_long("SBFT_HOOK_COLLECT_SPIN_US", 20);
         order.reset(new std::atomic<int>[voters]);
+        arr_ns.reset(new int64_t[voters]);
         for (int i = 0; i < voters; ++i) order[i].store(0);
         const int nd = deliverers > 0 ? std::min(deliverers, voters) : voters;
         for (int j = 0; j < nd; ++j)
@@ -513,6 +526,7 @@ struct HookChannel {
                     seen = g;
                     for (int i = j; i < voters; i += nd) {
                         const int k = arrived.fetch_add(1, std::memory_order_seq_cst);
+                        arr_ns[k] = now_ns();
                         order[k].store(i + 1, std::memory_order_release);
                         if (k + 1 >= wake_at.load(std::memory_order_seq_cst)) waker.notify();
                     }
@@ -555,13 +569,25 @@ struct HookChannel {
             for (auto& x : w) futex(&x->st, FUTEX_WAKE_PRIVATE, 1);
         }
         int valid = 0, consumed = 0, in_flight = 0, in_votes = 0;
+        int64_t wake_ns = now_ns(), last_arr = 0;
+        const int64_t t0_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count();
         std::vector<int> pending;
         auto harvest = [&](BatchWorker& x) {
             if (x.rc) wrong++;
+            const bool short_before = valid < need;
             for (size_t k = 0; k < x.batch.size(); ++k) {
                 const bool is_bad = bad_dec && x.who[k] == 7;
                 if (is_bad != (x.res[k] != 0)) wrong++;
                 if (!x.res[k] && valid < need) ++valid;
+            }
+            if (short_before && valid >= need) {  // this batch completed the quorum
+                const int64_t h = now_ns();
+                ph_arrive.push_back((x.last_arr_ns - t0_ns) / 1e3);
+                ph_wake.push_back(std::max<int64_t>(0, x.wake_ns - x.last_arr_ns) / 1e3);
+                ph_post.push_back((x.post_ns - std::max(x.wake_ns, x.last_arr_ns)) / 1e3);
+                ph_pickup.push_back((x.call0_ns - x.post_ns) / 1e3);
+                ph_call.push_back((x.call1_ns - x.call0_ns) / 1e3);
+                ph_view.push_back((h - x.call1_ns) / 1e3);
             }
             in_flight--;
             in_votes -= (int)x.batch.size();
@@ -580,6 +606,7 @@ struct HookChannel {
                 int i;
                 while ((i = order[consumed].load(std::memory_order_acquire)) == 0) __builtin_ia32_pause();
                 pending.push_back(i - 1);
+                last_arr = arr_ns[consumed];
                 progress = true;
             }
             // the patch's canLaunch: quorum reachable, a batch slot free
@@ -600,6 +627,9 @@ struct HookChannel {
                 in_flight++;
                 in_votes += (int)x->batch.size();
                 ++launches;
+                x->wake_ns = wake_ns;
+                x->last_arr_ns = last_arr;
+                x->post_ns = now_ns();
                 x->post();
                 progress = true;
             }
@@ -616,6 +646,7 @@ struct HookChannel {
                            worker_done();
                 });
                 wake_at.store(0, std::memory_order_relaxed);
+                wake_ns = now_ns();
             }
         }
         const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
@@ -690,6 +721,9 @@ static int quorum_hook(int voters, int need, int decisions, int inflight) {
     sbft_verifier* v = sbft_verifier_new(ctx, 1);
     int wrong = 0, launches = 0;
     std::vector<double> t;
+    std::string phases = "{}";
+    uint64_t klaunch = 0;
+    double kms = 0;
     {
         VoteSet vs(ctx, v, voters, 1000);
         HookChannel ch;
@@ -703,19 +737,35 @@ static int quorum_hook(int voters, int need, int decisions, int inflight) {
         ch.bads = &vs.bads;
         ch.start();
         for (int g = -5; g < decisions; ++g) {
-            if (g == 0) ch.launches = 0;
+            if (g == 0) {
+                ch.launches = 0;
+                for (auto* ph : {&ch.ph_arrive, &ch.ph_wake, &ch.ph_post, &ch.ph_pickup, &ch.ph_call, &ch.ph_view})
+                    ph->clear();
+                (void)sbft_gv_kernel_timing(ctx, 1);  // HIP events around every keyed launch
+                (void)sbft_gv_kernel_time(ctx, &klaunch, &kms);
+            }
             const double us = ch.decide(g + 5, (g + 80) % VoteSet::NB, g % 10 == 9);
             if (g >= 0) t.push_back(us);
         }
         ch.finish();
+        (void)sbft_gv_kernel_time(ctx, &klaunch, &kms);
         wrong = ch.wrong;
         launches = ch.launches;
+        char buf[512];
+        std::snprintf(buf, sizeof buf,
+                      "{\"release_to_last_vote_us\": %.1f, \"collector_wake_us\": %.1f, \"batch_post_us\": %.1f, "
+                      "\"worker_pickup_us\": %.1f, \"engine_call_us\": %.1f, \"view_wake_us\": %.1f, "
+                      "\"keyed_kernel_us_mean\": %.1f, \"timed_launches\": %llu}",
+                      pct(ch.ph_arrive, 50), pct(ch.ph_wake, 50), pct(ch.ph_post, 50), pct(ch.ph_pickup, 50),
+                      pct(ch.ph_call, 50), pct(ch.ph_view, 50), klaunch ? kms * 1e3 / (double)klaunch : 0.0,
+                      (unsigned long long)klaunch);
+        phases = buf;
     }
     std::printf("{\"mode\": \"quorum-hook\", \"voters\": %d, \"need\": %d, \"decisions\": %d, \"inflight\": %d, "
                 "\"p50_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f, \"launches_per_decision\": %.2f, "
-                "\"wrong_verdicts\": %d}\n",
+                "\"phases_p50\": %s, \"wrong_verdicts\": %d}\n",
                 voters, need, decisions, std::max(1, inflight), pct(t, 50) / 1e3, pct(t, 99) / 1e3, pct(t, 100) / 1e3,
-                (double)launches / decisions, wrong);
+                (double)launches / decisions, phases.c_str(), wrong);
     sbft_verifier_free(v);
     sbft_gv_destroy(ctx);
     return wrong ? 2 : 0;
@@ -1214,6 +1264,126 @@ static int proposal_cpu(int requests, int decisions, int threads) {
 // (generic path), one with a bad signature at a varying index, one truncated (malformed), and
 // the honest one again with every client registered (keyed path). Checks every verdict, count
 // and reported index; reports the honest generic call's p50/p99.
+// proposal-phases REQUESTS CALLS REGISTERED: where a VerifyProposal call's time goes (VERDICT r05
+// #4). The engine's SBFT_VP_TRACE split of every call (submit | parse | copy wait | staging |
+// launch | the rest: kernel, verdicts, return), captured from its stderr, and HIP events around
+// the call's one kernel (sbft_gv_kernel_timing: p256_verify_half_kernel<true> generic, the keyed
+// lanes kernel with the clients registered). Reports medians over all calls and over the calls
+// above the 95th percentile (the tail), with the kernel's time in each.
+static int proposal_phases(int requests, int calls, int registered) {
+    setenv("SBFT_VP_TRACE", "1", 1);  // before the engine's first VerifyProposal reads it
+    char tpath[] = "/tmp/sbft_vp_traceXXXXXX";
+    const int tfd = mkstemp(tpath);
+    if (tfd < 0) return 1;
+    std::fflush(stderr);
+    const int saved = dup(2);
+    dup2(tfd, 2);
+    sbft_gv_ctx* ctx = nullptr;
+    if (sbft_gv_init(nullptr, &ctx)) {
+        dup2(saved, 2);
+        std::fprintf(stderr, "no GPU\n");
+        return 1;
+    }
+    sbft_verifier* v = sbft_verifier_new(ctx, 0);
+    std::vector<uint8_t> payload(4), keys;
+    uint32_t cnt = (uint32_t)requests;
+    std::memcpy(payload.data(), &cnt, 4);
+    for (int i = 0; i < requests; ++i) {
+        uint8_t d[32], pub[65], buf[1024];
+        priv_of(50'000 + i, d);
+        sbft_signer* c = sbft_signer_new(ctx, 1, d);
+        sbft_signer_public_key(c, pub);
+        keys.insert(keys.end(), pub, pub + 65);
+        std::string body(64 + i % 193, (char)('a' + i % 26));
+        const std::string cid = "client" + std::to_string(i), rid = "tx" + std::to_string(i);
+        const int64_t len = sbft_make_request(c, cid.c_str(), rid.c_str(), (const uint8_t*)body.data(), body.size(), buf,
+                                              sizeof buf);
+        sbft_signer_free(c);
+        if (len <= 0) return 3;
+        const uint32_t l = (uint32_t)len;
+        payload.insert(payload.end(), (const uint8_t*)&l, (const uint8_t*)&l + 4);
+        payload.insert(payload.end(), buf, buf + len);
+    }
+    if (registered) sbft_verifier_add_clients(v, keys.data(), (size_t)requests);
+    std::vector<char> infos((size_t)requests * 40);
+    char err[256];
+    sbft_proposal p{payload.data(), payload.size(), (const uint8_t*)"h", 1, (const uint8_t*)"m", 1, 0};
+    int wrong = 0;
+    for (int g = 0; g < 5; ++g) {  // warm-up
+        size_t count = 0;
+        int64_t bad = -1;
+        wrong += sbft_verifier_verify_proposal(v, &p, infos.data(), infos.size(), &count, &bad, err, sizeof err) != 0;
+    }
+    (void)sbft_gv_kernel_timing(ctx, 1);
+    uint64_t nl = 0;
+    double kms = 0;
+    (void)sbft_gv_kernel_time(ctx, &nl, &kms);
+    std::fflush(stderr);
+    const off_t mark = lseek(tfd, 0, SEEK_END);
+    std::vector<double> tot, kern;
+    for (int g = 0; g < calls; ++g) {
+        size_t count = 0;
+        int64_t bad = -1;
+        const auto t0 = Clock::now();
+        const int rc = sbft_verifier_verify_proposal(v, &p, infos.data(), infos.size(), &count, &bad, err, sizeof err);
+        tot.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+        wrong += rc != 0 || count != (size_t)requests;
+        (void)sbft_gv_kernel_time(ctx, &nl, &kms);
+        kern.push_back(nl == 1 ? kms * 1e3 : -1.0);
+    }
+    std::fflush(stderr);
+    dup2(saved, 2);
+    // the calls' trace lines, in call order (the engine prints one per call)
+    std::vector<std::array<double, 6>> ph;
+    {
+        FILE* f = std::fopen(tpath, "r");
+        if (f) {
+            std::fseek(f, (long)mark, SEEK_SET);
+            char line[512];
+            while (std::fgets(line, sizeof line, f)) {
+                int a = 0;
+                std::array<double, 6> x{};
+                if (std::sscanf(line, "vp async=%d submit=%lf parse=%lf copy_wait_sync=%lf stage=%lf launch=%lf rest=%lf",
+                                &a, &x[0], &x[1], &x[2], &x[3], &x[4], &x[5]) == 7)
+                    ph.push_back(x);
+            }
+            std::fclose(f);
+        }
+        unlink(tpath);
+        close(tfd);
+    }
+    const double p95 = pct(tot, 95);
+    auto med = [&](bool tail, int field) {  // field -1: the kernel
+        std::vector<double> v;
+        for (size_t i = 0; i < tot.size(); ++i)
+            if (!tail || tot[i] > p95) {
+                if (field < 0) {
+                    if (kern[i] >= 0) v.push_back(kern[i]);
+                } else if (i < ph.size()) {
+                    v.push_back(ph[i][field]);
+                }
+            }
+        return pct(v, 50);
+    };
+    auto group = [&](bool tail) {
+        char b[400];
+        std::snprintf(b, sizeof b,
+                      "{\"submit_us\": %.1f, \"parse_us\": %.1f, \"copy_wait_us\": %.1f, \"stage_us\": %.1f, "
+                      "\"launch_us\": %.1f, \"kernel_verdicts_return_us\": %.1f, \"kernel_us\": %.1f}",
+                      med(tail, 0), med(tail, 1), med(tail, 2), med(tail, 3), med(tail, 4), med(tail, 5), med(tail, -1));
+        return std::string(b);
+    };
+    std::printf("{\"mode\": \"proposal-phases\", \"requests\": %d, \"calls\": %d, \"registered\": %d, "
+                "\"p50_ms\": %.4f, \"p95_ms\": %.4f, \"p99_ms\": %.4f, \"kernel_us_p50\": %.1f, "
+                "\"kernel_us_p99\": %.1f, \"traced_calls\": %zu, \"all_p50\": %s, \"tail_above_p95\": %s, "
+                "\"wrong_verdicts\": %d}\n",
+                requests, calls, registered, pct(tot, 50) / 1e3, p95 / 1e3, pct(tot, 99) / 1e3, pct(kern, 50),
+                pct(kern, 99), ph.size(), group(false).c_str(), group(true).c_str(), wrong);
+    sbft_verifier_free(v);
+    sbft_gv_destroy(ctx);
+    return wrong ? 2 : 0;
+}
+
 static int proposal_gpu(int requests, int decisions) {
     sbft_gv_ctx* ctx = nullptr;
     if (sbft_gv_init(nullptr, &ctx)) {
@@ -1348,6 +1518,7 @@ int main(int argc, char** argv) {
     if (mode == "quorum-vote-cpu") return quorum_vote_cpu(arg(2, 67), arg(3, 66), arg(4, 200), arg(5, 67));
     if (mode == "proposal-cpu") return proposal_cpu(arg(2, 10000), arg(3, 20), arg(4, 16));
     if (mode == "proposal-gpu") return proposal_gpu(arg(2, 3000), arg(3, 20));
+    if (mode == "proposal-phases") return proposal_phases(arg(2, 10000), arg(3, 200), arg(4, 0));
     if (mode == "parse-cpu") return parse_cpu(arg(2, 6000), arg(3, 50));
     std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
     return 1;
