@@ -307,20 +307,25 @@ struct Slot {
         }
     };
     // mapped, coherent host memory the VerifyProposal launches read their message offsets and
-    // lengths from (sbft_gv_framed_overlapped; no copy, caller holds mu)
+    // lengths from (sbft_gv_framed_overlapped; no copy, caller holds mu). Called while the helper
+    // may still be queueing the payload copy on `stream`: when the buffer grows, the
+    // synchronisation and hipHostFree below wait behind that copy, so the overlap holds only for
+    // calls that do not grow it -- the buffer doubles, so after a proposal of a given size
+    // every later one up to twice as large reuses it.
     uint8_t* vmap = nullptr;
     uint8_t* vmap_dev = nullptr;
     size_t vmap_cap = 0;
     int reserve_vmap(size_t bytes) {
         NOMEM_POINT();
         if (bytes <= vmap_cap) return SBFT_GV_OK;
+        const size_t old_cap = vmap_cap;
         if (vmap) {
             (void)hipStreamSynchronize(stream);  // the last launches that read it have drained
             (void)hipHostFree(vmap);
         }
         vmap = vmap_dev = nullptr;
         vmap_cap = 0;
-        size_t want = std::max(bytes, (size_t)1 << 18);
+        size_t want = std::max(bytes, std::max((size_t)1 << 18, 2 * old_cap));
         want = (want + 4095) & ~(size_t)4095;
         if (hipHostMalloc((void**)&vmap, want, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
             vmap = nullptr;
@@ -2283,14 +2288,30 @@ int sign_wave(sbft_gv_ctx* ctx, const uint8_t* d, const uint8_t* k, const uint8_
 // New client keys whose tables still fit (caller holds keys_mu): the client budget per device
 // (ctx->client_cap, default 1/8 of the device's memory) and, on every device, the memory above
 // the staging reserve. A device with k slots pays k tables per key.
-size_t client_key_room(sbft_gv_ctx* ctx) {
+// Client keys that still fit every device's budget, or SBFT_GV_EDEVICE in *rc when a device's
+// memory cannot be queried (an engine failure, never reported as a spent budget). The calling
+// thread's current device is restored.
+size_t client_key_room(sbft_gv_ctx* ctx, int* rc) {
+    *rc = SBFT_GV_OK;
     const size_t tb = sbft_comb_table_bytes();
     std::map<int, size_t> spd;
     for (Slot* sl : ctx->slots) ++spd[sl->device];
     size_t room = SIZE_MAX;
+    int prev = -1;
+    const bool have_prev = hipGetDevice(&prev) == hipSuccess;
+    struct Restore {
+        bool on;
+        int dev;
+        ~Restore() {
+            if (on) (void)hipSetDevice(dev);
+        }
+    } restore{have_prev, prev};
     for (const auto& [dev, k] : spd) {
         size_t free_b = 0, total = 0;
-        if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total) != hipSuccess) return 0;
+        if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total) != hipSuccess) {
+            *rc = SBFT_GV_EDEVICE;
+            return 0;
+        }
         const uint64_t cap = ctx->client_cap ? ctx->client_cap : total / 8;
         const uint64_t used = (uint64_t)ctx->client_keys * tb * k;
         const size_t by_cap = used >= cap ? 0 : (size_t)((cap - used) / (tb * k));
@@ -2307,7 +2328,9 @@ int register_keys(sbft_gv_ctx* ctx, const uint8_t* qx, const uint8_t* qy, size_t
     if (!ctx || (n && (!qx || !qy || !key_ids)) || n > 0xffffffu) return SBFT_GV_EINVAL;
     std::lock_guard<std::mutex> g(ctx->keys_mu);
     const size_t before = ctx->keys.size();
-    const size_t max_new = client ? client_key_room(ctx) : SIZE_MAX;
+    int room_rc = SBFT_GV_OK;
+    const size_t max_new = client ? client_key_room(ctx, &room_rc) : SIZE_MAX;
+    if (room_rc) return room_rc;
     std::vector<size_t> pending;  // positions i whose key is new in this call
     std::vector<uint8_t> held(n, 1);  // 0: past the budget (id 0)
     for (size_t i = 0; i < n; ++i) {

@@ -2267,6 +2267,9 @@ __global__ __launch_bounds__(FRAMED ? 4 * SBFT_KEYED_FRAMED_TPB + 64 : 256) void
     }
     fn_mul(u, j < 2 ? e : r, w);  // u1 = e s^-1 (j < 2) or u2 = r s^-1 (plain)
     fn_canon(u, u);
+#if defined(SBFT_KEYED_HOT_TABLE) && !defined(SBFT_KEYED_PROBE)
+#error "SBFT_KEYED_HOT_TABLE returns wrong verdicts (timing probe only): build it with SBFT_KEYED_PROBE"
+#endif
 #ifdef SBFT_KEYED_HOT_TABLE  // development (timing only, wrong verdicts): every u2 Q from one key's table
     const uint4* tab = keytab[j < 2 ? 0u : (valid ? 1u : 0u)];
 #else

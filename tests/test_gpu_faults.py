@@ -127,3 +127,18 @@ def test_one_shot_fault_then_recovery(fnet):
     with pytest.raises(plugin.VerifyError) as ei:
         v.VerifyProposal(p)
     assert ei.value.code == plugin.EVERIFY and ei.value.index == 123
+
+
+def test_init_rejects_reserved_fields():
+    """sbft_gv_opts' reserved fields must be 0: a caller still setting a retired field (reserved0
+    was quad_max) gets SBFT_GV_EINVAL instead of having it read as something else."""
+    import ctypes
+    from smartbft_amd.gpuverify import Opts, load_library
+    L = load_library()
+    for field in ("reserved0", "reserved1"):
+        o = Opts()
+        o.device_mask = 1
+        setattr(o, field, 1)
+        ctx = ctypes.c_void_p()
+        assert L.sbft_gv_init(ctypes.byref(o), ctypes.byref(ctx)) == -1, field
+        assert not ctx.value

@@ -48,13 +48,16 @@ def test_exact_kernel_crafted_collisions(one_slot):
 
 
 def test_kernels_back_to_back_on_one_workspace(one_slot, p256_vectors):
-    """half -> pair -> lane -> half -> exact, then again with ragged sizes, on the one slot of one
-    context: whatever one kernel leaves in the slot's workspace (fixup counter and list, verdict
-    staging, s^-1 arrays, Q tables) must not change the next kernel's verdicts."""
-    from smartbft_amd.gpuverify import KERNEL_EXACT, KERNEL_HALF, KERNEL_PAIR, KERNEL_THROUGHPUT
+    """half -> wide half -> pair -> lane -> half -> wide half -> exact, then again with ragged
+    sizes, on the one slot of one context: whatever one kernel leaves in the slot's workspace
+    (fixup counter and list, verdict staging, s^-1 arrays, Q tables) must not change the next
+    kernel's verdicts."""
+    from smartbft_amd.gpuverify import (KERNEL_EXACT, KERNEL_HALF, KERNEL_HALF_WIDE, KERNEL_PAIR,
+                                        KERNEL_THROUGHPUT)
     f, exp, cat, names = p256_vectors
-    order = [KERNEL_HALF, KERNEL_PAIR, KERNEL_THROUGHPUT, KERNEL_HALF, KERNEL_EXACT]
-    for sizes in ([len(exp)] * len(order), [1, 72, 1023, 2049, 3263]):
+    order = [KERNEL_HALF, KERNEL_HALF_WIDE, KERNEL_PAIR, KERNEL_THROUGHPUT, KERNEL_HALF, KERNEL_HALF_WIDE,
+             KERNEL_EXACT]
+    for sizes in ([len(exp)] * len(order), [1, 72, 1023, 2049, 3263, 7, 25]):
         for k, n in zip(order, sizes):
             idx = np.arange(n) % len(exp)
             got = one_slot.verify_kernel(k, *split_fields(f[idx]))
@@ -68,6 +71,6 @@ def test_exact_kernel_rejects_unknown_kernel(one_slot, p256_vectors):
     from smartbft_amd.gpuverify import GpuVerifyError
     f, exp, _, _ = p256_vectors
     with pytest.raises(GpuVerifyError):
-        one_slot.verify_kernel(4, *split_fields(f[:8]))
+        one_slot.verify_kernel(5, *split_fields(f[:8]))
     with pytest.raises(GpuVerifyError):
         one_slot.verify_kernel(-1, *split_fields(f[:8]))

@@ -117,6 +117,40 @@ def test_golden_vectors_keyed_paths(p256_vectors, path, monkeypatch):
     g.close()
 
 
+@pytest.mark.parametrize("host_sinv_max", ["96", "0"])
+def test_golden_vectors_keyed_host_sinv(p256_vectors, host_sinv_max, monkeypatch):
+    """The zero-copy wavefront path with s^-1 from the host (batches of at most keyed_host_sinv_max
+    = 96 signatures, modn::sinv_batch_mont; s = 0 and s >= n are swapped for 1 there and rejected
+    by the kernel's `valid` flag) and with it off (SBFT_KEYED_HOST_SINV_MAX=0: the kernel inverts),
+    every golden category -- out-of-range s included -- in batches of 96 and of odd sizes."""
+    from smartbft_amd import GpuVerifier
+    monkeypatch.setenv("SBFT_KEYED_ZC_MAX", "100000")
+    monkeypatch.setenv("SBFT_KEYED_LANES_MIN", "0")
+    monkeypatch.setenv("SBFT_KEYED_HOST_SINV_MAX", host_sinv_max)
+    g = GpuVerifier(device_mask=1)
+    f, exp, cat, names = p256_vectors
+    rng = np.random.default_rng(12)
+    keep = []
+    for c in np.unique(cat):
+        idx = np.nonzero(cat == c)[0]
+        keep.extend(idx if len(idx) <= 96 else rng.choice(idx, 24, replace=False))
+    keep = np.sort(np.array(keep))
+    rows = f[keep]
+    ids = _register_all(g, rows)
+    d, r, s, _, _ = split_fields(rows)
+    want = exp[keep]
+    for size in (96, 67, 1):
+        for lo in range(0, len(keep), size):
+            sel = np.arange(lo, min(lo + size, len(keep)))
+            got = g.verify_keyed(d[sel], r[sel], s[sel], ids[sel])
+            bad = np.nonzero(got != want[sel])[0]
+            assert len(bad) == 0, (host_sinv_max, size, lo,
+                                   {names[c]: int((cat[keep][sel][bad] == c).sum()) for c in np.unique(cat[keep][sel][bad])})
+            if size == 1 and lo > 40:
+                break
+    g.close()
+
+
 def _signed(n, nkeys, seed, corrupt=0.3):
     rng = random.Random(seed)
     keys = [rng.randrange(1, N) for _ in range(nkeys)]
