@@ -477,8 +477,12 @@ struct Slot {
     }
 
     uint64_t dgen = 0;  // dbuf allocations so far (a new one may reuse the old address)
+    // dbuf reservations so far: a path that wants to know whether anyone else wrote dbuf since
+    // its own last use compares this (enqueue_framed_share's fix-up counter)
+    uint64_t duses = 0, share_clean_at = UINT64_MAX;
     int reserve(size_t bytes) {
         NOMEM_POINT();
+        ++duses;
         if (bytes <= dcap) return SBFT_GV_OK;
         if (dbuf) (void)hipFree(dbuf);
         dbuf = nullptr;
@@ -1430,6 +1434,77 @@ int enqueue_selftest(const Chunk& c, int op, const uint8_t* a, const uint8_t* b,
 
 // Each device chunk is enqueued and synchronised by its own host thread (for_each_device);
 // a chunk's slot is locked by the thread that drives it.
+// One device's share of a split VerifyProposal (the multi-device branch of
+// sbft_gv_framed_overlapped) in the one-slot path's form: the share's offsets and lengths and its
+// verdicts live in the slot's mapped host memory (no copies of them), the payload slice is the
+// one DMA, and the fused hash + verify launch is followed by the fix-up kernel only when the
+// kernel raised the mapped flag. The fix-up counter at dbuf's start is cleared only when another
+// path used dbuf since this path's last call, or that call flagged a tuple (a clean call leaves it
+// 0). Synchronous. The caller holds the slot's lock.
+int enqueue_framed_share(const Chunk& c, const uint8_t* blob, size_t blob_len, const uint64_t* off,
+                         const uint32_t* len, int32_t sig_rel, int32_t pub_rel, uint8_t* ok_out) {
+    Slot* sl = c.slot;
+    const size_t n = c.count, b = c.begin;
+    if (n == 0) return SBFT_GV_OK;
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (size_t k = b; k < b + n; ++k) {
+        if (off[k] + len[k] > blob_len || off[k] + len[k] < off[k]) return SBFT_GV_EINVAL;
+        lo = std::min(lo, off[k]);
+        hi = std::max(hi, off[k] + len[k]);
+        const int64_t end = (int64_t)(off[k] + len[k]);
+        for (int32_t rel : {sig_rel, pub_rel}) {
+            const int64_t a = end + rel;
+            if (a < 0 || (uint64_t)a + 64 > blob_len) return SBFT_GV_EINVAL;
+            lo = std::min(lo, (uint64_t)a);
+            hi = std::max(hi, (uint64_t)a + 64);
+        }
+    }
+    const size_t span = hi - lo;
+    const size_t fw = align_up(sbft_verify_work_bytes(n), 256);
+    const size_t fb = align_up(span + SBFT_GV_SHA_BLOB_PAD, 256);  // + the hash's over-read
+    const size_t fd = align_up(32 * n, 256), fo = align_up(8 * n, 256), fl = align_up(4 * n, 256);
+    HIPCHK(hipSetDevice(sl->device));
+    const uint64_t gen0 = sl->dgen;
+    const bool clean = sl->share_clean_at == sl->duses;  // nobody used dbuf since our clean call
+    int rc = sl->reserve(fw + fb + 5 * fd);  // work | blob | digests | r | s | qx | qy
+    if (!rc) rc = sl->reserve_vmap(fo + fl + align_up(n, 256) + 256);
+    if (rc) return rc;
+    const void* gcomb = sl->gcomb_table();
+    if (!gcomb) return SBFT_GV_ENOMEM;
+    sl->share_clean_at = UINT64_MAX;
+    uint8_t* d = sl->dbuf;
+    uint8_t *d_work = d, *d_blob = d + fw, *d_dig = d_blob + fb, *v = d_dig + fd;
+    uint64_t* ho = (uint64_t*)sl->vmap;
+    uint32_t* hl = (uint32_t*)(sl->vmap + fo);
+    for (size_t k = 0; k < n; ++k) {
+        ho[k] = off[b + k] - lo;
+        hl[k] = len[b + k];
+    }
+    uint8_t* const h_ok = sl->vmap + fo + fl;
+    const uint8_t* vd = sl->vmap_dev;
+    uint8_t* const d_hok = sl->vmap_dev + fo + fl;
+    volatile uint32_t* const flag = (volatile uint32_t*)(h_ok + align_up(n, 256));
+    *flag = 0;
+    if ((!clean || sl->dgen != gen0) && hipMemsetAsync(d_work, 0, sizeof(uint32_t), sl->stream) != hipSuccess)
+        return SBFT_GV_EDEVICE;
+    HIPCHK(hipMemcpyAsync(d_blob, blob + lo, span, hipMemcpyHostToDevice, sl->stream));
+    if (sbft_launch_p256_verify_framed(d_blob, (const uint64_t*)vd, (const uint32_t*)(vd + fo), (uint32_t)n, sig_rel,
+                                       pub_rel, d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_hok, (uint32_t*)d_work,
+                                       gcomb, sl->stream, c.lanes, (uint32_t*)(d_hok + align_up(n, 256))))
+        return SBFT_GV_ELAUNCH;
+    HIPCHK(stream_sync(sl->stream));
+    if (*flag) {
+        if (sbft_launch_p256_verify_fixup(d_dig, v, v + fd, v + 2 * fd, v + 3 * fd, d_hok, (const uint32_t*)d_work,
+                                          (uint32_t)n, sl->stream))
+            return SBFT_GV_ELAUNCH;
+        HIPCHK(stream_sync(sl->stream));
+    } else {
+        sl->share_clean_at = sl->duses;  // the counter stays 0 for the next share call
+    }
+    std::memcpy(ok_out + b, h_ok, n);
+    return SBFT_GV_OK;
+}
+
 template <class F>
 int run_chunks(sbft_gv_ctx* ctx, size_t n, F&& enqueue) {
     std::vector<Chunk> chunks = plan(ctx, n);
@@ -1544,6 +1619,8 @@ int sbft_gv_sha256_verify_p256_framed(sbft_gv_ctx* ctx, const uint8_t* blob, siz
     fr.sig_rel = sig_rel;
     fr.pub_rel = pub_rel;
     return run_chunks(ctx, n, [&](const Chunk& c, size_t i) {
+        if (framed_fused_on() && c.lanes >= 2)  // the fused launch, offsets and verdicts in mapped memory
+            return enqueue_framed_share(c, blob, blob_len, off, len, sig_rel, pub_rel, ok_out);
         return enqueue_hash(c, blob, blob_len, off, len, nullptr, nullptr, nullptr, nullptr, ok_out, nullptr,
                             rebased[i], fr);
     });
@@ -1674,7 +1751,6 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         drain.armed = false;
         if (!may_split && stream_sync(sl->stream) != hipSuccess) return SBFT_GV_EDEVICE;
         lk.unlock();
-        if (during) during();
         Framing fr;
         fr.on = true;
         fr.sig_rel = sig_rel;
@@ -1685,9 +1761,27 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
             fr.keyed_min = ctx->keyed_lanes_min;
         }
         std::vector<std::vector<uint64_t>> rebased(ctx->slots.size() + 1);
-        return run_chunks(ctx, n, [&](const Chunk& c, size_t i) {
-            return enqueue_hash(c, blob, blob_len, off.data(), len.data(), nullptr, nullptr, nullptr, nullptr,
-                                ok.data(), nullptr, rebased[i], fr);
+        // The shares run on the context's workers (share i on worker i + 1) while this thread does
+        // the caller's host work (`during`: the full format check and the RequestInfo records),
+        // as the one-slot path does it under its launch.
+        const std::vector<Chunk> chunks = plan(ctx, n);
+        return for_each_device(ctx, chunks.size() + 1, [&](size_t i) -> int {
+            if (i == 0) {
+                if (during) during();
+                return SBFT_GV_OK;
+            }
+            const Chunk& c = chunks[i - 1];
+            std::lock_guard<std::mutex> slk(c.slot->mu);
+            int rc;
+            // a share the fused hash + verify launch takes: the one-slot path's mapped-memory form
+            if (framed_fused_on() && c.lanes >= 2 && !(fr.kid && fr.keyed_min && c.count >= fr.keyed_min))
+                rc = enqueue_framed_share(c, blob, blob_len, off.data(), len.data(), sig_rel, pub_rel, ok.data());
+            else
+                rc = enqueue_hash(c, blob, blob_len, off.data(), len.data(), nullptr, nullptr, nullptr, nullptr,
+                                  ok.data(), nullptr, rebased[i - 1], fr);
+            (void)hipSetDevice(c.slot->device);
+            if (stream_sync(c.slot->stream) != hipSuccess && rc == SBFT_GV_OK) rc = SBFT_GV_EDEVICE;
+            return rc;
         });
     }
     if (src) return src;  // the bounds checks and the offsets' staging above

@@ -2454,6 +2454,19 @@ extern "C" size_t sbft_verify_work_bytes(size_t n) {
            (size_t)SBFT_VERIFY_QTAB_BYTES * n;
 }
 
+// The wide half kernel's workgroup uses ~65 KB of static LDS, so two could share a CU (160 KB):
+// their three verify wavefronts would then share SIMDs and both run at half speed. Its launches
+// ask for enough dynamic LDS to make a workgroup take more than half of a CU's, so workgroups of
+// concurrent launches (other callers, or the K slots of a one-GPU split rehearsal) wait for a
+// CU of their own instead. One CU per workgroup is how a launch of up to halfq_max tuples lays
+// out anyway. (Dynamic LDS the kernel never touches: a reservation only.)
+static size_t halfq_dyn_lds(const void* kernel) {
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, kernel) != hipSuccess) return 0;
+    const size_t want = 82u * 1024u;  // > 160 KB / 2
+    return a.sharedSizeBytes >= want ? 0 : want - a.sharedSizeBytes;
+}
+
 extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d_r, const uint8_t* d_s,
                                        const uint8_t* d_qx, const uint8_t* d_qy, uint8_t* d_ok,
                                        uint32_t n, uint32_t* d_work, const void* d_gcomb, hipStream_t stream,
@@ -2516,7 +2529,8 @@ extern "C" int sbft_launch_p256_verify(const uint8_t* d_digest, const uint8_t* d
                            d_digest, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, sbft::FramedIn{});
     } else if (lanes == 4) {  // ... a quad per ladder: 24 tuples per workgroup
         const unsigned hblocks = (n + sbft::kHalfTuplesQ - 1) / sbft::kHalfTuplesQ;
-        hipLaunchKernelGGL((sbft::p256_verify_half_kernel<false, true>), dim3(hblocks), dim3(sbft::kHalfThreads), 0,
+        static const size_t dyn = halfq_dyn_lds((const void*)sbft::p256_verify_half_kernel<false, true>);
+        hipLaunchKernelGGL((sbft::p256_verify_half_kernel<false, true>), dim3(hblocks), dim3(sbft::kHalfThreads), dyn,
                            stream, d_digest, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb,
                            sbft::FramedIn{});
     } else if (lanes == 2) {  // 64-lane workgroups of 32 tuples
@@ -2630,8 +2644,9 @@ extern "C" int sbft_launch_p256_verify_framed(const uint8_t* d_blob, const uint6
                          : lanes == 3 ? (unsigned)sbft::kHalfTuples
                                       : (unsigned)sbft::small_kernel_tuples<2, true>();
     const unsigned sblocks = (n + tpw - 1) / tpw;
+    static const size_t dynq = halfq_dyn_lds((const void*)sbft::p256_verify_half_kernel<true, true>);
     if (lanes == 4)
-        hipLaunchKernelGGL((sbft::p256_verify_half_kernel<true, true>), dim3(sblocks), dim3(sbft::kHalfThreads), 0,
+        hipLaunchKernelGGL((sbft::p256_verify_half_kernel<true, true>), dim3(sblocks), dim3(sbft::kHalfThreads), dynq,
                            stream, d_dig, d_r, d_s, d_qx, d_qy, d_ok, n, d_work, (const uint4*)d_gcomb, fr);
     else if (lanes == 3)
         hipLaunchKernelGGL((sbft::p256_verify_half_kernel<true>), dim3(sblocks), dim3(sbft::kHalfThreads), 0, stream,

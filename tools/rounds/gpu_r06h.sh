@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 6: the wide kernel with its dynamic-LDS reservation (one workgroup per CU): the half /
+# split / config suites, the kernel at share sizes, and the split path's host cost on one GPU.
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=r06h
+out=gpurun_out/$T.txt; : > $out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_field.py tests/test_gpu_half.py tests/test_gpu_split.py tests/test_gpu_configs.py tests/test_gpu_fixup.py -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || { tail -30 gpurun_out/${T}_tests.log; exit 1; }
+tail -1 gpurun_out/${T}_tests.log >> $out
+for n in 1250 5000; do
+  timeout -k 10 180 python -u tools/half_wide_sizes.py $n 30 >> $out 2> gpurun_out/${T}_sizes_$n.err || { tail -20 gpurun_out/${T}_sizes_$n.err; cat $out; exit 1; }
+done
+for spec in "2500 2" "5000 4" "10000 8" "10000 2"; do
+  set -- $spec
+  timeout -k 10 300 python -u tools/split_probe.py $1 $2 100 >> $out 2> gpurun_out/${T}_probe_$1_$2.err || { tail -10 gpurun_out/${T}_probe_$1_$2.err; cat $out; exit 1; }
+done
+cat $out
