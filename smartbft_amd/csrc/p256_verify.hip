@@ -1570,6 +1570,49 @@ SBFT_DEV void f29_sqrt_chain(f29& y, const f29& x) {
     y = t;
 }
 
+// z^-1 = z^(p - 2) in the Montgomery domain: 255 squarings and 13 products on the addition chain
+// x2, x4, x8, x16, x24, x28, x30, x32 (x_k = z^(2^k - 1)), then (((x32 2^32 z) 2^128 x32) 2^32 x32)
+// 2^30 x30, 2^2 z -- one rolled loop over the 13 links (a squaring loop, one product by a
+// selected multiplier, the result kept by select), so the code is two products' worth.
+SBFT_DEV void f29_inv_chain(f29& out, const f29& z) {
+    // per link: squarings, multiplier (0 z, 1 x2, 2 x4, 3 x8, 4 x30, 5 x32), slot the result goes to
+    constexpr u32 kSq = 1u | 2u << 8 | 4u << 16 | 8u << 24, kSq2 = 8u | 4u << 8 | 2u << 16 | 2u << 24,
+                  kSq3 = 32u | 128u << 8 | 32u << 16 | 30u << 24;
+    f29 m1 = z, m2 = z, m3 = z, m4 = z, m5 = z, t = z;
+#pragma unroll 1
+    for (int l = 0; l < 13; ++l) {
+        const u32 sq = l < 4 ? (kSq >> (8 * l)) & 255u
+                     : l < 8 ? (kSq2 >> (8 * (l - 4))) & 255u
+                     : l < 12 ? (kSq3 >> (8 * (l - 8))) & 255u : 2u;
+        // multiplier: links 0..12 -> z, x2, x4, x8, x8, x4, x2, x2, z, x32, x32, x30, z
+        const int mi = (int)((0x455011233210ull >> (4 * l)) & 15);  // nibble l (link 0 lowest)
+        f29_sqr_n(t, (int)sq);
+        f29 m;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            u32 v = z.v[i];
+            v = mi == 1 ? m1.v[i] : v;
+            v = mi == 2 ? m2.v[i] : v;
+            v = mi == 3 ? m3.v[i] : v;
+            v = mi == 4 ? m4.v[i] : v;
+            v = mi == 5 ? m5.v[i] : v;
+            m.v[i] = v;
+        }
+        f29_mul_ilp(t, t, m);
+        // results kept: link 0 -> x2, 1 -> x4, 2 -> x8, 6 -> x30, 7 -> x32
+        if (l == 0) m1 = t;
+        if (l == 1) m2 = t;
+        if (l == 2) m3 = t;
+        if (l == 6) m4 = t;
+        if (l == 7) m5 = t;
+    }
+    out = t;
+}
+
+#ifndef SBFT_HALF_GAFF
+#define SBFT_HALF_GAFF 2  // the wide form's affine (v u1) G: 1 safegcd, 2 Fermat chain, 0 none (general join)
+#endif
+
 template <bool FRAMED, bool QUAD = false>
 __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const uint8_t* __restrict__ digest,
                                                                     const uint8_t* __restrict__ rr,
@@ -1746,6 +1789,31 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         bool ginf = true;  // the first addition returns its addend (add_aff_fix)
         comb_add_u1g(g, c, neg1, gcomb, [](jp29& a, const f29& x2, const f29& y2) { p29_add_aff_lean(a, x2, y2); },
                      [&](auto reload) { add_aff_fix(g, ginf, [](jp29& p) { p29_dbl(p, p); }, reload); });
+        // The verify wavefronts join the sum with one mixed addition (a quad's or a pair's), so it
+        // is made affine here: the helper has ~150 us to spare after the comb for one inversion and
+        // four products. Z = 0 without the infinity flag (no honest tuple) keeps the Jacobian sum
+        // for the general join.
+        bool gaff = false;
+        if constexpr (SBFT_HALF_GAFF != 0) {
+            gaff = !ginf && !f29_zero_mod_p(g.z);
+            f29 zinv, z2, z3, ax, ay;
+            if (SBFT_HALF_GAFF == 1) {
+                fe zi;
+                inv::inv_mod(zi.v, f29_canon_plain(gaff ? g.z : f29_const(C29_ONE)).v, dtab, true);
+                f29_mul(zinv, f29_from_u256(zi), f29_const(C29_R2));  // 1 / Z
+            } else {
+                f29_inv_chain(zinv, g.z);
+            }
+            f29_sqr(z2, zinv);
+            f29_mul(z3, z2, zinv);
+            f29_mul(ax, g.x, z2);
+            f29_mul(ay, g.y, z3);
+            if (gaff) {
+                g.x = ax;
+                g.y = ay;
+                g.z = f29_const(C29_ONE);
+            }
+        }
         probe(5);
         // No square test here (round 5): whether x = r is on the curve at all (r^3 - 3r + b a
         // square) is decided by the comparison itself; only an irregular end of the ladders
@@ -1758,7 +1826,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                 gsum[(9 + k) * T + lane] = g.y.v[k];
                 gsum[(18 + k) * T + lane] = g.z.v[k];
             }
-            gsum[27 * T + lane] = ginf ? 1u : 0u;
+            gsum[27 * T + lane] = (ginf ? 1u : 0u) | (gaff ? 2u : 0u);
         }
         __syncthreads();  // #2: hand-over to the verify wavefronts
         probe_dump("helper sinv,hgcd,published,barrier1,hash,comb", lane == 0);
@@ -1883,7 +1951,8 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     jp29 acc;
     f29 vw;
     plw29 q;
-    q4w q4;
+    q4w q4, qfin;  // QUAD: the ladder's end as a quad state (the join's mixed addition starts there)
+    plw29 qfinp;   // the same as a pair state (four-lane form)
     if constexpr (QUAD) {
         // the top term 16^L: the base itself, Z = 1, W = c
         {
@@ -1924,6 +1993,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         }
         q4w_to(acc, qw);
         vw = q4w_w(qw);
+        qfin = qw;
     } else {
         // the top term 16^L (k = 16^L + sum d_i 16^i): the base itself, Z = 1, W = c
         {
@@ -1975,6 +2045,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         }
         plw29_to(acc, qw);
         vw = qw.w;
+        qfinp = qw;
     }
     bool inf = false;  // only a classic (fb) ladder can meet infinity, at its last addition
     if (__builtin_expect(__any(fb), 0)) {  // classic ladders (pair A, c = 1): the exact repairs
@@ -2016,14 +2087,62 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
     __syncthreads();  // #2: the helper's (v u1) G and the square test are in gsum
     probe(6);
     const u32 gflags = gsum[27 * T + pr];
-    {
-        jp29 g;
+    jp29 g;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            g.x.v[i] = gsum[i * T + pr];
-            g.y.v[i] = gsum[(9 + i) * T + pr];
-            g.z.v[i] = gsum[(18 + i) * T + pr];
+    for (int i = 0; i < 9; ++i) {
+        g.x.v[i] = gsum[i * T + pr];
+        g.y.v[i] = gsum[(9 + i) * T + pr];
+        g.z.v[i] = gsum[(18 + i) * T + pr];
+    }
+    // T = acc + g (pair / quad A), V on E_c: x(V) = X_V / W_V. Accept iff T != infinity and
+    // X_T W_V == X_V Z_T^2. No square test is needed for a regular end (Z_T, W_V != 0): if c =
+    // r^3 - 3r + b is not a square, E_c is the quadratic twist, and x(V) = X_V / W_V has f(x) =
+    // x^3 - 3x + b = (Y_V / c)^2 / c a non-square (f has no root: the curve has no point of order
+    // 2), so it is the x of no point of the curve, T's included, and the comparison fails -- as
+    // Go's x(R) = r must, since no point has x = r. (A twist point of small order, which could end V
+    // at infinity, is out of reach: the twist order is 3 5 13 179 times a 241-bit prime, and P' is
+    // fixed by r.)
+    bool accept = false, irregular = false, exc = false, joined = false;
+    if constexpr (QUAD) {
+        // The wide form's join: the helper's affine sum added to quad A's end state by one quad
+        // mixed addition (4 steps) and both sides of the comparison in one step, W_T = Z_T^2 on
+        // the curve (c = 1), instead of the general Jacobian addition and three products on every
+        // lane (19 products in sequence). Only when no tuple of the wavefront runs the classic
+        // ladder, every sum is affine and no addition meets H = 0 (c G = +-w Q): else the general
+        // join below, from the same end state.
+        if (!__any(fb || (gflags & 2u) == 0)) {
+            q4w t4 = qfin;
+            q4_add_full(t4, g.x, g.y);
+            const f29 zt = f29_qperm<0xAA>(t4.z);
+            const bool hz = role == 0 && f29_zero_mod_p(zt);
+            if (!__any(hz)) {
+                joined = true;
+                f29 o, d;
+                f29_mul_ilp(o, f29_qsel<kQL1>(t4.xy, VX), f29_qsel<kQL1>(VW, f29_qperm<0xAA>(t4.w)));  // X_T W_V | X_V W_T
+                f29_sub(d, f29_qperm<0x00>(o), f29_qperm<0x55>(o));
+                irregular = f29_zero_mod_p(zt) || f29_zero_mod_p(VW);
+                accept = !irregular && f29_zero_mod_p_any(d);
+            }
         }
+    } else {
+        // The four-lane form's join, the same way: one paired mixed addition (5 steps) and one
+        // paired step for both sides of the comparison
+        if (!__any(fb || (gflags & 2u) == 0)) {
+            plw29 t2 = qfinp;
+            p29_add_aff_plw(t2, g.x, g.y);
+            const f29 zt = f29_sel_pair(t2.zy, t2.zo);  // Z_T in both lanes
+            const bool hz = role == 0 && f29_zero_mod_p(zt);
+            if (!__any(hz)) {
+                joined = true;
+                f29 o, d;
+                f29_mul_ilp(o, f29_sel_pair(t2.xb, VX), f29_sel_pair(VW, t2.w));  // X_T W_V | X_V W_T
+                f29_sub(d, o, f29_swap_pair(o));
+                irregular = f29_zero_mod_p(zt) || f29_zero_mod_p(VW);
+                accept = !irregular && f29_zero_mod_p_any(d);
+            }
+        }
+    }
+    if (!joined) {  // wave-uniform
         const bool ginf = (gflags & 1u) != 0;
         const jp29 a0 = acc;
         p29_add_jac_lean(acc, g);
@@ -2038,23 +2157,15 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             if (inf) acc = g;
             inf = (hz && !twice) || (inf && ginf);
         }
-    }
-    // T = acc (pair A), V on E_c: x(V) = X_V / W_V. Accept iff T != infinity and X_T W_V == X_V Z_T^2.
-    // No square test is needed for a regular end (Z_T, W_V != 0): if c = r^3 - 3r + b is not a
-    // square, E_c is the quadratic twist, and x(V) = X_V / W_V has f(x) = x^3 - 3x + b = (Y_V / c)^2
-    // / c a non-square (f has no root: the curve has no point of order 2), so it is the x of no
-    // point of the curve, T's included, and the comparison fails -- as Go's x(R) = r must, since
-    // no point has x = r. (A twist point of small order, which could end V at infinity, is out of
-    // reach: the twist order is 3 5 13 179 times a 241-bit prime, and P' is fixed by r.)
-    bool accept, exc = false;
-    {
         f29 zt2, lhs, rhs2, d;
         f29_sqr(zt2, acc.z);
         f29_mul(lhs, acc.x, VW);
         f29_mul(rhs2, VX, zt2);
         f29_sub(d, lhs, rhs2);  // |limb| < 2^29.2, |.| < 2^257
-        const bool irregular = f29_zero_mod_p(acc.z) || f29_zero_mod_p(VW);
+        irregular = f29_zero_mod_p(acc.z) || f29_zero_mod_p(VW);
         accept = !irregular && f29_zero_mod_p_any(d);
+    }
+    {
         // never for a valid honest tuple; an invalid one (rejected whatever its pairs computed)
         // must not send its wavefront down this path
         if (__builtin_expect(__any(irregular && !inf && valid && !fb), 0)) {
