@@ -1545,9 +1545,18 @@ SBFT_DEV f29 f29_qperm(const f29& a) {  // quad_perm DPP: lane j gets lane ((CTR
 // b on the quad lanes of M, quad_perm CTRL of a elsewhere: one v_cndmask_b32_dpp per limb (the DPP
 // applies to the select's src0), so a move and a select cost one instruction. The mask goes to VCC
 // in the block; s_nop 1 covers the DPP read of a VGPR the instruction in front may have written.
+#ifndef SBFT_QSELP_ASM
+#define SBFT_QSELP_ASM 1
+#endif
 template <u64 M, int CTRL>
 SBFT_DEV f29 f29_qselp(const f29& a, const f29& b) {
     f29 r;
+    if (!SBFT_QSELP_ASM) {  // a move and a select per limb, scheduled limb by limb
+        const f29 p = f29_qperm<CTRL>(a);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) r.v[i] = qsel<M>(p.v[i], b.v[i]);
+        return r;
+    }
 #define SBFT_QP "quad_perm:[%10,%11,%12,%13] row_mask:0xf bank_mask:0xf\n"
     asm("s_mov_b64 vcc, %9\n"
         "s_nop 1\n"
