@@ -1,4 +1,4 @@
-"""Differential parity sweep at scale (round 5): N seeded tuples -- GPU-signed, then a seeded mix of
+"""Differential parity sweep at scale (round 5; round 6 adds the wide half kernel): N seeded tuples -- GPU-signed, then a seeded mix of
 corruptions and edge forms -- through every verify kernel of the engine and the keyed paths,
 each compared verdict for verdict with the oracle (oracle/p256_oracle.c, the C restatement of Go's
 crypto/ecdsa.Verify: the checker, as in the tests). Prints one JSON line.
@@ -231,7 +231,7 @@ def main():
     fields = (e, r, s, qx, qy)
     record("selected", gv.verify(*fields))
     for name, kn in (("throughput", gpuverify.KERNEL_THROUGHPUT), ("pair", gpuverify.KERNEL_PAIR),
-                     ("half", gpuverify.KERNEL_HALF)):
+                     ("half", gpuverify.KERNEL_HALF), ("half_wide", gpuverify.KERNEL_HALF_WIDE)):
         record(name, gv.verify_kernel(kn, *fields))
     sub = np.arange(min(a.exact, a.n))
     record("exact", gv.verify_kernel(gpuverify.KERNEL_EXACT, *(f[sub] for f in fields)), sub)
