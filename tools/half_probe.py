@@ -15,6 +15,12 @@ gv = GpuVerifier(device_mask=1, halfq_max=0 if os.environ.get("HALF_PROBE_WIDE",
 reqs = make_signed_requests(gv, n, start=4242)
 v = plugin.Verifier(gv, 0)
 p = plugin.Proposal(plugin.encode_payload(reqs), b"h", b"m", 0)
+# HALF_PROBE_NOCHECK=1: a timing-only build with wrong verdicts (run it with SBFT_GV_SELFTEST=0)
+nocheck = os.environ.get("HALF_PROBE_NOCHECK") == "1"
 for _ in range(int(os.environ.get("HALF_PROBE_CALLS", "4"))):  # more for a rocprofv3 average
-    assert len(v.VerifyProposal(p)) == len(reqs)
+    try:
+        assert len(v.VerifyProposal(p)) == len(reqs)
+    except Exception:
+        if not nocheck:
+            raise
 sys.stdout.flush()

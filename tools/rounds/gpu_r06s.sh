@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 6: helper on lane pairs in the wide form (s^-1 split over the pair) and the curve check after
+# barrier 1 -- half suites on the new build, then phase probes against HEAD (h0) at 1,250 / 5,000
+# (wide) and 10,000 (four-lane).
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+V=$PWD/tools/variants
+T=r06s
+out=gpurun_out/$T.txt; : > $out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_half.py tests/test_gpu_exceptional.py tests/test_gpu_configs.py tests/test_gpu_fixup.py tests/test_gpu_verify.py -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || { tail -30 gpurun_out/${T}_tests.log; exit 1; }
+tail -1 gpurun_out/${T}_tests.log >> $out
+for n in 1250 5000 10000; do
+for h in h0 h1; do
+  w=1; [ $n = 10000 ] && w=0
+  echo "== n=$n $h" >> $out
+  HALF_PROBE_N=$n HALF_PROBE_WIDE=$w SBFT_GV_LIB=$V/lib_probe_$h.so timeout -k 10 120 python tools/half_probe.py > gpurun_out/${T}_${n}_$h.log 2>&1 || { tail -5 gpurun_out/${T}_${n}_$h.log; exit 1; }
+  grep "half-probe " gpurun_out/${T}_${n}_$h.log | tail -4 >> $out
+done
+done
+cat $out
