@@ -1662,9 +1662,12 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     const uint64_t pre_gen = sl->dgen;
     if (pre_dbuf && hipMemsetAsync(pre_dbuf + 256, 0, sizeof(uint32_t), sl->stream) != hipSuccess)
         return SBFT_GV_EDEVICE;
+    TC::time_point tcs{}, tce{};  // the payload copy's start and return (SBFT_VP_TRACE)
     auto copy = [&] {
+        if (trace) tcs = TC::now();
         if (blob_len && (ce = hipSetDevice(dev)) == hipSuccess)
             ce = hipMemcpyAsync(sl->bbuf, blob, blob_len, hipMemcpyHostToDevice, sl->stream);
+        if (trace) tce = TC::now();
     };
     // A batch that may be split over the slots copies per share (each device its own slice): the
     // whole-payload copy to this slot would be wasted, and the split path waits for it. Each framed
@@ -1672,8 +1675,13 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
     // with blob_len < 128 min_split no split is possible and the copy overlaps the parse as before.
     const bool may_split = ctx->slots.size() > 1 && blob_len / 128 >= ctx->min_split;
     bool async = false;
+    // SBFT_VP_COPY_FIRST=1 (diagnostics): the copy on this thread before the parse, not beside it
+    static const bool copy_first = [] {
+        const char* e = getenv("SBFT_VP_COPY_FIRST");
+        return e && e[0] == '1';
+    }();
     if (!may_split) {
-        async = ctx->helper.try_submit(copy);
+        async = !copy_first && ctx->helper.try_submit(copy);
         if (!async) copy();
     }
     const auto t1 = TC::now();
@@ -1732,15 +1740,19 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         bool on;
         TC::time_point a, b, c, d, e, f;  // e: offsets staged, f: launch returned (fused path)
         bool async;
+        const TC::time_point *cs, *ce;  // the copy's start and return
         ~Tr() {
             if (!on) return;
             auto us = [](TC::time_point x, TC::time_point y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
             const TC::time_point z = TC::now();
             if (f == TC::time_point{}) e = f = d;
-            fprintf(stderr, "vp async=%d submit=%.1f parse=%.1f copy_wait_sync=%.1f stage=%.1f launch=%.1f rest=%.1f us\n",
-                    (int)async, us(a, b), us(b, c), us(c, d), us(d, e), us(e, f), us(f, z));
+            const bool cp = *cs != TC::time_point{} && *ce != TC::time_point{};
+            fprintf(stderr, "vp async=%d submit=%.1f parse=%.1f copy_wait_sync=%.1f stage=%.1f launch=%.1f rest=%.1f us"
+                    " copy=%.1f,%.1f\n",
+                    (int)async, us(a, b), us(b, c), us(c, d), us(d, e), us(e, f), us(f, z), cp ? us(a, *cs) : -1.0,
+                    cp ? us(a, *ce) : -1.0);
         }
-    } tr{trace, t0, t1, t2, t3, {}, {}, async};
+    } tr{trace, t0, t1, t2, t3, {}, {}, async, &tcs, &tce};
     if (prc) return prc;
     if (sync_rc) return sync_rc;
     ok.assign(n, 0);

@@ -1334,7 +1334,7 @@ static int proposal_phases(int requests, int calls, int registered) {
     std::fflush(stderr);
     dup2(saved, 2);
     // the calls' trace lines, in call order (the engine prints one per call)
-    std::vector<std::array<double, 6>> ph;
+    std::vector<std::array<double, 8>> ph;  // + the payload copy's start and return (from the call's start)
     {
         FILE* f = std::fopen(tpath, "r");
         if (f) {
@@ -1342,10 +1342,14 @@ static int proposal_phases(int requests, int calls, int registered) {
             char line[512];
             while (std::fgets(line, sizeof line, f)) {
                 int a = 0;
-                std::array<double, 6> x{};
+                std::array<double, 8> x{};
+                x[6] = x[7] = -1;
                 if (std::sscanf(line, "vp async=%d submit=%lf parse=%lf copy_wait_sync=%lf stage=%lf launch=%lf rest=%lf",
-                                &a, &x[0], &x[1], &x[2], &x[3], &x[4], &x[5]) == 7)
+                                &a, &x[0], &x[1], &x[2], &x[3], &x[4], &x[5]) == 7) {
+                    const char* cp = std::strstr(line, "copy=");
+                    if (cp) (void)std::sscanf(cp, "copy=%lf,%lf", &x[6], &x[7]);
                     ph.push_back(x);
+                }
             }
             std::fclose(f);
         }
@@ -1359,18 +1363,20 @@ static int proposal_phases(int requests, int calls, int registered) {
             if (!tail || tot[i] > p95) {
                 if (field < 0) {
                     if (kern[i] >= 0) v.push_back(kern[i]);
-                } else if (i < ph.size()) {
+                } else if (i < ph.size() && ph[i][field] >= 0) {
                     v.push_back(ph[i][field]);
                 }
             }
         return pct(v, 50);
     };
     auto group = [&](bool tail) {
-        char b[400];
+        char b[512];
         std::snprintf(b, sizeof b,
                       "{\"submit_us\": %.1f, \"parse_us\": %.1f, \"copy_wait_us\": %.1f, \"stage_us\": %.1f, "
-                      "\"launch_us\": %.1f, \"kernel_verdicts_return_us\": %.1f, \"kernel_us\": %.1f}",
-                      med(tail, 0), med(tail, 1), med(tail, 2), med(tail, 3), med(tail, 4), med(tail, 5), med(tail, -1));
+                      "\"launch_us\": %.1f, \"kernel_verdicts_return_us\": %.1f, \"kernel_us\": %.1f, "
+                      "\"copy_start_us\": %.1f, \"copy_return_us\": %.1f}",
+                      med(tail, 0), med(tail, 1), med(tail, 2), med(tail, 3), med(tail, 4), med(tail, 5), med(tail, -1),
+                      med(tail, 6), med(tail, 7));
         return std::string(b);
     };
     std::printf("{\"mode\": \"proposal-phases\", \"requests\": %d, \"calls\": %d, \"registered\": %d, "
