@@ -538,6 +538,11 @@ static_assert(kTTab * 80 == SBFT_VERIFY_QTAB_BYTES, "workspace Q-table stride (s
 #endif
 
 // 1. range checks and the on-curve check y^2 == x^3 - 3x + b (8 x 32 Montgomery domain)
+// The range part of verify_inputs_valid: r, s in [1, n), Qx, Qy in [0, p).
+SBFT_DEV bool verify_inputs_in_range(const fe& r, const fe& s, const fe& qx, const fe& qy) {
+    return !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) && fe_lt(qx, P256_P) &&
+           fe_lt(qy, P256_P);
+}
 SBFT_DEV bool verify_inputs_valid(const fe& r, const fe& s, const fe& qx, const fe& qy) {
     bool valid = !fe_is_zero_raw(r) && fe_lt(r, P256_N) && !fe_is_zero_raw(s) && fe_lt(s, P256_N) &&
                  fe_lt(qx, P256_P) && fe_lt(qy, P256_P);
@@ -815,6 +820,140 @@ SBFT_DEV void build_q_table_pair_w(const f29& qxm, const f29& qym, const f29& ac
     f29 x0, y0;
     pmul(x0, y0, qxm, kap, qym, kap);  // the base itself, divided by c
     st(0, x0, y0);
+}
+
+// build_q_table_pair_w on the four lanes of a quad (the wide half kernel, where lanes 2-3 of a
+// quad used to repeat the pair's steps): the same products on the same operands, so the same
+// table, in 39 product steps instead of 54. DBLU 3 steps (m^2 beside e^2 | x e); each co-Z
+// addition after the first 2 steps, the next addition's H^2 (= (w1 - X3)^2) riding on the spare
+// lane of this one's last step; the Z-ratio product tree and z c 4 steps; the conversion 2 steps
+// per entry, each entry's last two products in the next entry's steps, the base's in the last.
+template <class InvP, class Mark, class St, class Ld, class HSt, class HLd>
+SBFT_DEV void build_q_table_quad_w(const f29& qxm, const f29& qym, const f29& ac, const f29& cc, InvP inv_p, Mark mark,
+                                   St st, Ld ld, HSt hst, HLd hld) {
+    static_assert(kQTab == 8, "the Z-ratio product tree below is written for 7 ratios");
+    // lane j of the quad: a_j b_j
+    auto qm = [](const f29& a0, const f29& b0, const f29& a1, const f29& b1, const f29& a2, const f29& b2,
+                 const f29& a3, const f29& b3) {
+        f29 o;
+        f29_mul_ilp(o, f29_qsel<kQL3>(f29_qsel<kQL2>(f29_qsel<kQL1>(a0, a1), a2), a3),
+                    f29_qsel<kQL3>(f29_qsel<kQL2>(f29_qsel<kQL1>(b0, b1), b2), b3));
+        return o;
+    };
+    auto l0 = [](const f29& o) { return f29_qperm<0x00>(o); };
+    auto l1 = [](const f29& o) { return f29_qperm<0x55>(o); };
+    auto l2 = [](const f29& o) { return f29_qperm<0xAA>(o); };
+    auto l3 = [](const f29& o) { return f29_qperm<0xFF>(o); };
+    const f29 r2 = f29_const(C29_R2);
+    f29 dx, dy, cx, cy, z;
+    {  // DBLU as build_q_table_pair_w: x^2 | y^2, then e^2 | x e | m^2, then m (S - X2)
+        f29 o = qm(qxm, qxm, qym, qym, qxm, qxm, qym, qym);
+        const f29 b = l0(o), e = l1(o);
+        f29 m, t, l, m2;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) m.v[i] = 3 * (b.v[i] - ac.v[i]);  // |.| < 3 2^29.2 < 2^30.8
+        f29_normalize(m, m);                                          // M (N')
+        o = qm(e, e, qxm, e, m, m, m, m);
+        l = l0(o);
+        t = l1(o);
+        m2 = l2(o);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t.v[i] <<= 2;  // 4xE < 2^31
+        f29_normalize(cx, t);                       // S (N')
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t.v[i] = m2.v[i] - (cx.v[i] << 1);
+        f29_normalize(dx, t);                       // X2 (N')
+#pragma unroll
+        for (int i = 0; i < 9; ++i) l.v[i] <<= 2;  // 4L < 2^31
+        f29_normalize(l, l);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) l.v[i] <<= 1;  // 8L, |.| < 2^30.2
+        f29_normalize(cy, l);                       // 8L (N')
+        f29_sub(t, cx, dx);                         // S - X2, |.| < 2^29.3
+        f29_mul_ilp(m2, m, t);
+        f29_sub(t, m2, cy);
+        f29_normalize(dy, t);                       // Y2 (N')
+        f29_add(z, qym, qym);                       // Z = 2y
+    }
+    f29 h, c;  // this addition's H = dx - cx and H^2
+    f29_sub(h, dx, cx);
+    f29_mul_ilp(c, h, h);
+#pragma unroll 1
+    for (int k = 1; k < kQTab; ++k) {  // ZADDU: R^2 | W1 | W2, then A1 | C2 | the next H^2
+        f29 r, w1, w2, dd, t, u;
+        f29_sub(r, dy, cy);
+        f29 o = qm(r, r, dx, c, cx, c, r, r);
+        dd = l0(o);
+        w1 = l1(o);
+        w2 = l2(o);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t.v[i] = dd.v[i] - w1.v[i] - w2.v[i];
+        f29_normalize(cx, t);  // X3 (N')
+        f29_sub(u, w1, w2);
+        f29_sub(t, w1, cx);    // the next H (= w1 - X3)
+        o = qm(dy, u, r, t, t, t, t, t);
+        const f29 a1 = l0(o), c2 = l1(o);
+        c = l2(o);
+        f29_sub(u, c2, a1);
+        f29_normalize(cy, u);  // Y3 (N')
+        dx = w1;
+        dy = a1;
+        st(k, cx, cy);
+        hst(k - 1, h);
+        h = t;
+    }
+    f29 zt, zc;
+    {  // Z(T_7) = z h_1 ... h_7 and z c as a tree
+        f29 h0, h1, h2, h3, h4, h5, h6;
+        hld(0, h0);
+        hld(1, h1);
+        hld(2, h2);
+        hld(3, h3);
+        hld(4, h4);
+        hld(5, h5);
+        hld(6, h6);
+        f29 o = qm(z, h0, h1, h2, h3, h4, h5, h6);
+        const f29 p0 = l0(o), p1 = l1(o), p2 = l2(o), p3 = l3(o);
+        o = qm(p0, p1, p2, p3, p0, p1, p2, p3);
+        const f29 q0 = l0(o), q1 = l1(o);
+        o = qm(q0, q1, q1, cc, q0, q1, q1, cc);
+        zt = l0(o);
+        f29_mul_ilp(zc, q0, l1(o));
+    }
+    mark(0);  // co-Z chain done
+    f29 ic, lam, kap;
+    {
+        const fe zi = inv_p(f29_canon_plain(zc));
+        f29_mul_ilp(ic, f29_from_u256(zi), r2);  // 1 / (z c)
+    }
+    mark(1);  // inverted
+    {
+        const f29 o = qm(ic, cc, ic, zt, ic, cc, ic, zt);
+        lam = l0(o);  // 1 / z
+        kap = l1(o);  // 1 / c
+    }
+    // entry k: lam^2 | Y lam | lam h_k (the next lam) | (entry k+1's X lam^2 / c), then lam^2 / c |
+    // (entry k+1's Y lam^3 / c)
+    f29 px = kap, pyl = kap, pl2k = kap;  // entry k+1's X, Y lam, lam^2 / c (none before entry 7)
+#pragma unroll 1
+    for (int k = kQTab - 1; k >= 1; --k) {
+        f29 X, Y, hk;
+        ld(k, X, Y);
+        hld(k - 1, hk);
+        f29 o = qm(lam, lam, Y, lam, lam, hk, px, pl2k);
+        const f29 l2v = l0(o), yl = l1(o), nxt = l2(o), xo = l3(o);
+        o = qm(l2v, kap, pyl, pl2k, l2v, kap, pyl, pl2k);
+        if (k < kQTab - 1) st(k + 1, xo, l1(o));
+        pl2k = l0(o);
+        px = X;
+        pyl = yl;
+        lam = nxt;  // 1 / Z(T_{k-1})
+    }
+    {  // entry 1's products and the base itself, divided by c
+        const f29 o = qm(px, pl2k, pyl, pl2k, qxm, kap, qym, kap);
+        st(1, l0(o), l1(o));
+        st(0, l2(o), l3(o));
+    }
 }
 
 // 2-3. w = s^-1 of tuple t from the launch-wide Montgomery trick (p256_sinv_* kernels: 1,024
@@ -1540,6 +1679,24 @@ __device__ __constant__ static const u32 C29_B[9] = {0x1897bbfbu, 0x1cdf6229u, 0
                                                      0x0abf7212u, 0x1a06d110u, 0x17721d20u, 0x008600c3u};
 __device__ __constant__ static const u32 P256_PMN[8] = {0x039cdaaeu, 0x0c46353du, 0x58e8617bu, 0x43190553u, 0u, 0u, 0u, 0u};
 
+// verify_inputs_valid's curve equation in the ladders' radix-2^29 arithmetic (4 products against
+// the 8 x 32 form's 5): y^2 - (x^3 - 3x + b) == 0 mod p, with the bounds of the half kernel's
+// c = r^3 - 3r + b and of its square test (x, y < 2^256 in, as r there).
+SBFT_DEV bool q_on_curve29(const fe& qx, const fe& qy) {
+    const f29 r2c = f29_const(C29_R2), b = f29_const(C29_B);
+    f29 xm, ym, t2, t3, cv, yy, dd;
+    f29_mul_ilp(xm, f29_from_u256(qx), r2c);
+    f29_mul_ilp(ym, f29_from_u256(qy), r2c);
+    f29_sqr_ilp(t2, xm);
+    f29_mul_ilp(t3, t2, xm);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cv.v[i] = t3.v[i] - 3u * xm.v[i] + b.v[i];  // |limb| < 2^31
+    f29_normalize(cv, cv);                                                  // N'
+    f29_sqr_ilp(yy, ym);
+    f29_sub(dd, yy, cv);  // |limb| < 2^30, |.| < 2^259
+    return f29_zero_mod_p_any(dd);
+}
+
 SBFT_DEV void f29_sqr_n(f29& t, int k) {
 #pragma unroll 1
     for (int i = 0; i < k; ++i) f29_sqr_ilp(t, t);
@@ -1609,6 +1766,12 @@ SBFT_DEV void f29_inv_chain(f29& out, const f29& z) {
     out = t;
 }
 
+#ifndef SBFT_HALF_HPAIR
+#define SBFT_HALF_HPAIR 1  // wide form: the helper on lane pairs (s^-1 split over the pair)
+#endif
+#ifndef SBFT_HALF_QTAB_QUAD
+#define SBFT_HALF_QTAB_QUAD 1  // the wide form builds its tables on the quad (build_q_table_quad_w)
+#endif
 #ifndef SBFT_HALF_GAFF
 #define SBFT_HALF_GAFF 2  // the wide form's affine (v u1) G: 1 safegcd, 2 Fermat chain, 0 none (general join)
 #endif
@@ -1694,19 +1857,27 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
 
     if (threadIdx.x >= VT) {  // the helper wavefront (wave-uniform branch)
         const uint32_t lane = threadIdx.x - VT;
-        const bool mine = lane < (uint32_t)T;
-        const uint32_t slot = mine ? lane : 0u;
+        // The wide form (24 tuples) takes a lane pair per tuple: s^-1 split over the pair
+        // (inv::inv_mod_pair), the even lane publishing; the four-lane form a lane per tuple.
+        constexpr bool HP = QUAD && SBFT_HALF_HPAIR;
+        const uint32_t hslot = HP ? lane >> 1 : lane;
+        const bool hodd = HP && (lane & 1u) != 0;
+        const bool mine = hslot < (uint32_t)T;
+        const bool pub = mine && !hodd;
+        const uint32_t slot = mine ? hslot : 0u;
         const uint32_t tc = blockIdx.x * T + slot;
         const uint32_t ic = tc < n ? tc : n - 1;
         fe r, s, qx, qy;
         load_tuple(ic, r, s, qx, qy);
-        const bool valid = verify_inputs_valid(r, s, qx, qy);
+        const bool valid = HP ? verify_inputs_in_range(r, s, qx, qy) && q_on_curve29(qx, qy)
+                              : verify_inputs_valid(r, s, qx, qy);
         fe one = fe_zero();
         one.v[0] = 1;
         // barrier 1 waits for (v, w) only: s^-1, u2 and the reduction come first; the hash, u1 and
         // the comb sum are needed at barrier 2
         fe si, wm, u2;
-        inv::inv_mod(si.v, (valid ? s : one).v, dtab, false);  // plain s^-1 mod n
+        if constexpr (HP) inv::inv_mod_pair(si.v, (valid ? s : one).v, dtab, false, hodd);  // plain s^-1 mod n
+        else inv::inv_mod(si.v, (valid ? s : one).v, dtab, false);
         fn_mul(wm, si, fe_const(C_R2N));                          // s^-1 R
         fn_mul(u2, r, wm);
         fn_canon(u2, u2);
@@ -1740,13 +1911,13 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
             kb = one;
             vneg = false;
         }
-        if (mine) {
+        if (pub) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                hsc[k * T + lane] = ka.v[k];
-                hsc[(8 + k) * T + lane] = kb.v[k];
+                hsc[k * T + slot] = ka.v[k];
+                hsc[(8 + k) * T + slot] = kb.v[k];
             }
-            hsc[16 * T + lane] = (vneg ? 1u : 0u) | (fb ? 2u : 0u) | (valid ? 4u : 0u);
+            hsc[16 * T + slot] = (vneg ? 1u : 0u) | (fb ? 2u : 0u) | (valid ? 4u : 0u);
         }
         probe(2);
         __syncthreads();  // #1: the scalars are in hsc (the verify wavefronts' tables in qtab)
@@ -1766,7 +1937,7 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 e_raw.v[7 - k] = h[k];
-                if (mine) edig[k * T + lane] = h[k];
+                if (pub) edig[k * T + slot] = h[k];
             }
         } else {
             e_raw = load_be32(digest + 32ull * ic);
@@ -1819,14 +1990,14 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
         // square) is decided by the comparison itself; only an irregular end of the ladders
         // (Z_T or W_V = 0, never for an honest tuple) needs it, and the verify wavefronts compute
         // it for that case (the irregular branch of the final comparison)
-        if (mine) {
+        if (pub) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
-                gsum[k * T + lane] = g.x.v[k];
-                gsum[(9 + k) * T + lane] = g.y.v[k];
-                gsum[(18 + k) * T + lane] = g.z.v[k];
+                gsum[k * T + slot] = g.x.v[k];
+                gsum[(9 + k) * T + slot] = g.y.v[k];
+                gsum[(18 + k) * T + slot] = g.z.v[k];
             }
-            gsum[27 * T + lane] = (ginf ? 1u : 0u) | (gaff ? 2u : 0u);
+            gsum[27 * T + slot] = (ginf ? 1u : 0u) | (gaff ? 2u : 0u);
         }
         __syncthreads();  // #2: hand-over to the verify wavefronts
         probe_dump("helper sinv,hgcd,published,barrier1,hash,comb", lane == 0);
@@ -1887,23 +2058,23 @@ __global__ __launch_bounds__(kHalfThreads) void p256_verify_half_kernel(const ui
                 y.v[k] = qtab[(m * 18 + 9 + k) * 2 * T + col];
             }
         };
-        build_q_table_pair_w(
-            px, py, ac, cc, odd,
-            [&](const fe& zp) {  // both lanes of the pair hold the same z c
-                fe zi;
-                if (SBFT_HALF_INV_PAIR) inv::inv_mod_pair(zi.v, zp.v, dtab, true, odd);
-                else inv::inv_mod(zi.v, zp.v, dtab, true);
-                return zi;
-            },
-            [&](int m) { probe(m ? (m == 1 ? 2 : 3) : 1); }, st, ld,
-            [&](int m, const f29& h) {
+        auto inv_zc = [&](const fe& zp) {  // both lanes of the pair hold the same z c
+            fe zi;
+            if (SBFT_HALF_INV_PAIR) inv::inv_mod_pair(zi.v, zp.v, dtab, true, odd);
+            else inv::inv_mod(zi.v, zp.v, dtab, true);
+            return zi;
+        };
+        auto mark = [&](int m) { probe(m ? (m == 1 ? 2 : 3) : 1); };
+        auto hst = [&](int m, const f29& h) {
 #pragma unroll
-                for (int k = 0; k < 9; ++k) hrat[(m * 9 + k) * 2 * T + col] = h.v[k];
-            },
-            [&](int m, f29& h) {
+            for (int k = 0; k < 9; ++k) hrat[(m * 9 + k) * 2 * T + col] = h.v[k];
+        };
+        auto hld = [&](int m, f29& h) {
 #pragma unroll
-                for (int k = 0; k < 9; ++k) h.v[k] = hrat[(m * 9 + k) * 2 * T + col];
-            });
+            for (int k = 0; k < 9; ++k) h.v[k] = hrat[(m * 9 + k) * 2 * T + col];
+        };
+        if constexpr (QUAD && SBFT_HALF_QTAB_QUAD) build_q_table_quad_w(px, py, ac, cc, inv_zc, mark, st, ld, hst, hld);
+        else build_q_table_pair_w(px, py, ac, cc, odd, inv_zc, mark, st, ld, hst, hld);
     }
     probe(3);
     __syncthreads();  // #1: tables in qtab, the helper's scalars in hsc
