@@ -1777,7 +1777,29 @@ int sbft_gv_framed_overlapped(sbft_gv_ctx* ctx, const uint8_t* blob, size_t blob
         // the caller's host work (`during`: the full format check and the RequestInfo records),
         // as the one-slot path does it under its launch.
         const std::vector<Chunk> chunks = plan(ctx, n);
+        // SBFT_VP_TRACE: each share's pick-up and end on its worker, from the call's start
+        std::vector<std::array<TC::time_point, 2>> sh(trace ? chunks.size() + 1 : 0);
+        const TC::time_point ts = TC::now();
+        struct ShareTrace {
+            const std::vector<std::array<TC::time_point, 2>>& sh;
+            TC::time_point t0, ts;
+            ~ShareTrace() {
+                if (sh.empty()) return;
+                auto us = [](TC::time_point x, TC::time_point y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
+                fprintf(stderr, "vp-split start=%.1f", us(t0, ts));
+                for (size_t i = 0; i < sh.size(); ++i)
+                    fprintf(stderr, " s%zu=%.1f,%.1f", i, us(t0, sh[i][0]), us(t0, sh[i][1]));
+                fprintf(stderr, "\n");
+            }
+        } share_trace{sh, t0, ts};
         return for_each_device(ctx, chunks.size() + 1, [&](size_t i) -> int {
+            if (!sh.empty()) sh[i][0] = TC::now();
+            struct End {
+                std::array<TC::time_point, 2>* e;
+                ~End() {
+                    if (e) (*e)[1] = TC::now();
+                }
+            } end{sh.empty() ? nullptr : &sh[i]};
             if (i == 0) {
                 if (during) during();
                 return SBFT_GV_OK;
